@@ -1,0 +1,147 @@
+#!/usr/bin/env python3
+"""Regenerate the golden fixtures in tests/golden/ (run in the build container).
+
+Inputs (read-only, never copied as source):
+  * /root/reference/src/libressl-2.4.1/tests/aeadtests.txt — the reference's
+    EVP_AEAD KAT data file, copied verbatim as a data fixture;
+  * the vector tables inside the reference's tests/gcm128test.c:78-851,
+    tests/chachatest.c:36-221 and tests/poly1305test.c (NaCl / wrap / total
+    vectors) — only the numbers are extracted, re-encoded as JSON;
+  * oracle/_ref/libref.so — the reference compiled from its own sources
+    (oracle/Makefile); it seals TLS records with the t1_enc.c:832-975 framing
+    to give record-level vectors at sizes no reference test covers
+    (nothing pins 16 KiB / 1400 B / record level).
+
+Outputs: aeadtests.txt, gcm128_vectors.json, chacha_vectors.json,
+poly1305_vectors.json, records.json.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import re
+import shutil
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import pyoracle as po  # noqa: E402
+
+REFT = "/root/reference/src/libressl-2.4.1/tests"
+
+
+def c_byte_list(text: str) -> bytes:
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)   # drop C comments
+    vals = re.findall(r"0x([0-9a-fA-F]{1,2})|\b(\d+)\b", text)
+    return bytes(int(h, 16) if h else int(d) for h, d in vals)
+
+
+def parse_gcm128(path: str):
+    src = open(path).read()
+    body = src[src.index("gcm128_tests[] = {"):src.index("#define N_TESTS")]
+    cases = re.split(r"/\*\s*Test Case (\d+)\.\s*\*/", body)
+    out = []
+    for i in range(1, len(cases), 2):
+        num, txt = int(cases[i]), cases[i + 1]
+        f = {}
+        for name in ("K", "IV", "P", "A", "C", "T"):
+            m = re.search(r"\.%s\s*=\s*\{(.*?)\}" % name, txt, re.S)
+            f[name] = c_byte_list(m.group(1)) if m else b""
+        lens = {n: int(v) for n, v in re.findall(r"\.(\w+)_len\s*=\s*(\d+)", txt)}
+        rec = {"case": num}
+        for name in ("K", "IV", "P", "A", "C"):
+            n = lens.get(name, 0)
+            b = f[name][:n]
+            rec[name] = (b + bytes(n - len(b))).hex()   # `{0}` => zero-filled
+        rec["T"] = (f["T"] + bytes(16 - len(f["T"]))).hex()
+        out.append(rec)
+    return out
+
+
+def parse_chacha(path: str):
+    src = open(path).read()
+    body = src[src.index("chacha_test_vectors[] = {"):src.index("#define N_VECTORS")]
+    out = []
+    for m in re.finditer(r'\{\s*"([^"]*)",\s*\{(.*?)\},\s*\{(.*?)\},\s*(\d+),\s*\{(.*?)\},\s*\}',
+                         body, re.S):
+        desc, key, iv, n, ks = m.groups()
+        ks_b = c_byte_list(ks)
+        out.append({"desc": desc, "key": c_byte_list(key).hex(), "iv": c_byte_list(iv).hex(),
+                    "len": int(n), "out": (ks_b + bytes(int(n) - len(ks_b))).hex()})
+    return out
+
+
+def parse_poly1305(path: str):
+    src = open(path).read()
+    arrs = {}
+    for m in re.finditer(r"static const unsigned char (\w+)\[\d*\]\s*=\s*\{(.*?)\};", src, re.S):
+        arrs[m.group(1)] = c_byte_list(m.group(2)).hex()
+    return arrs
+
+
+def fill_bytes(seed: int, index: int, n: int) -> bytes:
+    """Counter-based SplitMix64 stream, identical to oracle_fill_bytes()."""
+    M = (1 << 64) - 1
+    st = (seed ^ (index * 0xD1B54A32D192ED03)) & M
+    out = bytearray()
+    w = 0
+    while len(out) < n:
+        w += 1
+        z = (st + w * 0x9E3779B97F4A7C15) & M
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        z ^= z >> 31
+        out += z.to_bytes(8, "little")
+    return bytes(out[:n])
+
+
+RECORD_SIZES = [0, 1, 13, 15, 16, 17, 31, 32, 63, 64, 65, 100, 255, 256, 1023, 1024,
+                1400, 4095, 4096, 16383, 16384]
+SEQS = [0, 1, 0xFF, 0x1FF, 0xFFFFFFFF, 0x0123456789ABCDEF, 0xFFFFFFFFFFFFFFFE]
+HEX_LIMIT = 300
+
+
+def make_records(ref: po.Reference):
+    recs = []
+    for kind_name, kind in po.KIND_BY_NAME.items():
+        for i, n in enumerate(RECORD_SIZES):
+            seed = 0x5EED1000 + 97 * kind + i
+            key = fill_bytes(seed, 1, po.KEY_LEN[kind])
+            fiv = fill_bytes(seed, 2, po.FIXED_IV_LEN[kind])
+            seq = SEQS[i % len(SEQS)]
+            rtype = 23 if i % 5 else 22
+            pt = fill_bytes(seed, 3, n)
+            ctx = ref.aead(kind, key)
+            body = po.tls_seal_record(ref, ctx, kind, fiv, seq, rtype, pt)
+            st, back = po.tls_open_record(ref, ctx, kind, fiv, seq, rtype, body)
+            assert st == 1 and back == pt
+            rec = {"aead": kind_name, "key": key.hex(), "fixed_iv": fiv.hex(), "seq": seq,
+                   "type": rtype, "version": 0x0303, "pt_seed": seed, "pt_len": n,
+                   "body_len": len(body), "body_sha256": hashlib.sha256(body).hexdigest()}
+            if len(body) <= HEX_LIMIT:
+                rec["body"] = body.hex()
+            recs.append(rec)
+    return recs
+
+
+def main():
+    os.makedirs(HERE, exist_ok=True)
+    shutil.copyfile(os.path.join(REFT, "aeadtests.txt"), os.path.join(HERE, "aeadtests.txt"))
+    json.dump(parse_gcm128(os.path.join(REFT, "gcm128test.c")),
+              open(os.path.join(HERE, "gcm128_vectors.json"), "w"), indent=1)
+    json.dump(parse_chacha(os.path.join(REFT, "chachatest.c")),
+              open(os.path.join(HERE, "chacha_vectors.json"), "w"), indent=1)
+    json.dump(parse_poly1305(os.path.join(REFT, "poly1305test.c")),
+              open(os.path.join(HERE, "poly1305_vectors.json"), "w"), indent=1)
+    po.build()
+    ref = po.Reference()
+    json.dump({"generator": "tests/golden/make_golden.py via oracle/_ref/libref.so",
+               "records": make_records(ref)},
+              open(os.path.join(HERE, "records.json"), "w"), indent=1)
+    print("golden fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()
