@@ -1,0 +1,152 @@
+/*
+ * tlsgpu.h — MI355X-native TLS 1.2 record bulk-cipher engine: batch C ABI.
+ *
+ * This is the GPU extension that sits beside the drop-in EVP_AEAD ABI
+ * (include/tlsgpu_evp.h).  It has no reference counterpart; it batches the
+ * per-record work that LibreSSL 2.4.1 does one record at a time in
+ *   tls1_enc() AEAD branch            ssl/t1_enc.c:832-975
+ *     -> EVP_AEAD_CTX_seal / _open    crypto/evp/evp_aead.c:89-144
+ *       -> aead_aes_gcm_seal / _open  crypto/evp/e_aes.c:1424-1510
+ *       -> aead_chacha20_poly1305_*   crypto/evp/e_chacha20poly1305.c:124-286
+ * and moves the per-direction key install of
+ *   tls1_change_cipher_state_aead()   ssl/t1_enc.c:444-495
+ * into a device session table.
+ *
+ * All pointers named d_* are device (HBM) pointers; the API never touches
+ * torch or any framework type.  Streams are hipStream_t passed as void*.
+ * Every function returns TLSGPU_OK (0) or a negative TLSGPU_E* code.
+ */
+#ifndef TLSGPU_H
+#define TLSGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TLSGPU_ABI_VERSION 1
+
+/* AEAD kinds (crypto/evp/e_aes.c:1512-1546, e_chacha20poly1305.c:288-322). */
+enum tlsgpu_aead {
+	TLSGPU_AES_128_GCM = 1,
+	TLSGPU_AES_256_GCM = 2,
+	TLSGPU_CHACHA20_POLY1305 = 3,	/* RFC 7539/7905, 12-byte nonce */
+	TLSGPU_CHACHA20_POLY1305_OLD = 4	/* draft-agl, 8-byte nonce */
+};
+
+/* Return codes. */
+#define TLSGPU_OK 0
+#define TLSGPU_EINVAL (-1)
+#define TLSGPU_ENOMEM (-2)
+#define TLSGPU_EHIP (-3)	/* HIP runtime error (no GPU, launch failure) */
+#define TLSGPU_ERANGE (-4)	/* session id / size out of range */
+
+/* Per-record status written by the batch calls (int32 per record).
+ *   >= 0  success: plaintext length (open) or record body length (seal)
+ *   TLSGPU_REC_BAD_MAC         tls1_enc returns -1 -> bad_record_mac alert
+ *                              (s3_pkt.c:450-462); the plaintext region
+ *                              [out, out+len) is zero-filled as
+ *                              EVP_AEAD_CTX_open does (evp_aead.c:137-143)
+ *   TLSGPU_REC_PUBLIC_INVALID  tls1_enc returns 0: record shorter than the
+ *                              explicit nonce or the tag (t1_enc.c:930,958)
+ */
+#define TLSGPU_REC_BAD_MAC (-1)
+#define TLSGPU_REC_PUBLIC_INVALID (-2)
+
+/* Largest record fragment the batch kernels accept (ciphertext bytes). */
+#define TLSGPU_MAX_RECORD (1u << 20)
+
+/* One TLS record, 32 bytes, device-resident array.
+ * open: in_off -> record fragment after the 5-byte header
+ *       (GCM: explicit nonce(8) || ct || tag(16); ChaCha: ct || tag(16)),
+ *       length = fragment length; plaintext written at out_off
+ *       (the TLS layer passes out = fragment + 8 for GCM, t1_enc.c:951-955).
+ * seal: in_off -> plaintext, length = plaintext length; the fragment
+ *       (explicit nonce || ct || tag) is written at out_off (t1_enc.c:898-914).
+ * seq is the record's 64-bit sequence number (read_sequence/write_sequence
+ * before tls1_record_sequence_increment, t1_enc.c:258-266,841-847). */
+typedef struct tlsgpu_record {
+	uint64_t in_off;
+	uint64_t out_off;
+	uint64_t seq;
+	uint32_t session;
+	uint32_t len_type;	/* bits 0-23: length; bits 24-31: content type */
+} tlsgpu_record;
+
+#define TLSGPU_LEN_TYPE(len, type) (((uint32_t)(type) << 24) | ((uint32_t)(len) & 0xFFFFFFu))
+
+/* Session parameters as installed at ChangeCipherSpec
+ * (t1_enc.c:444-495; nonce lengths from s3_lib.c cipher table). */
+typedef struct tlsgpu_session_params {
+	int32_t aead;			/* enum tlsgpu_aead */
+	uint32_t key_len;		/* 16 or 32 */
+	uint8_t key[32];
+	uint32_t fixed_iv_len;		/* 4 (GCM), 12 (ChaCha), 0 (ChaCha old) */
+	uint8_t fixed_iv[12];
+	uint32_t tag_len;		/* 0 = default 16 (EVP_AEAD_DEFAULT_TAG_LENGTH) */
+	uint16_t version;		/* s->version, e.g. 0x0303 */
+	uint16_t reserved;
+} tlsgpu_session_params;
+
+typedef struct tlsgpu_engine tlsgpu_engine;
+typedef struct tlsgpu_sessions tlsgpu_sessions;
+
+/* Engine = one GPU + one HIP stream + scratch pools. */
+int tlsgpu_engine_create(int device, tlsgpu_engine **out);
+void tlsgpu_engine_destroy(tlsgpu_engine *e);
+/* The engine's stream (hipStream_t) for callers that order their own work. */
+void *tlsgpu_engine_stream(tlsgpu_engine *e);
+int tlsgpu_engine_sync(tlsgpu_engine *e);
+/* Compute units of the engine's device (256 on MI355X). */
+int tlsgpu_engine_num_cus(tlsgpu_engine *e);
+
+/* Device session table with room for `capacity` sessions. */
+int tlsgpu_sessions_create(tlsgpu_engine *e, uint32_t capacity, tlsgpu_sessions **out);
+void tlsgpu_sessions_destroy(tlsgpu_sessions *t);
+/* Install n sessions (host params) at ids first..first+n-1.  Key schedule,
+ * H = E_K(0^128) and the GHASH power tables are derived on the device. */
+int tlsgpu_sessions_install(tlsgpu_sessions *t, uint32_t first, uint32_t n,
+    const tlsgpu_session_params *params);
+
+/* Batch record decrypt / encrypt (device-resident).  Records should be grouped
+ * by session for speed (a workgroup rebuilds its LDS GHASH table when the
+ * session changes); any order is correct.  d_status: int32 per record.
+ * Asynchronous on `stream` (NULL = engine stream). */
+int tlsgpu_open_batch(tlsgpu_sessions *t, const tlsgpu_record *d_recs, uint32_t n,
+    const uint8_t *d_in, uint8_t *d_out, int32_t *d_status, void *stream);
+int tlsgpu_seal_batch(tlsgpu_sessions *t, const tlsgpu_record *d_recs, uint32_t n,
+    const uint8_t *d_in, uint8_t *d_out, int32_t *d_status, void *stream);
+
+/* Deterministic synthetic bytes, counter-based SplitMix64 keyed by
+ * (seed, index0 + i) for each of n spans of span_len bytes at d_out + i*stride
+ * (same stream as the oracle's oracle_fill_bytes; used by bench/tests). */
+int tlsgpu_fill_synthetic(tlsgpu_engine *e, uint8_t *d_out, uint64_t stride,
+    uint32_t span_len, uint32_t n, uint64_t seed, uint64_t index0, void *stream);
+
+/* Device / pinned-host memory, copies and events on the engine's device, so
+ * callers need no other GPU runtime (the bench and tests use only these). */
+int tlsgpu_malloc(tlsgpu_engine *e, size_t bytes, void **d_ptr);
+int tlsgpu_free(tlsgpu_engine *e, void *d_ptr);
+int tlsgpu_host_alloc(tlsgpu_engine *e, size_t bytes, void **h_ptr);	/* pinned */
+int tlsgpu_host_free(tlsgpu_engine *e, void *h_ptr);
+/* Async copy in any direction (hipMemcpyDefault) on `stream` (NULL = engine). */
+int tlsgpu_memcpy(tlsgpu_engine *e, void *dst, const void *src, size_t bytes, void *stream);
+int tlsgpu_memset(tlsgpu_engine *e, void *d_ptr, int value, size_t bytes, void *stream);
+int tlsgpu_stream_create(tlsgpu_engine *e, void **stream);
+int tlsgpu_stream_destroy(tlsgpu_engine *e, void *stream);
+int tlsgpu_stream_sync(tlsgpu_engine *e, void *stream);
+int tlsgpu_event_create(tlsgpu_engine *e, void **event);
+int tlsgpu_event_destroy(tlsgpu_engine *e, void *event);
+int tlsgpu_event_record(tlsgpu_engine *e, void *event, void *stream);
+/* Milliseconds between two recorded events (waits for `end`). */
+int tlsgpu_event_elapsed_ms(tlsgpu_engine *e, void *start, void *end, float *ms);
+
+/* Human-readable last error of this thread. */
+const char *tlsgpu_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,359 @@
+"""talos_amd — MI355X-native TLS 1.2 record bulk-cipher engine (Python host side).
+
+The engine itself is ``libtlsgpu.so`` (HIP kernels for gfx950 behind a C ABI,
+``include/tlsgpu.h`` + the drop-in EVP_AEAD ABI ``include/tlsgpu_evp.h``).
+This module binds that ABI with ctypes and mirrors the reference's record-layer
+interface for the batch path:
+
+* :class:`Engine` / :class:`SessionTable` — device + device session table, the
+  state ``tls1_change_cipher_state_aead`` installs (ssl/t1_enc.c:444-495);
+* :func:`open_batch` / :func:`seal_batch` — ``tls1_enc(s, 0/1)``'s AEAD branch
+  (ssl/t1_enc.c:832-975) over a device-resident array of records;
+* :class:`EvpAead` — the per-call ``EVP_AEAD_CTX_*`` functions of
+  crypto/evp/evp_aead.c as exported by libtlsgpu.so.
+
+There is no CPU fallback: if the shared library is missing or no GPU is
+present the calls raise :class:`TlsGpuError`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIBPATH = os.path.join(HERE, "libtlsgpu.so")
+INCLUDE = os.path.join(ROOT, "include")
+
+AES_128_GCM, AES_256_GCM, CHACHA20_POLY1305, CHACHA20_POLY1305_OLD = 1, 2, 3, 4
+AEAD_NAMES = {"aes-128-gcm": AES_128_GCM, "aes-256-gcm": AES_256_GCM,
+              "chacha20-poly1305": CHACHA20_POLY1305,
+              "chacha20-poly1305-old": CHACHA20_POLY1305_OLD}
+KEY_LEN = {AES_128_GCM: 16, AES_256_GCM: 32, CHACHA20_POLY1305: 32, CHACHA20_POLY1305_OLD: 32}
+FIXED_IV_LEN = {AES_128_GCM: 4, AES_256_GCM: 4, CHACHA20_POLY1305: 12, CHACHA20_POLY1305_OLD: 0}
+EXPLICIT_NONCE_LEN = {AES_128_GCM: 8, AES_256_GCM: 8, CHACHA20_POLY1305: 0,
+                      CHACHA20_POLY1305_OLD: 0}
+TAG_LEN = 16
+
+REC_BAD_MAC = -1          # tls1_enc returns -1 (bad_record_mac)
+REC_PUBLIC_INVALID = -2   # tls1_enc returns 0
+MAX_RECORD = 1 << 20
+
+# tlsgpu_record (include/tlsgpu.h), 32 bytes
+RECORD_DTYPE = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("seq", "<u8"),
+                         ("session", "<u4"), ("len_type", "<u4")])
+assert RECORD_DTYPE.itemsize == 32
+
+
+class TlsGpuError(RuntimeError):
+    pass
+
+
+class _SessionParams(C.Structure):
+    _fields_ = [("aead", C.c_int32), ("key_len", C.c_uint32), ("key", C.c_uint8 * 32),
+                ("fixed_iv_len", C.c_uint32), ("fixed_iv", C.c_uint8 * 12),
+                ("tag_len", C.c_uint32), ("version", C.c_uint16), ("reserved", C.c_uint16)]
+
+
+@dataclass
+class SessionParams:
+    aead: int
+    key: bytes
+    fixed_iv: bytes = b""
+    tag_len: int = 0
+    version: int = 0x0303
+
+    def to_c(self) -> _SessionParams:
+        p = _SessionParams()
+        p.aead = self.aead
+        p.key_len = len(self.key)
+        C.memmove(p.key, self.key, len(self.key))
+        p.fixed_iv_len = len(self.fixed_iv)
+        if self.fixed_iv:
+            C.memmove(p.fixed_iv, self.fixed_iv, len(self.fixed_iv))
+        p.tag_len = self.tag_len
+        p.version = self.version
+        return p
+
+
+def build(quiet: bool = True) -> None:
+    """Compile libtlsgpu.so for gfx950 in-tree (hipcc)."""
+    subprocess.run(["make", "-C", HERE, "-j8"], check=True,
+                   stdout=subprocess.DEVNULL if quiet else None)
+
+
+_LIB = None
+
+
+def load_library(path: str = LIBPATH) -> C.CDLL:
+    """Load libtlsgpu.so; raise loudly when it is missing (no fallback)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise TlsGpuError(f"{path} not built: run `make -C talos_amd` (or __graft_entry__.build())")
+    lib = C.CDLL(path, mode=os.RTLD_LOCAL | os.RTLD_NOW)
+    vp, u32, u64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int
+    sigs = {
+        "tlsgpu_engine_create": (i32, [i32, C.POINTER(vp)]),
+        "tlsgpu_engine_destroy": (None, [vp]),
+        "tlsgpu_engine_stream": (vp, [vp]),
+        "tlsgpu_engine_sync": (i32, [vp]),
+        "tlsgpu_engine_num_cus": (i32, [vp]),
+        "tlsgpu_sessions_create": (i32, [vp, u32, C.POINTER(vp)]),
+        "tlsgpu_sessions_destroy": (None, [vp]),
+        "tlsgpu_sessions_install": (i32, [vp, u32, u32, vp]),
+        "tlsgpu_open_batch": (i32, [vp, vp, u32, vp, vp, vp, vp]),
+        "tlsgpu_seal_batch": (i32, [vp, vp, u32, vp, vp, vp, vp]),
+        "tlsgpu_fill_synthetic": (i32, [vp, vp, u64, u32, u32, u64, u64, vp]),
+        "tlsgpu_last_error": (C.c_char_p, []),
+        "tlsgpu_malloc": (i32, [vp, C.c_size_t, C.POINTER(vp)]),
+        "tlsgpu_free": (i32, [vp, vp]),
+        "tlsgpu_host_alloc": (i32, [vp, C.c_size_t, C.POINTER(vp)]),
+        "tlsgpu_host_free": (i32, [vp, vp]),
+        "tlsgpu_memcpy": (i32, [vp, vp, vp, C.c_size_t, vp]),
+        "tlsgpu_memset": (i32, [vp, vp, i32, C.c_size_t, vp]),
+        "tlsgpu_stream_create": (i32, [vp, C.POINTER(vp)]),
+        "tlsgpu_stream_destroy": (i32, [vp, vp]),
+        "tlsgpu_stream_sync": (i32, [vp, vp]),
+        "tlsgpu_event_create": (i32, [vp, C.POINTER(vp)]),
+        "tlsgpu_event_destroy": (i32, [vp, vp]),
+        "tlsgpu_event_record": (i32, [vp, vp, vp]),
+        "tlsgpu_event_elapsed_ms": (i32, [vp, vp, vp, C.POINTER(C.c_float)]),
+        "EVP_aead_aes_128_gcm": (vp, []),
+        "EVP_aead_aes_256_gcm": (vp, []),
+        "EVP_aead_chacha20_poly1305": (vp, []),
+        "EVP_aead_chacha20_poly1305_old": (vp, []),
+        "EVP_AEAD_key_length": (C.c_size_t, [vp]),
+        "EVP_AEAD_nonce_length": (C.c_size_t, [vp]),
+        "EVP_AEAD_max_overhead": (C.c_size_t, [vp]),
+        "EVP_AEAD_max_tag_len": (C.c_size_t, [vp]),
+        "EVP_AEAD_CTX_init": (i32, [vp, vp, vp, C.c_size_t, C.c_size_t, vp]),
+        "EVP_AEAD_CTX_cleanup": (None, [vp]),
+        "EVP_AEAD_CTX_seal": (i32, [vp, vp, C.POINTER(C.c_size_t), C.c_size_t, vp, C.c_size_t,
+                                    vp, C.c_size_t, vp, C.c_size_t]),
+        "EVP_AEAD_CTX_open": (i32, [vp, vp, C.POINTER(C.c_size_t), C.c_size_t, vp, C.c_size_t,
+                                    vp, C.c_size_t, vp, C.c_size_t]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load_library().tlsgpu_last_error()
+        raise TlsGpuError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+class Engine:
+    """One GPU + HIP stream (tlsgpu_engine_create)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = C.c_void_p()
+        _check(self.lib.tlsgpu_engine_create(device, C.byref(h)), "tlsgpu_engine_create")
+        self.handle = h
+        self.device = device
+
+    @property
+    def stream(self) -> int:
+        return self.lib.tlsgpu_engine_stream(self.handle)
+
+    @property
+    def num_cus(self) -> int:
+        return self.lib.tlsgpu_engine_num_cus(self.handle)
+
+    def sync(self) -> None:
+        _check(self.lib.tlsgpu_engine_sync(self.handle), "tlsgpu_engine_sync")
+
+    def sync_stream(self, stream: int | None = None) -> None:
+        _check(self.lib.tlsgpu_stream_sync(self.handle, stream), "tlsgpu_stream_sync")
+
+    def new_stream(self) -> int:
+        h = C.c_void_p()
+        _check(self.lib.tlsgpu_stream_create(self.handle, C.byref(h)), "tlsgpu_stream_create")
+        return h.value
+
+    def fill_synthetic(self, d_out: int, stride: int, span_len: int, n: int, seed: int,
+                       index0: int = 0, stream: int | None = None) -> None:
+        _check(self.lib.tlsgpu_fill_synthetic(self.handle, d_out, stride, span_len, n, seed,
+                                              index0, stream), "tlsgpu_fill_synthetic")
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.tlsgpu_engine_destroy(self.handle)
+            self.handle = None
+
+
+class DeviceBuffer:
+    """HBM buffer owned through the engine (tlsgpu_malloc); numpy on the host side."""
+
+    def __init__(self, engine: Engine, nbytes: int):
+        self.engine = engine
+        self.lib = engine.lib
+        self.nbytes = int(nbytes)
+        p = C.c_void_p()
+        _check(self.lib.tlsgpu_malloc(engine.handle, max(self.nbytes, 1), C.byref(p)),
+               "tlsgpu_malloc")
+        self.ptr = p.value
+
+    def upload(self, data, offset: int = 0, stream: int | None = None, sync: bool = True):
+        arr = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8)
+                                   if isinstance(data, (bytes, bytearray)) else data)
+        assert offset + arr.nbytes <= self.nbytes
+        _check(self.lib.tlsgpu_memcpy(self.engine.handle, self.ptr + offset,
+                                      arr.ctypes.data, arr.nbytes, stream), "tlsgpu_memcpy")
+        if sync:
+            self.engine.sync_stream(stream)
+
+    def download(self, nbytes: int | None = None, offset: int = 0,
+                 stream: int | None = None) -> np.ndarray:
+        nbytes = self.nbytes - offset if nbytes is None else nbytes
+        out = np.empty(nbytes, dtype=np.uint8)
+        _check(self.lib.tlsgpu_memcpy(self.engine.handle, out.ctypes.data, self.ptr + offset,
+                                      nbytes, stream), "tlsgpu_memcpy")
+        self.engine.sync_stream(stream)
+        return out
+
+    def fill(self, value: int, stream: int | None = None, sync: bool = True) -> None:
+        _check(self.lib.tlsgpu_memset(self.engine.handle, self.ptr, value, self.nbytes, stream),
+               "tlsgpu_memset")
+        if sync:
+            self.engine.sync_stream(stream)
+
+    def free(self) -> None:
+        if self.ptr and self.engine.handle:
+            self.lib.tlsgpu_free(self.engine.handle, self.ptr)
+        self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Event:
+    def __init__(self, engine: Engine):
+        self.engine = engine
+        h = C.c_void_p()
+        _check(engine.lib.tlsgpu_event_create(engine.handle, C.byref(h)), "tlsgpu_event_create")
+        self.handle = h.value
+
+    def record(self, stream: int | None = None) -> None:
+        _check(self.engine.lib.tlsgpu_event_record(self.engine.handle, self.handle, stream),
+               "tlsgpu_event_record")
+
+    def elapsed_ms(self, end: "Event") -> float:
+        ms = C.c_float()
+        _check(self.engine.lib.tlsgpu_event_elapsed_ms(self.engine.handle, self.handle,
+                                                       end.handle, C.byref(ms)),
+               "tlsgpu_event_elapsed_ms")
+        return ms.value
+
+    def close(self) -> None:
+        if self.handle:
+            self.engine.lib.tlsgpu_event_destroy(self.engine.handle, self.handle)
+            self.handle = None
+
+
+class SessionTable:
+    """Device session table (tlsgpu_sessions_create / _install)."""
+
+    def __init__(self, engine: Engine, capacity: int):
+        self.engine = engine
+        self.lib = engine.lib
+        h = C.c_void_p()
+        _check(self.lib.tlsgpu_sessions_create(engine.handle, capacity, C.byref(h)),
+               "tlsgpu_sessions_create")
+        self.handle = h
+        self.capacity = capacity
+
+    def install(self, first: int, params: list[SessionParams]) -> None:
+        arr = (_SessionParams * len(params))(*[p.to_c() for p in params])
+        _check(self.lib.tlsgpu_sessions_install(self.handle, first, len(params), arr),
+               "tlsgpu_sessions_install")
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.tlsgpu_sessions_destroy(self.handle)
+            self.handle = None
+
+
+def len_type(length: int, rtype: int) -> int:
+    return ((rtype & 0xFF) << 24) | (length & 0xFFFFFF)
+
+
+def open_batch(table: SessionTable, d_recs: int, n: int, d_in: int, d_out: int,
+               d_status: int, stream: int | None = None) -> None:
+    """Decrypt n device-resident records (tls1_enc(s, 0) per record)."""
+    _check(table.lib.tlsgpu_open_batch(table.handle, d_recs, n, d_in, d_out, d_status, stream),
+           "tlsgpu_open_batch")
+
+
+def seal_batch(table: SessionTable, d_recs: int, n: int, d_in: int, d_out: int,
+               d_status: int, stream: int | None = None) -> None:
+    """Encrypt n device-resident records (tls1_enc(s, 1) per record)."""
+    _check(table.lib.tlsgpu_seal_batch(table.handle, d_recs, n, d_in, d_out, d_status, stream),
+           "tlsgpu_seal_batch")
+
+
+class _EvpCtx(C.Structure):
+    _fields_ = [("aead", C.c_void_p), ("aead_state", C.c_void_p)]
+
+
+class EvpAead:
+    """EVP_AEAD_CTX over libtlsgpu.so's drop-in ABI (evp.h:1211-1315)."""
+
+    GETTERS = {AES_128_GCM: "EVP_aead_aes_128_gcm", AES_256_GCM: "EVP_aead_aes_256_gcm",
+               CHACHA20_POLY1305: "EVP_aead_chacha20_poly1305",
+               CHACHA20_POLY1305_OLD: "EVP_aead_chacha20_poly1305_old"}
+
+    def __init__(self, kind: int, key: bytes, tag_len: int = 0):
+        self.lib = load_library()
+        self.aead = getattr(self.lib, self.GETTERS[kind])()
+        self.ctx = _EvpCtx()
+        kb = (C.c_ubyte * max(len(key), 1)).from_buffer_copy(key or b"\0")
+        self.ok = self.lib.EVP_AEAD_CTX_init(C.byref(self.ctx), self.aead, kb, len(key),
+                                             tag_len, None)
+
+    @staticmethod
+    def _b(b: bytes):
+        return (C.c_ubyte * max(len(b), 1)).from_buffer_copy(b or b"\0") if b is not None else None
+
+    def _call(self, fn, nonce, data, ad, max_out):
+        out = (C.c_ubyte * max(max_out, 1))()
+        ol = C.c_size_t(12345)
+        ok = fn(C.byref(self.ctx), out, C.byref(ol), max_out, self._b(nonce), len(nonce),
+                self._b(data), len(data), self._b(ad), len(ad))
+        return ok, bytes(out)[:ol.value] if ok else bytes(out)[:max_out], ol.value
+
+    def seal(self, nonce: bytes, pt: bytes, ad: bytes, max_out: int | None = None):
+        max_out = len(pt) + 16 if max_out is None else max_out
+        return self._call(self.lib.EVP_AEAD_CTX_seal, nonce, pt, ad, max_out)
+
+    def open(self, nonce: bytes, ct: bytes, ad: bytes, max_out: int | None = None):
+        max_out = len(ct) if max_out is None else max_out
+        return self._call(self.lib.EVP_AEAD_CTX_open, nonce, ct, ad, max_out)
+
+    def cleanup(self) -> None:
+        self.lib.EVP_AEAD_CTX_cleanup(C.byref(self.ctx))
+
+
+def header_symbols() -> list[str]:
+    """Function names declared in include/*.h (the exported ABI)."""
+    import re
+    names = []
+    for h in ("tlsgpu.h", "tlsgpu_evp.h"):
+        src = open(os.path.join(INCLUDE, h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names += re.findall(r"\b((?:tlsgpu|EVP)_\w+)\s*\(", src)
+    return sorted(set(n for n in names if not n.startswith("TLSGPU")))

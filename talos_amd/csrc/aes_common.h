@@ -1,0 +1,62 @@
+// aes_common.h — AES S-box / T-table constants generated at compile time and
+// small device helpers shared by the HIP kernels.
+//
+// The tables are derived (GF(2^8) inverse via exp/log of generator 3 plus the
+// FIPS-197 affine map) rather than transcribed, and stored in the
+// little-endian column layout the kernels use: a state column is one uint32
+// with row 0 in bits 0-7, so Te0_le[x] = {2S, S, S, 3S} (bytes 0..3) is the
+// MixColumns image of row 0 (crypto/aes/aes_core.c:55-622 keeps the
+// big-endian equivalents Te0..Te3).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tg {
+
+struct ByteTable { uint8_t v[256]; };
+struct WordTable { uint32_t v[256]; };
+
+constexpr uint8_t xtime8(uint8_t x) {
+  return (uint8_t)((x << 1) ^ ((x & 0x80) ? 0x1b : 0));
+}
+
+constexpr ByteTable make_sbox() {
+  uint8_t exp[256] = {}, log[256] = {};
+  uint8_t p = 1;
+  for (int i = 0; i < 255; i++) {
+    exp[i] = p;
+    log[p] = (uint8_t)i;
+    p = (uint8_t)(p ^ xtime8(p));  // multiply by generator 3
+  }
+  ByteTable s{};
+  for (int x = 0; x < 256; x++) {
+    uint8_t inv = x ? exp[(255 - log[x]) % 255] : 0;
+    uint8_t r = inv;
+    for (int k = 1; k <= 4; k++) r ^= (uint8_t)((inv << k) | (inv >> (8 - k)));
+    s.v[x] = (uint8_t)(r ^ 0x63);
+  }
+  return s;
+}
+
+constexpr ByteTable kSbox = make_sbox();
+
+constexpr WordTable make_te0_le() {
+  WordTable t{};
+  for (int x = 0; x < 256; x++) {
+    uint32_t s = kSbox.v[x], s2 = xtime8((uint8_t)s), s3 = s2 ^ s;
+    t.v[x] = s2 | (s << 8) | (s << 16) | (s3 << 24);
+  }
+  return t;
+}
+
+constexpr WordTable kTe0 = make_te0_le();
+static_assert(kSbox.v[0] == 0x63 && kSbox.v[0x53] == 0xed, "AES S-box");
+
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int n) {
+  return (x << n) | (x >> (32 - n));
+}
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) {
+  return __builtin_amdgcn_perm(x, x, 0x00010203u);
+}
+
+}  // namespace tg

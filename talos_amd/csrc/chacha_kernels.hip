@@ -1,0 +1,393 @@
+// chacha_kernels.hip — ChaCha20-Poly1305 TLS record open/seal for gfx950.
+//
+// Replaces, per record, aead_chacha20_poly1305_seal/open
+// (crypto/evp/e_chacha20poly1305.c:124-286) driven by tls1_enc
+// (ssl/t1_enc.c:832-975): ChaCha20 with a 64-bit block counter
+// (chacha/chacha.c:59-77, chacha-merged.c:113-270), the Poly1305 one-time key
+// from block 0 (:178-180), Poly1305-donna with 26-bit limbs
+// (poly1305-donna.c:54-321) over the RFC 7539 layout
+// AD || pad16 || CT || pad16 || le64(|AD|) || le64(|CT|) (:182-190), or the
+// draft layout AD || le64(|AD|) || CT || le64(|CT|) for the 8-byte-nonce "old"
+// AEAD (:160-170).  Open computes the MAC over the ciphertext while it
+// decrypts and zero-fills the plaintext on a tag mismatch, which yields the
+// same output as the reference's MAC-then-decrypt order (:276-283).
+//
+// Mapping: one record per lane.  Poly1305 is a serial Horner chain with a
+// per-record key r, so a lane owns the whole chain (no cross-lane combine);
+// the VALU does ARX + 32x32->64 multiplies only, no LDS.
+#include "aes_common.h"
+#include "tlsgpu_internal.h"
+
+namespace tg {
+
+typedef __attribute__((address_space(4))) const uint32_t cu32c;
+
+__device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+#define CC_QR(a, b, c, d)            \
+  a += b; d = rotl32(d ^ a, 16);     \
+  c += d; b = rotl32(b ^ c, 12);     \
+  a += b; d = rotl32(d ^ a, 8);      \
+  c += d; b = rotl32(b ^ c, 7);
+
+__device__ __forceinline__ void chacha_block(const uint32_t in[16], uint32_t x[16]) {
+#pragma unroll
+  for (int i = 0; i < 16; i++) x[i] = in[i];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    CC_QR(x[0], x[4], x[8], x[12]);
+    CC_QR(x[1], x[5], x[9], x[13]);
+    CC_QR(x[2], x[6], x[10], x[14]);
+    CC_QR(x[3], x[7], x[11], x[15]);
+    CC_QR(x[0], x[5], x[10], x[15]);
+    CC_QR(x[1], x[6], x[11], x[12]);
+    CC_QR(x[2], x[7], x[8], x[13]);
+    CC_QR(x[3], x[4], x[9], x[14]);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; i++) x[i] += in[i];
+}
+
+struct Poly {
+  uint32_t r0, r1, r2, r3, r4, s1, s2, s3, s4;
+  uint32_t h0, h1, h2, h3, h4;
+  uint32_t pad0, pad1, pad2, pad3;
+};
+
+__device__ __forceinline__ void poly_init(Poly& p, const uint32_t k[8]) {
+  // clamp r (poly1305-donna.c:59-64) on the key words
+  uint32_t t0 = k[0], t1 = k[1], t2 = k[2], t3 = k[3];
+  p.r0 = t0 & 0x3ffffff;
+  p.r1 = ((t0 >> 26) | (t1 << 6)) & 0x3ffff03;
+  p.r2 = ((t1 >> 20) | (t2 << 12)) & 0x3ffc0ff;
+  p.r3 = ((t2 >> 14) | (t3 << 18)) & 0x3f03fff;
+  p.r4 = (t3 >> 8) & 0x00fffff;
+  p.s1 = p.r1 * 5; p.s2 = p.r2 * 5; p.s3 = p.r3 * 5; p.s4 = p.r4 * 5;
+  p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0;
+  p.pad0 = k[4]; p.pad1 = k[5]; p.pad2 = k[6]; p.pad3 = k[7];
+}
+
+// One 16-byte block m (LE words) with the 2^128 bit given by hibit.
+__device__ __forceinline__ void poly_block(Poly& p, uint32_t m0, uint32_t m1, uint32_t m2,
+                                           uint32_t m3, uint32_t hibit) {
+  uint32_t h0 = p.h0 + (m0 & 0x3ffffff);
+  uint32_t h1 = p.h1 + (((m0 >> 26) | (m1 << 6)) & 0x3ffffff);
+  uint32_t h2 = p.h2 + (((m1 >> 20) | (m2 << 12)) & 0x3ffffff);
+  uint32_t h3 = p.h3 + (((m2 >> 14) | (m3 << 18)) & 0x3ffffff);
+  uint32_t h4 = p.h4 + ((m3 >> 8) | hibit);
+  uint64_t d0 = (uint64_t)h0 * p.r0 + (uint64_t)h1 * p.s4 + (uint64_t)h2 * p.s3 +
+                (uint64_t)h3 * p.s2 + (uint64_t)h4 * p.s1;
+  uint64_t d1 = (uint64_t)h0 * p.r1 + (uint64_t)h1 * p.r0 + (uint64_t)h2 * p.s4 +
+                (uint64_t)h3 * p.s3 + (uint64_t)h4 * p.s2;
+  uint64_t d2 = (uint64_t)h0 * p.r2 + (uint64_t)h1 * p.r1 + (uint64_t)h2 * p.r0 +
+                (uint64_t)h3 * p.s4 + (uint64_t)h4 * p.s3;
+  uint64_t d3 = (uint64_t)h0 * p.r3 + (uint64_t)h1 * p.r2 + (uint64_t)h2 * p.r1 +
+                (uint64_t)h3 * p.r0 + (uint64_t)h4 * p.s4;
+  uint64_t d4 = (uint64_t)h0 * p.r4 + (uint64_t)h1 * p.r3 + (uint64_t)h2 * p.r2 +
+                (uint64_t)h3 * p.r1 + (uint64_t)h4 * p.r0;
+  uint32_t c = (uint32_t)(d0 >> 26); h0 = (uint32_t)d0 & 0x3ffffff;
+  d1 += c; c = (uint32_t)(d1 >> 26); h1 = (uint32_t)d1 & 0x3ffffff;
+  d2 += c; c = (uint32_t)(d2 >> 26); h2 = (uint32_t)d2 & 0x3ffffff;
+  d3 += c; c = (uint32_t)(d3 >> 26); h3 = (uint32_t)d3 & 0x3ffffff;
+  d4 += c; c = (uint32_t)(d4 >> 26); h4 = (uint32_t)d4 & 0x3ffffff;
+  h0 += c * 5; c = h0 >> 26; h0 &= 0x3ffffff;
+  h1 += c;
+  p.h0 = h0; p.h1 = h1; p.h2 = h2; p.h3 = h3; p.h4 = h4;
+}
+
+// poly1305-donna.c:231-321: full carry, conditional subtract, + pad.
+__device__ __forceinline__ void poly_finish(const Poly& p, uint32_t mac[4]) {
+  uint32_t h0 = p.h0, h1 = p.h1, h2 = p.h2, h3 = p.h3, h4 = p.h4, c;
+  c = h1 >> 26; h1 &= 0x3ffffff;
+  h2 += c; c = h2 >> 26; h2 &= 0x3ffffff;
+  h3 += c; c = h3 >> 26; h3 &= 0x3ffffff;
+  h4 += c; c = h4 >> 26; h4 &= 0x3ffffff;
+  h0 += c * 5; c = h0 >> 26; h0 &= 0x3ffffff;
+  h1 += c;
+  uint32_t g0 = h0 + 5; c = g0 >> 26; g0 &= 0x3ffffff;
+  uint32_t g1 = h1 + c; c = g1 >> 26; g1 &= 0x3ffffff;
+  uint32_t g2 = h2 + c; c = g2 >> 26; g2 &= 0x3ffffff;
+  uint32_t g3 = h3 + c; c = g3 >> 26; g3 &= 0x3ffffff;
+  uint32_t g4 = h4 + c - (1u << 26);
+  uint32_t mask = (g4 >> 31) - 1;
+  h0 = (h0 & ~mask) | (g0 & mask);
+  h1 = (h1 & ~mask) | (g1 & mask);
+  h2 = (h2 & ~mask) | (g2 & mask);
+  h3 = (h3 & ~mask) | (g3 & mask);
+  h4 = (h4 & ~mask) | (g4 & mask);
+  uint32_t w0 = h0 | (h1 << 26), w1 = (h1 >> 6) | (h2 << 20), w2 = (h2 >> 12) | (h3 << 14),
+           w3 = (h3 >> 18) | (h4 << 8);
+  uint64_t f = (uint64_t)w0 + p.pad0; mac[0] = (uint32_t)f;
+  f = (uint64_t)w1 + p.pad1 + (f >> 32); mac[1] = (uint32_t)f;
+  f = (uint64_t)w2 + p.pad2 + (f >> 32); mac[2] = (uint32_t)f;
+  f = (uint64_t)w3 + p.pad3 + (f >> 32); mac[3] = (uint32_t)f;
+}
+
+// Byte-stream Poly1305 (poly1305-donna.c:176-212 buffering) for the draft
+// layout, whose segments are not 16-byte aligned.
+struct PolyStream {
+  uint32_t buf[4];
+  uint32_t fill;
+};
+__device__ __forceinline__ void ps_byte(Poly& p, PolyStream& s, uint32_t b) {
+  uint32_t w = s.fill >> 2, sh = 8 * (s.fill & 3);
+  if (w == 0) s.buf[0] |= b << sh;
+  else if (w == 1) s.buf[1] |= b << sh;
+  else if (w == 2) s.buf[2] |= b << sh;
+  else s.buf[3] |= b << sh;
+  if (++s.fill == 16) {
+    poly_block(p, s.buf[0], s.buf[1], s.buf[2], s.buf[3], 1u << 24);
+    s.buf[0] = s.buf[1] = s.buf[2] = s.buf[3] = 0;
+    s.fill = 0;
+  }
+}
+__device__ __forceinline__ void ps_u64(Poly& p, PolyStream& s, uint64_t v) {
+  for (int k = 0; k < 8; k++) ps_byte(p, s, (uint32_t)(v >> (8 * k)) & 0xFF);
+}
+__device__ __forceinline__ void ps_final(Poly& p, PolyStream& s) {
+  if (s.fill) {  // 0x01 terminator, zero pad, no 2^128 bit (:214-230)
+    uint32_t w = s.fill >> 2, bit = 1u << (8 * (s.fill & 3));
+    s.buf[0] |= w == 0 ? bit : 0u;
+    s.buf[1] |= w == 1 ? bit : 0u;
+    s.buf[2] |= w == 2 ? bit : 0u;
+    s.buf[3] |= w == 3 ? bit : 0u;
+    poly_block(p, s.buf[0], s.buf[1], s.buf[2], s.buf[3], 0);
+  }
+}
+
+struct CcRec {
+  const uint8_t* src;
+  uint8_t* dst;
+  const uint8_t* tag_in;
+  uint8_t* tag_out;
+  const uint8_t* aad_ptr;  // raw mode
+  uint32_t ad[4];          // TLS mode 13-byte AAD (LE words, zero padded)
+  uint32_t ad_len;
+  uint32_t n;
+  uint32_t st[16];         // ChaCha input block with counter 0
+  bool old;
+  uint64_t zero_len;
+  int32_t ok_status;
+  bool valid;
+};
+
+template <bool SEAL>
+__device__ void cc_record(const CcRec& rc, uint32_t tag_len, int32_t* status_slot) {
+  uint32_t st[16], ks[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) st[i] = rc.st[i];
+  chacha_block(st, ks);  // counter 0 block -> one-time Poly1305 key
+  Poly p;
+  poly_init(p, ks);
+  PolyStream ps = {{0, 0, 0, 0}, 0};
+  const uint32_t n = rc.n;
+
+  // AD
+  if (!rc.old) {
+    for (uint32_t o = 0; o < rc.ad_len; o += 16) {
+      uint32_t b[4] = {0, 0, 0, 0};
+      if (rc.aad_ptr) {
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+          if (o + k < rc.ad_len) b[k >> 2] |= (uint32_t)rc.aad_ptr[o + k] << (8 * (k & 3));
+      } else {
+        b[0] = rc.ad[0]; b[1] = rc.ad[1]; b[2] = rc.ad[2]; b[3] = rc.ad[3];
+      }
+      poly_block(p, b[0], b[1], b[2], b[3], 1u << 24);  // pad16
+    }
+  } else {
+    for (uint32_t o = 0; o < rc.ad_len; o++)
+      ps_byte(p, ps, rc.aad_ptr ? rc.aad_ptr[o] : (rc.ad[o >> 2] >> (8 * (o & 3))) & 0xFF);
+    ps_u64(p, ps, rc.ad_len);
+  }
+
+  const bool aligned = ((((uintptr_t)rc.src) | ((uintptr_t)rc.dst)) & 15) == 0;
+  // data: counter 1.. (64-bit counter in words 12-13, chacha-merged.c:230-236)
+  uint64_t ctr = ((uint64_t)st[13] << 32) | st[12];
+  for (uint32_t off = 0; off < n; off += 64) {
+    ctr += 1;
+    st[12] = (uint32_t)ctr;
+    st[13] = (uint32_t)(ctr >> 32);
+    chacha_block(st, ks);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      uint32_t o = off + 16 * q;
+      if (o >= n) break;
+      uint32_t nb = min(16u, n - o);
+      uint32_t in[4] = {0, 0, 0, 0};
+      if (nb == 16 && aligned) {
+        uint4 t = *reinterpret_cast<const uint4*>(rc.src + o);
+        in[0] = t.x; in[1] = t.y; in[2] = t.z; in[3] = t.w;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+          if ((uint32_t)k < nb) in[k >> 2] |= (uint32_t)rc.src[o + k] << (8 * (k & 3));
+      }
+      uint32_t ob[4] = {in[0] ^ ks[4 * q], in[1] ^ ks[4 * q + 1], in[2] ^ ks[4 * q + 2],
+                        in[3] ^ ks[4 * q + 3]};
+      if (nb < 16) {  // zero the pad bytes so the MAC sees pad16 zeros
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+          int32_t b = (int32_t)nb - 4 * w;
+          uint32_t keep = b >= 4 ? 0xFFFFFFFFu : (b <= 0 ? 0u : ((1u << (8 * b)) - 1u));
+          ob[w] &= keep;
+        }
+      }
+      if (nb == 16 && aligned) {
+        *reinterpret_cast<uint4*>(rc.dst + o) = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+          if ((uint32_t)k < nb) rc.dst[o + k] = (uint8_t)(ob[k >> 2] >> (8 * (k & 3)));
+      }
+      const uint32_t* c = SEAL ? ob : in;
+      if (!rc.old) {
+        poly_block(p, c[0], c[1], c[2], c[3], 1u << 24);
+      } else {
+        for (uint32_t k = 0; k < nb; k++) ps_byte(p, ps, (c[k >> 2] >> (8 * (k & 3))) & 0xFF);
+      }
+    }
+  }
+  if (!rc.old) {
+    poly_block(p, rc.ad_len, 0, n, 0, 1u << 24);  // le64(ad_len) || le64(ct_len)
+  } else {
+    ps_u64(p, ps, n);
+    ps_final(p, ps);
+  }
+  uint32_t mac[4];
+  poly_finish(p, mac);
+  if (SEAL) {
+    for (uint32_t k = 0; k < tag_len; k++) rc.tag_out[k] = (uint8_t)(mac[k >> 2] >> (8 * (k & 3)));
+    *status_slot = rc.ok_status;
+  } else {
+    uint32_t diff = 0;
+    for (uint32_t k = 0; k < tag_len; k++)
+      diff |= rc.tag_in[k] ^ ((mac[k >> 2] >> (8 * (k & 3))) & 0xFF);
+    if (diff) {
+      for (uint64_t o = 0; o < rc.zero_len; o++) rc.dst[o] = 0;
+      *status_slot = TLSGPU_REC_BAD_MAC;
+    } else {
+      *status_slot = rc.ok_status;
+    }
+  }
+}
+
+__device__ __forceinline__ void cc_state(uint32_t st[16], const DevSession* S) {
+  st[0] = 0x61707865u; st[1] = 0x3320646eu; st[2] = 0x79622d32u; st[3] = 0x6b206574u;
+  const uint32_t* kw = reinterpret_cast<const uint32_t*>(S->chacha_key);
+#pragma unroll
+  for (int i = 0; i < 8; i++) st[4 + i] = kw[i];
+}
+
+template <bool SEAL, bool RAW>
+__global__ __launch_bounds__(256) void chacha_batch_kernel(BatchArgs a) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= a.n) return;
+  CcRec rc;
+  int32_t* slot = a.status + r;
+  const DevSession* S;
+  uint32_t tag_len;
+  if (RAW) {
+    const RawJob j = reinterpret_cast<const RawJob*>(a.descs)[r];
+    S = a.sessions + j.session;
+    uint32_t kind = S->kind;
+    if (kind != TLSGPU_CHACHA20_POLY1305 && kind != TLSGPU_CHACHA20_POLY1305_OLD) return;
+    tag_len = S->tag_len;
+    rc.old = kind == TLSGPU_CHACHA20_POLY1305_OLD;
+    const uint8_t* nonce = (const uint8_t*)j.nonce;
+    cc_state(rc.st, S);
+    if (!rc.old) {  // ctr = LE32(nonce[0..3]) << 32 ; iv = nonce + 4
+      rc.st[12] = 0;
+      rc.st[13] = ld_le32(nonce);
+      rc.st[14] = ld_le32(nonce + 4);
+      rc.st[15] = ld_le32(nonce + 8);
+    } else {
+      rc.st[12] = 0; rc.st[13] = 0;
+      rc.st[14] = ld_le32(nonce);
+      rc.st[15] = ld_le32(nonce + 4);
+    }
+    rc.src = (const uint8_t*)j.in;
+    rc.dst = (uint8_t*)j.out;
+    rc.aad_ptr = (const uint8_t*)j.aad;
+    rc.ad_len = j.aad_len;
+    if (SEAL) {
+      rc.n = j.in_len;
+      rc.tag_out = rc.dst + j.in_len;
+      rc.ok_status = (int32_t)(j.in_len + tag_len);
+    } else {
+      rc.n = j.in_len - tag_len;
+      rc.tag_in = rc.src + rc.n;
+      rc.ok_status = (int32_t)rc.n;
+    }
+    rc.zero_len = j.max_out;
+  } else {
+    const tlsgpu_record d = reinterpret_cast<const tlsgpu_record*>(a.descs)[r];
+    S = a.sessions + d.session;
+    uint32_t kind = S->kind;
+    if (kind != TLSGPU_CHACHA20_POLY1305 && kind != TLSGPU_CHACHA20_POLY1305_OLD) return;
+    tag_len = S->tag_len;
+    rc.old = kind == TLSGPU_CHACHA20_POLY1305_OLD;
+    uint32_t len = d.len_type & 0xFFFFFFu, type = d.len_type >> 24;
+    const uint8_t* ip = a.in + d.in_off;
+    uint8_t* op = a.out + d.out_off;
+    if (SEAL) {
+      rc.n = len;
+      rc.src = ip;
+      rc.dst = op;
+      rc.tag_out = op + len;
+      rc.ok_status = (int32_t)(len + tag_len);
+      rc.zero_len = 0;
+    } else {
+      if (len < tag_len) {  // t1_enc.c:958-959 (no explicit nonce for ChaCha)
+        *slot = TLSGPU_REC_PUBLIC_INVALID;
+        return;
+      }
+      rc.n = len - tag_len;
+      rc.src = ip;
+      rc.dst = op;
+      rc.tag_in = ip + rc.n;
+      rc.ok_status = (int32_t)rc.n;
+      rc.zero_len = rc.n;
+    }
+    // nonce: RFC 7905 fixed(12) XOR (0^4 || seq) ; old: fixed(0) || seq
+    uint32_t sq_hi = bswap32((uint32_t)(d.seq >> 32)), sq_lo = bswap32((uint32_t)d.seq);
+    cc_state(rc.st, S);
+    const uint32_t* fx = reinterpret_cast<const uint32_t*>(S->fixed_nonce);
+    rc.st[12] = 0;
+    if (!rc.old) {
+      rc.st[13] = fx[0];
+      rc.st[14] = fx[1] ^ sq_hi;
+      rc.st[15] = fx[2] ^ sq_lo;
+    } else {
+      rc.st[13] = 0;
+      rc.st[14] = sq_hi;
+      rc.st[15] = sq_lo;
+    }
+    uint32_t v = S->version;
+    rc.aad_ptr = nullptr;
+    rc.ad_len = 13;
+    rc.ad[0] = sq_hi;
+    rc.ad[1] = sq_lo;
+    rc.ad[2] = type | (((v >> 8) & 0xFF) << 8) | ((v & 0xFF) << 16) | (((rc.n >> 8) & 0xFF) << 24);
+    rc.ad[3] = rc.n & 0xFF;
+  }
+  cc_record<SEAL>(rc, tag_len, slot);
+}
+
+int launch_chacha(const BatchArgs& a, bool seal, bool raw, int groups, hipStream_t s) {
+  (void)groups;
+  if (a.n == 0) return 0;
+  dim3 grid((a.n + 255) / 256), block(256);
+  if (seal) {
+    if (raw) hipLaunchKernelGGL((chacha_batch_kernel<true, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((chacha_batch_kernel<true, false>), grid, block, 0, s, a);
+  } else {
+    if (raw) hipLaunchKernelGGL((chacha_batch_kernel<false, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((chacha_batch_kernel<false, false>), grid, block, 0, s, a);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace tg

@@ -1,0 +1,630 @@
+// engine.cpp — host side of libtlsgpu.so: the batch C ABI (include/tlsgpu.h)
+// and the drop-in EVP_AEAD ABI (include/tlsgpu_evp.h).
+//
+// The EVP_AEAD functions keep LibreSSL 2.4.1's argument checks and error
+// behaviour (crypto/evp/evp_aead.c:50-144, e_aes.c:1372-1510,
+// e_chacha20poly1305.c:52-286): same return values, ERR queue entries when a
+// LibreSSL libcrypto is present in the process (weak ERR_put_error), zero-fill
+// of out[0..max_out_len) and *out_len = 0 on every failure.  The cipher work of
+// each call runs on the GPU as a one-record "raw" batch; this library contains
+// no CPU cipher path.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/tlsgpu.h"
+#include "../../include/tlsgpu_evp.h"
+#include "tlsgpu_internal.h"
+
+using namespace tg;
+
+// ---------------------------------------------------------------------------
+// error reporting
+static thread_local char g_err[256] = "";
+
+static int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+#define HIPCHK(x)                                                              \
+  do {                                                                         \
+    hipError_t _e = (x);                                                       \
+    if (_e != hipSuccess)                                                      \
+      return fail(TLSGPU_EHIP, "%s: %s", #x, hipGetErrorString(_e));          \
+  } while (0)
+
+extern "C" const char* tlsgpu_last_error(void) { return g_err; }
+
+// ---------------------------------------------------------------------------
+// engine / sessions
+struct tlsgpu_engine {
+  int device;
+  hipStream_t stream;
+  int num_cus;
+};
+
+struct tlsgpu_sessions {
+  tlsgpu_engine* eng;
+  uint32_t capacity;
+  DevSession* d_sess;
+  DevGcmTables* d_gcm;
+  std::vector<int32_t> kinds;  // host mirror of installed kinds
+  bool have[5];                // any session of kind k installed
+};
+
+extern "C" int tlsgpu_engine_create(int device, tlsgpu_engine** out) {
+  if (!out) return fail(TLSGPU_EINVAL, "null out");
+  *out = nullptr;
+  int count = 0;
+  HIPCHK(hipGetDeviceCount(&count));
+  if (device < 0 || device >= count)
+    return fail(TLSGPU_EINVAL, "device %d out of range (%d GPUs)", device, count);
+  HIPCHK(hipSetDevice(device));
+  auto* e = new (std::nothrow) tlsgpu_engine();
+  if (!e) return fail(TLSGPU_ENOMEM, "engine alloc");
+  e->device = device;
+  HIPCHK(hipDeviceGetAttribute(&e->num_cus, hipDeviceAttributeMultiprocessorCount, device));
+  HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+  *out = e;
+  return TLSGPU_OK;
+}
+
+extern "C" void tlsgpu_engine_destroy(tlsgpu_engine* e) {
+  if (!e) return;
+  hipSetDevice(e->device);
+  hipStreamSynchronize(e->stream);
+  hipStreamDestroy(e->stream);
+  delete e;
+}
+
+extern "C" void* tlsgpu_engine_stream(tlsgpu_engine* e) { return e ? (void*)e->stream : nullptr; }
+
+extern "C" int tlsgpu_engine_sync(tlsgpu_engine* e) {
+  if (!e) return fail(TLSGPU_EINVAL, "null engine");
+  HIPCHK(hipSetDevice(e->device));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return TLSGPU_OK;
+}
+
+extern "C" int tlsgpu_engine_num_cus(tlsgpu_engine* e) { return e ? e->num_cus : 0; }
+
+extern "C" int tlsgpu_sessions_create(tlsgpu_engine* e, uint32_t capacity, tlsgpu_sessions** out) {
+  if (!e || !out || capacity == 0) return fail(TLSGPU_EINVAL, "bad arguments");
+  *out = nullptr;
+  HIPCHK(hipSetDevice(e->device));
+  auto* t = new (std::nothrow) tlsgpu_sessions();
+  if (!t) return fail(TLSGPU_ENOMEM, "sessions alloc");
+  t->eng = e;
+  t->capacity = capacity;
+  t->kinds.assign(capacity, 0);
+  memset(t->have, 0, sizeof(t->have));
+  if (hipMalloc(&t->d_sess, sizeof(DevSession) * (size_t)capacity) != hipSuccess ||
+      hipMalloc(&t->d_gcm, sizeof(DevGcmTables) * (size_t)capacity) != hipSuccess) {
+    hipFree(t->d_sess);
+    delete t;
+    return fail(TLSGPU_ENOMEM, "device session table (%u sessions)", capacity);
+  }
+  HIPCHK(hipMemsetAsync(t->d_sess, 0, sizeof(DevSession) * (size_t)capacity, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  *out = t;
+  return TLSGPU_OK;
+}
+
+extern "C" void tlsgpu_sessions_destroy(tlsgpu_sessions* t) {
+  if (!t) return;
+  hipSetDevice(t->eng->device);
+  hipStreamSynchronize(t->eng->stream);
+  hipFree(t->d_sess);
+  hipFree(t->d_gcm);
+  delete t;
+}
+
+static bool valid_params(const tlsgpu_session_params& p) {
+  uint32_t tag = p.tag_len == 0 ? 16 : p.tag_len;
+  if (tag > 16 || p.fixed_iv_len > 12) return false;
+  switch (p.aead) {
+    case TLSGPU_AES_128_GCM: return p.key_len == 16;
+    case TLSGPU_AES_256_GCM:
+    case TLSGPU_CHACHA20_POLY1305:
+    case TLSGPU_CHACHA20_POLY1305_OLD: return p.key_len == 32;
+  }
+  return false;
+}
+
+extern "C" int tlsgpu_sessions_install(tlsgpu_sessions* t, uint32_t first, uint32_t n,
+                                       const tlsgpu_session_params* params) {
+  if (!t || (!params && n)) return fail(TLSGPU_EINVAL, "bad arguments");
+  if ((uint64_t)first + n > t->capacity)
+    return fail(TLSGPU_ERANGE, "sessions [%u, %u) exceed capacity %u", first, first + n,
+                t->capacity);
+  for (uint32_t i = 0; i < n; i++)
+    if (!valid_params(params[i])) return fail(TLSGPU_EINVAL, "invalid session params at %u", i);
+  if (n == 0) return TLSGPU_OK;
+  HIPCHK(hipSetDevice(t->eng->device));
+  tlsgpu_session_params* d_params = nullptr;
+  HIPCHK(hipMalloc(&d_params, sizeof(tlsgpu_session_params) * n));
+  hipError_t err = hipMemcpyAsync(d_params, params, sizeof(tlsgpu_session_params) * n,
+                                  hipMemcpyHostToDevice, t->eng->stream);
+  int rc = err == hipSuccess
+               ? launch_session_install(t->d_sess, t->d_gcm, d_params, first, n, t->eng->stream)
+               : -1;
+  hipError_t serr = hipStreamSynchronize(t->eng->stream);
+  hipFree(d_params);
+  if (err != hipSuccess || rc != 0 || serr != hipSuccess)
+    return fail(TLSGPU_EHIP, "session install failed: %s",
+                hipGetErrorString(err != hipSuccess ? err : serr));
+  for (uint32_t i = 0; i < n; i++) {
+    t->kinds[first + i] = params[i].aead;
+    t->have[params[i].aead] = true;
+  }
+  return TLSGPU_OK;
+}
+
+static int groups_for(const tlsgpu_engine* e, uint32_t n, uint32_t* per_group) {
+  // one persistent 16-wave workgroup per CU, contiguous record ranges
+  uint32_t groups = (uint32_t)e->num_cus;
+  uint32_t min_per = 16;
+  if ((uint64_t)groups * min_per > n) groups = (n + min_per - 1) / min_per;
+  if (groups == 0) groups = 1;
+  *per_group = (n + groups - 1) / groups;
+  groups = (n + *per_group - 1) / *per_group;
+  return (int)groups;
+}
+
+static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const uint8_t* d_in,
+                     uint8_t* d_out, int32_t* d_status, hipStream_t s, bool seal, bool raw) {
+  BatchArgs a;
+  a.sessions = t->d_sess;
+  a.gcm_tables = t->d_gcm;
+  a.descs = d_descs;
+  a.n = n;
+  a.in = d_in;
+  a.out = d_out;
+  a.status = d_status;
+  int groups = groups_for(t->eng, n, &a.records_per_group);
+  // records whose session is empty/invalid keep this status
+  HIPCHK(hipMemsetD32Async((hipDeviceptr_t)d_status, (int)TLSGPU_REC_PUBLIC_INVALID, n, s));
+  if (t->have[TLSGPU_AES_128_GCM] && launch_gcm(a, seal, raw, 10, groups, s))
+    return fail(TLSGPU_EHIP, "gcm-128 launch: %s", hipGetErrorString(hipGetLastError()));
+  if (t->have[TLSGPU_AES_256_GCM] && launch_gcm(a, seal, raw, 14, groups, s))
+    return fail(TLSGPU_EHIP, "gcm-256 launch: %s", hipGetErrorString(hipGetLastError()));
+  if ((t->have[TLSGPU_CHACHA20_POLY1305] || t->have[TLSGPU_CHACHA20_POLY1305_OLD]) &&
+      launch_chacha(a, seal, raw, groups, s))
+    return fail(TLSGPU_EHIP, "chacha launch: %s", hipGetErrorString(hipGetLastError()));
+  return TLSGPU_OK;
+}
+
+extern "C" int tlsgpu_open_batch(tlsgpu_sessions* t, const tlsgpu_record* d_recs, uint32_t n,
+                                 const uint8_t* d_in, uint8_t* d_out, int32_t* d_status,
+                                 void* stream) {
+  if (!t || (n && (!d_recs || !d_in || !d_out || !d_status)))
+    return fail(TLSGPU_EINVAL, "bad arguments");
+  if (n == 0) return TLSGPU_OK;
+  HIPCHK(hipSetDevice(t->eng->device));
+  return run_batch(t, d_recs, n, d_in, d_out, d_status,
+                   stream ? (hipStream_t)stream : t->eng->stream, false, false);
+}
+
+extern "C" int tlsgpu_seal_batch(tlsgpu_sessions* t, const tlsgpu_record* d_recs, uint32_t n,
+                                 const uint8_t* d_in, uint8_t* d_out, int32_t* d_status,
+                                 void* stream) {
+  if (!t || (n && (!d_recs || !d_in || !d_out || !d_status)))
+    return fail(TLSGPU_EINVAL, "bad arguments");
+  if (n == 0) return TLSGPU_OK;
+  HIPCHK(hipSetDevice(t->eng->device));
+  return run_batch(t, d_recs, n, d_in, d_out, d_status,
+                   stream ? (hipStream_t)stream : t->eng->stream, true, false);
+}
+
+extern "C" int tlsgpu_fill_synthetic(tlsgpu_engine* e, uint8_t* d_out, uint64_t stride,
+                                     uint32_t span_len, uint32_t n, uint64_t seed,
+                                     uint64_t index0, void* stream) {
+  if (!e || (!d_out && n)) return fail(TLSGPU_EINVAL, "bad arguments");
+  HIPCHK(hipSetDevice(e->device));
+  if (launch_fill_synthetic(d_out, stride, span_len, n, seed, index0,
+                            stream ? (hipStream_t)stream : e->stream))
+    return fail(TLSGPU_EHIP, "fill launch: %s", hipGetErrorString(hipGetLastError()));
+  return TLSGPU_OK;
+}
+
+// ---------------------------------------------------------------------------
+// memory / streams / events
+#define ENG_OR_FAIL(e) \
+  if (!(e)) return fail(TLSGPU_EINVAL, "null engine"); \
+  HIPCHK(hipSetDevice((e)->device))
+
+static hipStream_t pick(tlsgpu_engine* e, void* s) { return s ? (hipStream_t)s : e->stream; }
+
+extern "C" int tlsgpu_malloc(tlsgpu_engine* e, size_t bytes, void** d_ptr) {
+  ENG_OR_FAIL(e);
+  if (!d_ptr) return fail(TLSGPU_EINVAL, "null out");
+  if (hipMalloc(d_ptr, bytes ? bytes : 1) != hipSuccess)
+    return fail(TLSGPU_ENOMEM, "hipMalloc(%zu)", bytes);
+  return TLSGPU_OK;
+}
+extern "C" int tlsgpu_free(tlsgpu_engine* e, void* d_ptr) {
+  ENG_OR_FAIL(e);
+  HIPCHK(hipFree(d_ptr));
+  return TLSGPU_OK;
+}
+extern "C" int tlsgpu_host_alloc(tlsgpu_engine* e, size_t bytes, void** h_ptr) {
+  ENG_OR_FAIL(e);
+  if (!h_ptr) return fail(TLSGPU_EINVAL, "null out");
+  if (hipHostMalloc(h_ptr, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess)
+    return fail(TLSGPU_ENOMEM, "hipHostMalloc(%zu)", bytes);
+  return TLSGPU_OK;
+}
+extern "C" int tlsgpu_host_free(tlsgpu_engine* e, void* h_ptr) {
+  ENG_OR_FAIL(e);
+  HIPCHK(hipHostFree(h_ptr));
+  return TLSGPU_OK;
+}
+extern "C" int tlsgpu_memcpy(tlsgpu_engine* e, void* dst, const void* src, size_t bytes,
+                             void* stream) {
+  ENG_OR_FAIL(e);
+  if (bytes) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, pick(e, stream)));
+  return TLSGPU_OK;
+}
+extern "C" int tlsgpu_memset(tlsgpu_engine* e, void* d_ptr, int value, size_t bytes,
+                             void* stream) {
+  ENG_OR_FAIL(e);
+  if (bytes) HIPCHK(hipMemsetAsync(d_ptr, value, bytes, pick(e, stream)));
+  return TLSGPU_OK;
+}
+extern "C" int tlsgpu_stream_create(tlsgpu_engine* e, void** stream) {
+  ENG_OR_FAIL(e);
+  hipStream_t s;
+  HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  *stream = s;
+  return TLSGPU_OK;
+}
+extern "C" int tlsgpu_stream_destroy(tlsgpu_engine* e, void* stream) {
+  ENG_OR_FAIL(e);
+  HIPCHK(hipStreamDestroy((hipStream_t)stream));
+  return TLSGPU_OK;
+}
+extern "C" int tlsgpu_stream_sync(tlsgpu_engine* e, void* stream) {
+  ENG_OR_FAIL(e);
+  HIPCHK(hipStreamSynchronize(pick(e, stream)));
+  return TLSGPU_OK;
+}
+extern "C" int tlsgpu_event_create(tlsgpu_engine* e, void** event) {
+  ENG_OR_FAIL(e);
+  hipEvent_t ev;
+  HIPCHK(hipEventCreate(&ev));
+  *event = ev;
+  return TLSGPU_OK;
+}
+extern "C" int tlsgpu_event_destroy(tlsgpu_engine* e, void* event) {
+  ENG_OR_FAIL(e);
+  HIPCHK(hipEventDestroy((hipEvent_t)event));
+  return TLSGPU_OK;
+}
+extern "C" int tlsgpu_event_record(tlsgpu_engine* e, void* event, void* stream) {
+  ENG_OR_FAIL(e);
+  HIPCHK(hipEventRecord((hipEvent_t)event, pick(e, stream)));
+  return TLSGPU_OK;
+}
+extern "C" int tlsgpu_event_elapsed_ms(tlsgpu_engine* e, void* start, void* end, float* ms) {
+  ENG_OR_FAIL(e);
+  HIPCHK(hipEventSynchronize((hipEvent_t)end));
+  HIPCHK(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end));
+  return TLSGPU_OK;
+}
+
+// ---------------------------------------------------------------------------
+// EVP_AEAD drop-in (include/openssl/evp.h:1211-1315)
+
+// ERR queue hook: resolved only when a LibreSSL libcrypto is in the process.
+extern "C" void ERR_put_error(int lib, int func, int reason, const char* file, int line)
+    __attribute__((weak));
+
+// Values from LibreSSL include/openssl/evp.h:1327-1491 and err.h:163.
+enum {
+  ERR_LIB_EVP_ = 6,
+  F_AEAD_AES_GCM_INIT = 187, F_AEAD_AES_GCM_OPEN = 188, F_AEAD_AES_GCM_SEAL = 189,
+  F_AEAD_CHACHA20_POLY1305_INIT = 192, F_AEAD_CHACHA20_POLY1305_OPEN = 193,
+  F_AEAD_CHACHA20_POLY1305_SEAL = 194, F_AEAD_CTX_OPEN = 185, F_AEAD_CTX_SEAL = 186,
+  F_EVP_AEAD_CTX_INIT = 180,
+  R_BAD_DECRYPT = 100, R_BAD_KEY_LENGTH = 137, R_BUFFER_TOO_SMALL = 155, R_IV_TOO_LARGE = 102,
+  R_OUTPUT_ALIASES_INPUT = 172, R_TAG_TOO_LARGE = 171, R_TOO_LARGE = 164,
+  R_UNSUPPORTED_KEY_SIZE = 108,
+};
+
+static void evp_err(int func, int reason) {
+  if (ERR_put_error) ERR_put_error(ERR_LIB_EVP_, func, reason, __FILE__, __LINE__);
+}
+
+struct evp_aead_st {
+  unsigned char key_len, nonce_len, overhead, max_tag_len;
+  int kind;
+};
+
+static const evp_aead_st k_aes128 = {16, 12, 16, 16, TLSGPU_AES_128_GCM};
+static const evp_aead_st k_aes256 = {32, 12, 16, 16, TLSGPU_AES_256_GCM};
+static const evp_aead_st k_cc = {32, 12, 16, 16, TLSGPU_CHACHA20_POLY1305};
+static const evp_aead_st k_cc_old = {32, 8, 16, 16, TLSGPU_CHACHA20_POLY1305_OLD};
+
+extern "C" const EVP_AEAD* EVP_aead_aes_128_gcm(void) { return &k_aes128; }
+extern "C" const EVP_AEAD* EVP_aead_aes_256_gcm(void) { return &k_aes256; }
+extern "C" const EVP_AEAD* EVP_aead_chacha20_poly1305(void) { return &k_cc; }
+extern "C" const EVP_AEAD* EVP_aead_chacha20_poly1305_old(void) { return &k_cc_old; }
+extern "C" size_t EVP_AEAD_key_length(const EVP_AEAD* a) { return a->key_len; }
+extern "C" size_t EVP_AEAD_nonce_length(const EVP_AEAD* a) { return a->nonce_len; }
+extern "C" size_t EVP_AEAD_max_overhead(const EVP_AEAD* a) { return a->overhead; }
+extern "C" size_t EVP_AEAD_max_tag_len(const EVP_AEAD* a) { return a->max_tag_len; }
+
+// Process-wide engine for the per-call path (device from TLSGPU_DEVICE, default 0).
+static std::mutex g_mu;
+static tlsgpu_engine* g_engine = nullptr;
+
+static tlsgpu_engine* default_engine() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_engine) {
+    const char* d = getenv("TLSGPU_DEVICE");
+    if (tlsgpu_engine_create(d ? atoi(d) : 0, &g_engine) != TLSGPU_OK) g_engine = nullptr;
+  }
+  return g_engine;
+}
+
+struct AeadState {
+  tlsgpu_sessions* sess;
+  int kind;
+  unsigned tag_len;
+};
+
+// Per-thread staging for one call: device buffer + stream (calls on one ctx may
+// run concurrently from several threads, evp.h:1273-1274).
+struct Staging {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  uint8_t* d_buf = nullptr;
+  size_t cap = 0;
+  ~Staging() {
+    if (d_buf) hipFree(d_buf);
+    if (stream) hipStreamDestroy(stream);
+  }
+  bool ensure(int dev, size_t bytes) {
+    if (hipSetDevice(dev) != hipSuccess) return false;
+    if (!stream && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess)
+      return false;
+    device = dev;
+    if (cap >= bytes) return true;
+    if (d_buf) hipFree(d_buf);
+    d_buf = nullptr;
+    cap = 0;
+    size_t want = bytes < (1u << 20) ? (1u << 20) : bytes;
+    if (hipMalloc(&d_buf, want) != hipSuccess) return false;
+    cap = want;
+    return true;
+  }
+};
+static thread_local Staging t_stage;
+
+extern "C" int EVP_AEAD_CTX_init(EVP_AEAD_CTX* ctx, const EVP_AEAD* aead, const unsigned char* key,
+                                 size_t key_len, size_t tag_len, ENGINE* impl) {
+  (void)impl;
+  ctx->aead = aead;
+  ctx->aead_state = nullptr;
+  if (key_len != aead->key_len) {  // evp_aead.c:55-58
+    evp_err(F_EVP_AEAD_CTX_INIT, R_UNSUPPORTED_KEY_SIZE);
+    return 0;
+  }
+  bool gcm = aead->kind == TLSGPU_AES_128_GCM || aead->kind == TLSGPU_AES_256_GCM;
+  if (tag_len == EVP_AEAD_DEFAULT_TAG_LENGTH) tag_len = 16;
+  if (tag_len > 16) {  // e_aes.c:1388-1391, e_chacha20poly1305.c:62-65
+    evp_err(gcm ? F_AEAD_AES_GCM_INIT : F_AEAD_CHACHA20_POLY1305_INIT,
+            gcm ? R_TAG_TOO_LARGE : R_TOO_LARGE);
+    return 0;
+  }
+  tlsgpu_engine* e = default_engine();
+  if (!e) return 0;
+  auto* st = new (std::nothrow) AeadState();
+  if (!st) return 0;
+  st->kind = aead->kind;
+  st->tag_len = (unsigned)tag_len;
+  if (tlsgpu_sessions_create(e, 1, &st->sess) != TLSGPU_OK) {
+    delete st;
+    return 0;
+  }
+  tlsgpu_session_params p;
+  memset(&p, 0, sizeof(p));
+  p.aead = aead->kind;
+  p.key_len = (uint32_t)key_len;
+  memcpy(p.key, key, key_len);
+  p.tag_len = (uint32_t)tag_len;
+  p.version = 0x0303;
+  int rc = tlsgpu_sessions_install(st->sess, 0, 1, &p);
+  memset(&p, 0, sizeof(p));
+  if (rc != TLSGPU_OK) {
+    tlsgpu_sessions_destroy(st->sess);
+    delete st;
+    return 0;
+  }
+  ctx->aead_state = st;
+  return 1;
+}
+
+extern "C" void EVP_AEAD_CTX_cleanup(EVP_AEAD_CTX* ctx) {
+  if (ctx->aead == nullptr) return;
+  auto* st = (AeadState*)ctx->aead_state;
+  if (st) {
+    // scrub the device key material before freeing (explicit_bzero analogue)
+    hipSetDevice(st->sess->eng->device);
+    hipMemset(st->sess->d_sess, 0, sizeof(DevSession));
+    hipMemset(st->sess->d_gcm, 0, sizeof(DevGcmTables));
+    tlsgpu_sessions_destroy(st->sess);
+    delete st;
+  }
+  ctx->aead_state = nullptr;
+  ctx->aead = nullptr;
+}
+
+static int check_alias(const unsigned char* in, size_t in_len, const unsigned char* out) {
+  if (out <= in) return 1;
+  if (in + in_len <= out) return 1;
+  return 0;
+}
+
+// One EVP call on the GPU.  Layout of the staging buffer:
+// [RawJob | status | nonce | ad | in | out] each 256-B aligned.
+static int gpu_call(const AeadState* st, bool seal, unsigned char* out, size_t* out_len,
+                    size_t max_out_len, const unsigned char* nonce, size_t nonce_len,
+                    const unsigned char* in, size_t in_len, const unsigned char* ad,
+                    size_t ad_len) {
+  auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+  size_t out_bytes = seal ? in_len + st->tag_len : (max_out_len > in_len ? max_out_len : in_len);
+  size_t o_job = 0, o_status = al(sizeof(RawJob)), o_nonce = o_status + 256;
+  size_t o_ad = o_nonce + al(nonce_len + 1), o_in = o_ad + al(ad_len + 1);
+  size_t o_out = o_in + al(in_len + 1), total = o_out + al(out_bytes + 1);
+  tlsgpu_engine* e = st->sess->eng;
+  if (!t_stage.ensure(e->device, total)) return -1;
+  uint8_t* b = t_stage.d_buf;
+  hipStream_t s = t_stage.stream;
+  RawJob j;
+  j.in = (uint64_t)(b + o_in);
+  j.out = (uint64_t)(b + o_out);
+  j.nonce = (uint64_t)(b + o_nonce);
+  j.aad = (uint64_t)(b + o_ad);
+  j.in_len = (uint32_t)in_len;
+  j.nonce_len = (uint32_t)nonce_len;
+  j.aad_len = (uint32_t)ad_len;
+  j.session = 0;
+  j.max_out = max_out_len;
+  if (hipMemcpyAsync(b + o_job, &j, sizeof(j), hipMemcpyHostToDevice, s) != hipSuccess) return -1;
+  if (nonce_len && hipMemcpyAsync(b + o_nonce, nonce, nonce_len, hipMemcpyHostToDevice, s)) return -1;
+  if (ad_len && hipMemcpyAsync(b + o_ad, ad, ad_len, hipMemcpyHostToDevice, s)) return -1;
+  if (in_len && hipMemcpyAsync(b + o_in, in, in_len, hipMemcpyHostToDevice, s)) return -1;
+  BatchArgs a;
+  a.sessions = st->sess->d_sess;
+  a.gcm_tables = st->sess->d_gcm;
+  a.descs = b + o_job;
+  a.n = 1;
+  a.records_per_group = 1;
+  a.in = nullptr;
+  a.out = nullptr;
+  a.status = (int32_t*)(b + o_status);
+  bool gcm = st->kind == TLSGPU_AES_128_GCM || st->kind == TLSGPU_AES_256_GCM;
+  int rc = gcm ? launch_gcm(a, seal, true, st->kind == TLSGPU_AES_128_GCM ? 10 : 14, 1, s)
+               : launch_chacha(a, seal, true, 1, s);
+  if (rc) return -1;
+  int32_t status = TLSGPU_REC_BAD_MAC;
+  if (hipMemcpyAsync(&status, b + o_status, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
+  if (hipStreamSynchronize(s) != hipSuccess) return -1;
+  if (status < 0) {
+    // the kernel zero-filled max_out_len bytes of its output region
+    if (max_out_len &&
+        hipMemcpy(out, b + o_out, max_out_len, hipMemcpyDeviceToHost) != hipSuccess)
+      memset(out, 0, max_out_len);
+    return 0;
+  }
+  if (status && hipMemcpy(out, b + o_out, (size_t)status, hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  *out_len = (size_t)status;
+  return 1;
+}
+
+extern "C" int EVP_AEAD_CTX_seal(const EVP_AEAD_CTX* ctx, unsigned char* out, size_t* out_len,
+                                 size_t max_out_len, const unsigned char* nonce, size_t nonce_len,
+                                 const unsigned char* in, size_t in_len, const unsigned char* ad,
+                                 size_t ad_len) {
+  const AeadState* st = (const AeadState*)ctx->aead_state;
+  size_t possible_out_len = in_len + ctx->aead->overhead;
+  bool gcm = ctx->aead->kind == TLSGPU_AES_128_GCM || ctx->aead->kind == TLSGPU_AES_256_GCM;
+  int r;
+  if (possible_out_len < in_len) {  // evp_aead.c:96-100
+    evp_err(F_AEAD_CTX_SEAL, R_TOO_LARGE);
+    goto error;
+  }
+  if (!check_alias(in, in_len, out)) {
+    evp_err(F_AEAD_CTX_SEAL, R_OUTPUT_ALIASES_INPUT);
+    goto error;
+  }
+  if (!st) goto error;
+  if (gcm) {
+    if (max_out_len < in_len + st->tag_len) {  // e_aes.c:1434-1437
+      evp_err(F_AEAD_AES_GCM_SEAL, R_BUFFER_TOO_SMALL);
+      goto error;
+    }
+    if (in_len > TLSGPU_MAX_RECORD * 64ull || ad_len > TLSGPU_MAX_RECORD * 64ull) goto error;
+  } else {
+    if ((uint64_t)in_len >= (1ull << 32) * 64 - 64) {  // e_chacha20poly1305.c:144-147
+      evp_err(F_AEAD_CHACHA20_POLY1305_SEAL, R_TOO_LARGE);
+      goto error;
+    }
+    if (max_out_len < in_len + st->tag_len) {
+      evp_err(F_AEAD_CHACHA20_POLY1305_SEAL, R_BUFFER_TOO_SMALL);
+      goto error;
+    }
+    if (nonce_len != ctx->aead->nonce_len) {
+      evp_err(F_AEAD_CHACHA20_POLY1305_SEAL, R_IV_TOO_LARGE);
+      goto error;
+    }
+  }
+  r = gpu_call(st, true, out, out_len, max_out_len, nonce, nonce_len, in, in_len, ad, ad_len);
+  if (r == 1) return 1;
+error:
+  memset(out, 0, max_out_len);  // evp_aead.c:113-118
+  *out_len = 0;
+  return 0;
+}
+
+extern "C" int EVP_AEAD_CTX_open(const EVP_AEAD_CTX* ctx, unsigned char* out, size_t* out_len,
+                                 size_t max_out_len, const unsigned char* nonce, size_t nonce_len,
+                                 const unsigned char* in, size_t in_len, const unsigned char* ad,
+                                 size_t ad_len) {
+  const AeadState* st = (const AeadState*)ctx->aead_state;
+  bool gcm = ctx->aead->kind == TLSGPU_AES_128_GCM || ctx->aead->kind == TLSGPU_AES_256_GCM;
+  int r;
+  if (!check_alias(in, in_len, out)) {
+    evp_err(F_AEAD_CTX_OPEN, R_OUTPUT_ALIASES_INPUT);
+    goto error;
+  }
+  if (!st) goto error;
+  if (gcm) {
+    if (in_len < st->tag_len) {  // e_aes.c:1473-1476
+      evp_err(F_AEAD_AES_GCM_OPEN, R_BAD_DECRYPT);
+      goto error;
+    }
+    if (max_out_len < in_len - st->tag_len) {
+      evp_err(F_AEAD_AES_GCM_OPEN, R_BUFFER_TOO_SMALL);
+      goto error;
+    }
+    if (in_len > TLSGPU_MAX_RECORD * 64ull || ad_len > TLSGPU_MAX_RECORD * 64ull) goto error;
+  } else {
+    if (in_len < st->tag_len) {  // e_chacha20poly1305.c:223-226
+      evp_err(F_AEAD_CHACHA20_POLY1305_OPEN, R_BAD_DECRYPT);
+      goto error;
+    }
+    if ((uint64_t)in_len >= (1ull << 32) * 64 - 64) {
+      evp_err(F_AEAD_CHACHA20_POLY1305_OPEN, R_TOO_LARGE);
+      goto error;
+    }
+    if (nonce_len != ctx->aead->nonce_len) {
+      evp_err(F_AEAD_CHACHA20_POLY1305_OPEN, R_IV_TOO_LARGE);
+      goto error;
+    }
+    if (max_out_len < in_len - st->tag_len) {
+      evp_err(F_AEAD_CHACHA20_POLY1305_OPEN, R_BUFFER_TOO_SMALL);
+      goto error;
+    }
+  }
+  r = gpu_call(st, false, out, out_len, max_out_len, nonce, nonce_len, in, in_len, ad, ad_len);
+  if (r == 1) return 1;
+  evp_err(gcm ? F_AEAD_AES_GCM_OPEN : F_AEAD_CHACHA20_POLY1305_OPEN, R_BAD_DECRYPT);
+error:
+  memset(out, 0, max_out_len);  // evp_aead.c:137-143
+  *out_len = 0;
+  return 0;
+}

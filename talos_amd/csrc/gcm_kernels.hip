@@ -1,0 +1,636 @@
+// gcm_kernels.hip — AES-GCM TLS record open/seal for gfx950 (MI355X).
+//
+// Replaces, per record, aead_aes_gcm_open/seal (crypto/evp/e_aes.c:1424-1510)
+// driven by tls1_enc (ssl/t1_enc.c:832-975), i.e. CRYPTO_gcm128_setiv
+// (gcm128.c:749-824), _aad (:826-881), _decrypt_ctr32/_encrypt_ctr32
+// (:1242-1475, inc32 counter), _finish/_tag (:1477-1521) and the
+// constant-time tag check (e_aes.c:1502) with zero-fill on failure
+// (evp_aead.c:137-143).
+//
+// Layout and mapping:
+//   * persistent workgroups of 16 waves, one per CU, each owning a contiguous
+//     range of records; a record is processed by one wave, block i of the
+//     record by lane i % 64 at step i / 64 (coalesced 16-B lane accesses);
+//   * LDS (one array, 147,520 B):
+//       AES  [0, 64K):      row x = 32 bank-replicated copies of Te0[x] then of
+//                           Te1[x]; address = v_perm(state byte, lane bank) so a
+//                           lookup is 1 VALU + 1 conflict-free ds_read_b32;
+//       KTAB [64K, 128K):   T[j][b] = (byte b at position j) * H^64, row b,
+//                           slot j; lane m = lane%16 reads position (k+m)%16
+//                           at step k (its state pre-rotated by m bytes) so the
+//                           16 lanes of every ds_read_b128 group hit 16
+//                           different slots: conflict-free GHASH lookups;
+//       SHOUP [128K, +16.6K): 4-bit tables of H^1..H^65 for the per-lane final
+//                           multiply; REM4: 16-entry reduction table;
+//   * GHASH: lane l runs a Horner chain x <- x*H^64 ^ E_j over the extended
+//     block sequence E = [AAD', C_0..C_{nb-1}, lengths] (j = l mod 64), then
+//     y_l = x_l * H^(nb+1-jlast_l) and an XOR butterfly across the wave.
+#include "aes_common.h"
+#include "tlsgpu_internal.h"
+
+namespace tg {
+
+__device__ const WordTable g_te0 = kTe0;
+
+constexpr int kThreads = 1024;
+constexpr int kWaves = kThreads / kWave;
+constexpr uint32_t AES_OFF = 0;
+constexpr uint32_t KT_OFF = 65536;
+constexpr uint32_t SH_OFF = 131072;
+constexpr uint32_t R4_OFF = SH_OFF + kPowMax * 256;
+constexpr uint32_t LDS_BYTES = R4_OFF + 64;
+
+__shared__ __attribute__((aligned(16))) uint8_t s_lds[LDS_BYTES];
+
+// Wave-uniform data (session header, round keys, descriptors) is read through
+// the constant address space so it lands in SGPRs via s_load.
+typedef __attribute__((address_space(4))) const uint32_t cu32;
+template <typename T>
+__device__ __forceinline__ cu32* as_const(const T* p) { return (cu32*)(p); }
+
+// ---------------------------------------------------------------------------
+// LDS access helpers
+__device__ __forceinline__ uint32_t lds_u32(uint32_t off) {
+  return *reinterpret_cast<const uint32_t*>(s_lds + off);
+}
+__device__ __forceinline__ uint4 lds_u128(uint32_t off) {
+  return *reinterpret_cast<const uint4*>(s_lds + off);
+}
+
+// address of Te0[byte r of w] for this lane: [0, 0, byte, lane bank]
+template <int R>
+__device__ __forceinline__ uint32_t taddr(uint32_t w, uint32_t laneoff) {
+  return __builtin_amdgcn_perm(w, laneoff, 0x0C0C0000u | ((4u + R) << 8));
+}
+__device__ __forceinline__ uint32_t rotl16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
+
+#define TE0(w, r) lds_u32(AES_OFF + taddr<r>((w), laneoff))
+#define TE1(w, r) lds_u32(AES_OFF + 128 + taddr<r>((w), laneoff))
+
+// One full AES round on little-endian columns (ShiftRows: row r of output
+// column c comes from input column c+r).
+__device__ __forceinline__ void aes_round(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3,
+                                          uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3,
+                                          uint32_t laneoff) {
+  uint32_t t0 = TE0(s0, 0) ^ TE1(s1, 1) ^ k0 ^ rotl16(TE0(s2, 2) ^ TE1(s3, 3));
+  uint32_t t1 = TE0(s1, 0) ^ TE1(s2, 1) ^ k1 ^ rotl16(TE0(s3, 2) ^ TE1(s0, 3));
+  uint32_t t2 = TE0(s2, 0) ^ TE1(s3, 1) ^ k2 ^ rotl16(TE0(s0, 2) ^ TE1(s1, 3));
+  uint32_t t3 = TE0(s3, 0) ^ TE1(s0, 1) ^ k3 ^ rotl16(TE0(s1, 2) ^ TE1(s2, 3));
+  s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+}
+
+// Final round: SubBytes/ShiftRows only.  S[x] is byte 1 (and 2) of Te0_le[x]
+// and byte 3 of Te1_le[x].
+__device__ __forceinline__ uint32_t last_col(uint32_t a, uint32_t b, uint32_t c, uint32_t d,
+                                             uint32_t k, uint32_t laneoff) {
+  uint32_t lo = __builtin_amdgcn_perm(TE0(b, 1), TE0(a, 0), 0x0C0C0501u);
+  uint32_t hi = __builtin_amdgcn_perm(TE1(d, 3), TE0(c, 2), 0x07020C0Cu);
+  return lo ^ hi ^ k;
+}
+__device__ __forceinline__ void aes_last(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3,
+                                         cu32* rk, uint32_t laneoff) {
+  uint32_t t0 = last_col(s0, s1, s2, s3, rk[0], laneoff);
+  uint32_t t1 = last_col(s1, s2, s3, s0, rk[1], laneoff);
+  uint32_t t2 = last_col(s2, s3, s0, s1, rk[2], laneoff);
+  uint32_t t3 = last_col(s3, s0, s1, s2, rk[3], laneoff);
+  s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+}
+
+// Full block encryption (used for E_K(J0)).
+template <int ROUNDS>
+__device__ __forceinline__ void aes_block(uint32_t s[4], cu32* rk,
+                                          uint32_t laneoff) {
+  s[0] ^= rk[0]; s[1] ^= rk[1]; s[2] ^= rk[2]; s[3] ^= rk[3];
+#pragma unroll
+  for (int r = 1; r < ROUNDS; r++)
+    aes_round(s[0], s[1], s[2], s[3], rk[4 * r], rk[4 * r + 1], rk[4 * r + 2], rk[4 * r + 3],
+              laneoff);
+  aes_last(s[0], s[1], s[2], s[3], rk + 4 * ROUNDS, laneoff);
+}
+
+// Per-record CTR constants: J0 columns 0..2 through AddRoundKey 0 and the
+// constant three quarters of round 1 (only column 3 carries the counter).
+struct CtrConst { uint32_t k1[4]; uint32_t rk03; };
+
+__device__ __forceinline__ CtrConst ctr_setup(const uint32_t j0[4], cu32* rk,
+                                              uint32_t laneoff) {
+  uint32_t s0 = j0[0] ^ rk[0], s1 = j0[1] ^ rk[1], s2 = j0[2] ^ rk[2];
+  CtrConst c;
+  c.k1[0] = TE0(s0, 0) ^ TE1(s1, 1) ^ rotl16(TE0(s2, 2)) ^ rk[4];
+  c.k1[1] = TE0(s1, 0) ^ TE1(s2, 1) ^ rotl16(TE1(s0, 3)) ^ rk[5];
+  c.k1[2] = TE0(s2, 0) ^ rotl16(TE0(s0, 2) ^ TE1(s1, 3)) ^ rk[6];
+  c.k1[3] = TE1(s0, 1) ^ rotl16(TE0(s1, 2) ^ TE1(s2, 3)) ^ rk[7];
+  c.rk03 = rk[3];
+  return c;
+}
+
+// Keystream block for 32-bit counter value ctr (big-endian in bytes 12..15).
+template <int ROUNDS>
+__device__ __forceinline__ void aes_ctr(uint32_t ks[4], uint32_t ctr, const CtrConst& c,
+                                        cu32* rk, uint32_t laneoff) {
+  uint32_t v = bswap32(ctr) ^ c.rk03;
+  uint32_t s0 = c.k1[0] ^ rotl16(TE1(v, 3));
+  uint32_t s1 = c.k1[1] ^ rotl16(TE0(v, 2));
+  uint32_t s2 = c.k1[2] ^ TE1(v, 1);
+  uint32_t s3 = c.k1[3] ^ TE0(v, 0);
+#pragma unroll
+  for (int r = 2; r < ROUNDS; r++)
+    aes_round(s0, s1, s2, s3, rk[4 * r], rk[4 * r + 1], rk[4 * r + 2], rk[4 * r + 3], laneoff);
+  aes_last(s0, s1, s2, s3, rk + 4 * ROUNDS, laneoff);
+  ks[0] = s0; ks[1] = s1; ks[2] = s2; ks[3] = s3;
+}
+
+// ---------------------------------------------------------------------------
+// GHASH helpers
+struct GhLane {
+  bool c2, c1;       // word-rotation selects for m = lane % 16
+  uint32_t r;        // byte rotation
+  uint32_t cq[4];    // slot bytes: cq[q].byte[i] = ((4q + i + m) & 15) * 16
+};
+
+__device__ __forceinline__ GhLane gh_lane(uint32_t lane) {
+  GhLane g;
+  uint32_t m = lane & 15;
+  g.c2 = (m >> 3) & 1;
+  g.c1 = (m >> 2) & 1;
+  g.r = m & 3;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) v |= (((4 * q + i + m) & 15) << 4) << (8 * i);
+    g.cq[q] = v;
+  }
+  return g;
+}
+
+template <int K>
+__device__ __forceinline__ uint32_t kaddr(uint32_t y, uint32_t cq) {
+  return __builtin_amdgcn_perm(y, cq, 0x0C0C0000u | ((4u + K) << 8) | K);
+}
+
+// out = x * H^64 using the LDS byte-position table (LE words).
+__device__ __forceinline__ void mul_k(const uint32_t x[4], uint32_t o[4], const GhLane& g) {
+  uint32_t a0 = g.c2 ? x[2] : x[0], a1 = g.c2 ? x[3] : x[1];
+  uint32_t a2 = g.c2 ? x[0] : x[2], a3 = g.c2 ? x[1] : x[3];
+  uint32_t b0 = g.c1 ? a1 : a0, b1 = g.c1 ? a2 : a1, b2 = g.c1 ? a3 : a2, b3 = g.c1 ? a0 : a3;
+  uint32_t y[4];
+  y[0] = __builtin_amdgcn_alignbyte(b1, b0, g.r);
+  y[1] = __builtin_amdgcn_alignbyte(b2, b1, g.r);
+  y[2] = __builtin_amdgcn_alignbyte(b3, b2, g.r);
+  y[3] = __builtin_amdgcn_alignbyte(b0, b3, g.r);
+  uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    uint4 v0 = lds_u128(KT_OFF + kaddr<0>(y[q], g.cq[q]));
+    uint4 v1 = lds_u128(KT_OFF + kaddr<1>(y[q], g.cq[q]));
+    uint4 v2 = lds_u128(KT_OFF + kaddr<2>(y[q], g.cq[q]));
+    uint4 v3 = lds_u128(KT_OFF + kaddr<3>(y[q], g.cq[q]));
+    acc.x ^= v0.x ^ v1.x ^ v2.x ^ v3.x;
+    acc.y ^= v0.y ^ v1.y ^ v2.y ^ v3.y;
+    acc.z ^= v0.z ^ v1.z ^ v2.z ^ v3.z;
+    acc.w ^= v0.w ^ v1.w ^ v2.w ^ v3.w;
+  }
+  o[0] = acc.x; o[1] = acc.y; o[2] = acc.z; o[3] = acc.w;
+}
+
+// z = x * H^e (Shoup 4-bit, gcm128.c:333-393), all in big-endian words.
+__device__ __forceinline__ void mul_shoup(const uint32_t X[4], uint32_t e, uint32_t Z[4]) {
+  const uint32_t base = SH_OFF + (e - 1) * 256;
+  uint32_t n0 = X[3] & 0xF;
+  uint4 m = lds_u128(base + n0 * 16);
+  uint32_t z0 = m.x, z1 = m.y, z2 = m.z, z3 = m.w;
+#pragma unroll
+  for (int k = 1; k < 32; k++) {
+    uint32_t nib = (X[3 - k / 8] >> (4 * (k % 8))) & 0xF;
+    uint32_t rem = z3 & 0xF;
+    z3 = __builtin_amdgcn_alignbit(z2, z3, 4);
+    z2 = __builtin_amdgcn_alignbit(z1, z2, 4);
+    z1 = __builtin_amdgcn_alignbit(z0, z1, 4);
+    z0 = (z0 >> 4) ^ lds_u32(R4_OFF + rem * 4);
+    uint4 t = lds_u128(base + nib * 16);
+    z0 ^= t.x; z1 ^= t.y; z2 ^= t.z; z3 ^= t.w;
+  }
+  Z[0] = z0; Z[1] = z1; Z[2] = z2; Z[3] = z3;
+}
+
+// Serial GHASH over a byte string with H (all lanes redundantly, rare path:
+// non-96-bit IVs and RAW-mode AAD).  x is big-endian words.  When final_mul
+// is false the last block is only XORed in (no trailing multiply).
+__device__ void ghash_serial(uint32_t x[4], const uint8_t* p, uint64_t len, bool final_mul) {
+  for (uint64_t off = 0; off < len; off += 16) {
+    uint32_t b[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      if (off + k < len) b[k >> 2] |= (uint32_t)p[off + k] << (24 - 8 * (k & 3));
+    x[0] ^= b[0]; x[1] ^= b[1]; x[2] ^= b[2]; x[3] ^= b[3];
+    if (off + 16 < len || final_mul) {
+      uint32_t z[4];
+      mul_shoup(x, 1, z);
+      x[0] = z[0]; x[1] = z[1]; x[2] = z[2]; x[3] = z[3];
+    }
+  }
+}
+
+__device__ __forceinline__ void be_from_le(const uint32_t* l, uint32_t* b) {
+  b[0] = bswap32(l[0]); b[1] = bswap32(l[1]); b[2] = bswap32(l[2]); b[3] = bswap32(l[3]);
+}
+
+// ---------------------------------------------------------------------------
+// Memory helpers (records are byte-aligned in general).
+__device__ __forceinline__ uint32_t load_u32_bytes(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+__device__ __forceinline__ void load_block(const uint8_t* p, uint32_t nbytes, bool aligned,
+                                           uint32_t v[4]) {
+  if (nbytes == 16 && aligned) {
+    uint4 t = *reinterpret_cast<const uint4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else {
+    v[0] = v[1] = v[2] = v[3] = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++)
+      if (k < nbytes) v[k >> 2] |= (uint32_t)p[k] << (8 * (k & 3));
+  }
+}
+
+__device__ __forceinline__ void store_block(uint8_t* p, uint32_t nbytes, bool aligned,
+                                            const uint32_t v[4]) {
+  if (nbytes == 16 && aligned) {
+    *reinterpret_cast<uint4*>(p) = make_uint4(v[0], v[1], v[2], v[3]);
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++)
+      if (k < nbytes) p[k] = (uint8_t)(v[k >> 2] >> (8 * (k & 3)));
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// Per-record context after parsing (TLS descriptor or raw job).
+struct RecCtx {
+  const uint8_t* src;     // open: ciphertext ; seal: plaintext
+  uint8_t* dst;           // open: plaintext  ; seal: ciphertext
+  const uint8_t* tag_in;  // open: received tag (tag_len bytes)
+  uint8_t* tag_out;       // seal: where the tag goes
+  uint32_t n;             // plaintext length
+  uint32_t j0[4];         // J0 (LE words)
+  uint32_t aad_be[4];     // AAD' = Horner of the AAD blocks without the final
+                          // multiply (gcm128.c:826-881 folded), BE words
+  uint64_t aad_len;       // bytes of AAD (for the lengths block)
+  uint64_t zero_len;      // bytes of dst zero-filled on failure
+  int32_t ok_status;      // status written on success
+};
+
+// GHASH(AAD || C || lengths) with the lane chains described in the header,
+// fused with CTR en/decryption.  Returns the tag check result (open) and
+// writes the tag (seal).
+template <bool SEAL, int ROUNDS>
+__device__ void gcm_record(const RecCtx& rc, const DevSession* __restrict__ S,
+                           int32_t* status_slot, uint32_t lane, uint32_t laneoff,
+                           const GhLane& gl) {
+  cu32* rk = as_const(S->rk);
+  const uint32_t n = rc.n;
+  const uint32_t nb = (n + 15) >> 4;
+
+  uint32_t ek0[4] = {rc.j0[0], rc.j0[1], rc.j0[2], rc.j0[3]};
+  aes_block<ROUNDS>(ek0, rk, laneoff);
+  const CtrConst cc = ctr_setup(rc.j0, rk, laneoff);
+  const uint32_t ctr0 = bswap32(rc.j0[3]) + 1u;  // inc32(J0), gcm128.c:815-823
+
+  const bool aligned = ((((uintptr_t)rc.src) | ((uintptr_t)rc.dst)) & 15) == 0;
+
+  // Horner chain state (LE words).  The AAD' element sits at j = -1, i.e. in
+  // lane 63's chain one H^64 step before C_63.
+  const bool has_aad = rc.aad_len != 0;
+  uint32_t x[4] = {0, 0, 0, 0};
+  if (has_aad && lane == 63) {
+    x[0] = bswap32(rc.aad_be[0]); x[1] = bswap32(rc.aad_be[1]);
+    x[2] = bswap32(rc.aad_be[2]); x[3] = bswap32(rc.aad_be[3]);
+  }
+
+  for (uint32_t base = 0; base < nb; base += kWave) {
+    const uint32_t i = base + lane;
+    const bool active = i < nb;
+    const uint32_t nbytes = active ? min(16u, n - 16u * i) : 0u;
+    uint32_t in[4];
+    load_block(rc.src + 16u * i, nbytes, aligned, in);
+    uint32_t ks[4];
+    aes_ctr<ROUNDS>(ks, ctr0 + i, cc, rk, laneoff);
+    if (nbytes < 16) {  // zero-padded GHASH block for the partial tail
+#pragma unroll
+      for (int w = 0; w < 4; w++) {
+        int32_t b = (int32_t)nbytes - 4 * w;
+        uint32_t keep = b >= 4 ? 0xFFFFFFFFu : (b <= 0 ? 0u : ((1u << (8 * b)) - 1u));
+        ks[w] &= keep;
+      }
+    }
+    uint32_t ob[4] = {in[0] ^ ks[0], in[1] ^ ks[1], in[2] ^ ks[2], in[3] ^ ks[3]};
+    if (active) store_block(rc.dst + 16u * i, nbytes, aligned, ob);
+    uint32_t xk[4];
+    mul_k(x, xk, gl);
+    if (active) {
+      const uint32_t* c = SEAL ? ob : in;
+      x[0] = xk[0] ^ c[0]; x[1] = xk[1] ^ c[1]; x[2] = xk[2] ^ c[2]; x[3] = xk[3] ^ c[3];
+    }
+  }
+
+  // lengths block BE64(aad bits) || BE64(ct bits) joins lane (nb % 64)'s chain
+  // at j = nb (gcm128.c:1477-1500).
+  const uint32_t lstar = nb & 63;
+  {
+    uint32_t xk[4];
+    mul_k(x, xk, gl);
+    if (lane == lstar) {
+      uint64_t ab = rc.aad_len * 8, cb = (uint64_t)n * 8;
+      x[0] = xk[0] ^ bswap32((uint32_t)(ab >> 32));
+      x[1] = xk[1] ^ bswap32((uint32_t)ab);
+      x[2] = xk[2] ^ bswap32((uint32_t)(cb >> 32));
+      x[3] = xk[3] ^ bswap32((uint32_t)cb);
+    }
+  }
+
+  // Last element index of this lane's chain and its remaining weight H^e.
+  int32_t jlast;
+  if (lane == lstar) {
+    jlast = (int32_t)nb;
+  } else if (lane < nb) {
+    jlast = (int32_t)(lane + ((nb - 1 - lane) & ~63u));
+  } else {
+    jlast = (has_aad && lane == 63) ? -1 : -2;  // -2: empty chain
+  }
+  uint32_t y[4] = {0, 0, 0, 0};
+  if (jlast != -2) {
+    uint32_t xb[4], zb[4];
+    be_from_le(x, xb);
+    mul_shoup(xb, (uint32_t)((int32_t)nb + 1 - jlast), zb);
+    y[0] = zb[0]; y[1] = zb[1]; y[2] = zb[2]; y[3] = zb[3];
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    y[0] ^= __shfl_xor(y[0], m);
+    y[1] ^= __shfl_xor(y[1], m);
+    y[2] ^= __shfl_xor(y[2], m);
+    y[3] ^= __shfl_xor(y[3], m);
+  }
+  // tag = GHASH ^ E_K(J0)  (y is BE words, ek0 LE words)
+  uint32_t tag[4] = {bswap32(y[0]) ^ ek0[0], bswap32(y[1]) ^ ek0[1], bswap32(y[2]) ^ ek0[2],
+                     bswap32(y[3]) ^ ek0[3]};
+  const uint32_t tag_len = as_const(&S->tag_len)[0];
+  const uint32_t tw = lane >> 2;
+  const uint32_t tword = tw == 0 ? tag[0] : tw == 1 ? tag[1] : tw == 2 ? tag[2] : tag[3];
+  const uint32_t tbyte = (tword >> (8 * (lane & 3))) & 0xFF;
+  if (SEAL) {
+    if (lane < tag_len) rc.tag_out[lane] = (uint8_t)tbyte;
+    if (lane == 0) *status_slot = rc.ok_status;
+  } else {
+    uint32_t diff = 0;
+    if (lane < tag_len) diff = rc.tag_in[lane] ^ tbyte;
+    bool bad = __any(diff != 0);  // constant-time in the data: every lane compares
+    if (bad) {
+      for (uint64_t o = lane; o < rc.zero_len; o += kWave) rc.dst[o] = 0;
+    }
+    if (lane == 0) *status_slot = bad ? TLSGPU_REC_BAD_MAC : rc.ok_status;
+  }
+}
+
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+         __builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+__device__ __forceinline__ tlsgpu_record load_desc(const tlsgpu_record* p) {
+  cu32* w = as_const(p);
+  tlsgpu_record d;
+  d.in_off = ((uint64_t)w[1] << 32) | w[0];
+  d.out_off = ((uint64_t)w[3] << 32) | w[2];
+  d.seq = ((uint64_t)w[5] << 32) | w[4];
+  d.session = w[6];
+  d.len_type = w[7];
+  return d;
+}
+
+// Build the per-record context from a TLS descriptor (t1_enc.c:832-975).
+// Returns false (and writes the status) when tls1_enc would return 0.
+template <bool SEAL>
+__device__ __forceinline__ bool parse_tls(const tlsgpu_record& d, const DevSession* __restrict__ S,
+                                          const uint8_t* in, uint8_t* out, int32_t* status_slot,
+                                          uint32_t lane, RecCtx& rc) {
+  uint32_t len = d.len_type & 0xFFFFFFu;
+  uint32_t type = d.len_type >> 24;
+  const uint8_t* ip = in + d.in_off;
+  uint8_t* op = out + d.out_off;
+  uint8_t explicit_nonce[8];
+  uint32_t tag_len = as_const(&S->tag_len)[0];
+  if (SEAL) {
+    rc.n = len;
+    rc.src = ip;
+    rc.dst = op + 8;
+    rc.tag_out = op + 8 + len;
+    rc.tag_in = nullptr;
+    for (int k = 0; k < 8; k++) explicit_nonce[k] = (uint8_t)(d.seq >> (56 - 8 * k));
+    if (lane < 8) op[lane] = (uint8_t)(d.seq >> (56 - 8 * lane));  // explicit nonce into the record
+    rc.ok_status = (int32_t)(len + 8 + tag_len);
+    rc.zero_len = 0;
+  } else {
+    if (len < 8 || len - 8 < tag_len) {
+      if (lane == 0) *status_slot = TLSGPU_REC_PUBLIC_INVALID;
+      return false;
+    }
+    for (int k = 0; k < 8; k++) explicit_nonce[k] = ip[k];
+    rc.n = len - 8 - tag_len;
+    rc.src = ip + 8;
+    rc.dst = op;
+    rc.tag_in = ip + 8 + rc.n;
+    rc.tag_out = nullptr;
+    rc.ok_status = (int32_t)rc.n;
+    rc.zero_len = rc.n;
+  }
+  // nonce = fixed_iv(4) || explicit(8); J0 = nonce || 0x00000001
+  rc.j0[0] = as_const(S->fixed_nonce)[0];
+  rc.j0[1] = (uint32_t)explicit_nonce[0] | ((uint32_t)explicit_nonce[1] << 8) |
+             ((uint32_t)explicit_nonce[2] << 16) | ((uint32_t)explicit_nonce[3] << 24);
+  rc.j0[2] = (uint32_t)explicit_nonce[4] | ((uint32_t)explicit_nonce[5] << 8) |
+             ((uint32_t)explicit_nonce[6] << 16) | ((uint32_t)explicit_nonce[7] << 24);
+  rc.j0[3] = 0x01000000u;
+  // AAD = seq(8) || type || version(2) || length(2), one zero-padded block
+  uint32_t v = as_const(&S->version)[0];
+  rc.aad_be[0] = (uint32_t)(d.seq >> 32);
+  rc.aad_be[1] = (uint32_t)d.seq;
+  rc.aad_be[2] = (type << 24) | ((v & 0xFFFF) << 8) | ((rc.n >> 8) & 0xFF);
+  rc.aad_be[3] = (rc.n & 0xFF) << 24;
+  rc.aad_len = 13;
+  return true;
+}
+
+// Raw EVP_AEAD job (arbitrary nonce and AAD; e_aes.c:1424-1510).  The host
+// already applied the argument checks of evp_aead.c / e_aes.c.
+template <bool SEAL>
+__device__ __forceinline__ void parse_raw(const RawJob& j, const DevSession* __restrict__ S,
+                                          RecCtx& rc) {
+  const uint8_t* ip = (const uint8_t*)j.in;
+  uint8_t* op = (uint8_t*)j.out;
+  const uint8_t* nonce = (const uint8_t*)j.nonce;
+  uint32_t tag_len = as_const(&S->tag_len)[0];
+  if (SEAL) {
+    rc.n = j.in_len;
+    rc.src = ip;
+    rc.dst = op;
+    rc.tag_out = op + j.in_len;
+    rc.tag_in = nullptr;
+    rc.ok_status = (int32_t)(j.in_len + tag_len);
+  } else {
+    rc.n = j.in_len - tag_len;
+    rc.src = ip;
+    rc.dst = op;
+    rc.tag_in = ip + rc.n;
+    rc.tag_out = nullptr;
+    rc.ok_status = (int32_t)rc.n;
+  }
+  rc.zero_len = j.max_out;
+  if (j.nonce_len == 12) {
+    rc.j0[0] = load_u32_bytes(nonce);
+    rc.j0[1] = load_u32_bytes(nonce + 4);
+    rc.j0[2] = load_u32_bytes(nonce + 8);
+    rc.j0[3] = 0x01000000u;
+  } else {  // J0 = GHASH(IV || pad || 0^64 || [len(IV)]_64)  (gcm128.c:770-812)
+    uint32_t xb[4] = {0, 0, 0, 0};
+    ghash_serial(xb, nonce, j.nonce_len, true);
+    uint64_t bits = (uint64_t)j.nonce_len * 8;
+    xb[2] ^= (uint32_t)(bits >> 32);
+    xb[3] ^= (uint32_t)bits;
+    uint32_t z[4];
+    mul_shoup(xb, 1, z);
+    rc.j0[0] = bswap32(z[0]); rc.j0[1] = bswap32(z[1]);
+    rc.j0[2] = bswap32(z[2]); rc.j0[3] = bswap32(z[3]);
+  }
+  rc.aad_be[0] = rc.aad_be[1] = rc.aad_be[2] = rc.aad_be[3] = 0;
+  rc.aad_len = j.aad_len;
+  if (j.aad_len) ghash_serial(rc.aad_be, (const uint8_t*)j.aad, j.aad_len, false);
+}
+
+// ---------------------------------------------------------------------------
+// Workgroup prologue / session table staging
+__device__ void fill_aes_lds() {
+  const uint32_t t = threadIdx.x;  // 1024 threads x 64 B = 64 KiB
+  const uint32_t row = t >> 2, part = t & 3;
+  uint32_t v = g_te0.v[row];
+  if (part >= 2) v = rotl32(v, 8);  // Te1 = rotl8(Te0)
+  uint4 w = make_uint4(v, v, v, v);
+  uint4* dst = reinterpret_cast<uint4*>(s_lds + AES_OFF + row * 256 + part * 64);
+  dst[0] = w; dst[1] = w; dst[2] = w; dst[3] = w;
+  if (t < 16) {  // rem_4bit >> 32 (gcm128.c:327-331), derived by four x-shifts
+    uint64_t hi = 0, lo = t;
+    for (int k = 0; k < 4; k++) {
+      uint64_t c = lo & 1;
+      lo = (lo >> 1) | (hi << 63);
+      hi = (hi >> 1) ^ (c ? 0xE100000000000000ull : 0);
+    }
+    *reinterpret_cast<uint32_t*>(s_lds + R4_OFF + t * 4) = (uint32_t)(hi >> 32);
+  }
+}
+
+// Expand the session's 128 basis vectors K*x^p into T[j][b] and copy the
+// Shoup tables of H^1..H^65.
+__device__ void load_session_tables(const DevGcmTables* __restrict__ tab) {
+  const uint32_t t = threadIdx.x;
+  const uint32_t j = __builtin_amdgcn_readfirstlane(t >> 6);  // byte position = wave id
+  const uint32_t bl = t & 63;
+  uint32_t lo[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < 6; k++) {   // bit k of the byte <-> x^(8j + 7 - k)
+    uint32_t msk = 0u - ((bl >> k) & 1u);
+    cu32* bv = as_const(tab->basis[8 * j + 7 - k]);
+    lo[0] ^= bv[0] & msk; lo[1] ^= bv[1] & msk; lo[2] ^= bv[2] & msk; lo[3] ^= bv[3] & msk;
+  }
+  cu32* b6 = as_const(tab->basis[8 * j + 1]);
+  cu32* b7 = as_const(tab->basis[8 * j + 0]);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    uint32_t m6 = (q & 1) ? 0xFFFFFFFFu : 0u, m7 = (q & 2) ? 0xFFFFFFFFu : 0u;
+    uint4 v = make_uint4(lo[0] ^ (b6[0] & m6) ^ (b7[0] & m7), lo[1] ^ (b6[1] & m6) ^ (b7[1] & m7),
+                         lo[2] ^ (b6[2] & m6) ^ (b7[2] & m7), lo[3] ^ (b6[3] & m6) ^ (b7[3] & m7));
+    uint32_t b = bl + 64u * q;
+    *reinterpret_cast<uint4*>(s_lds + KT_OFF + b * 256 + j * 16) = v;
+  }
+  const uint4* sh = reinterpret_cast<const uint4*>(&tab->shoup[0][0][0]);
+  for (uint32_t k = t; k < kPowMax * 16; k += kThreads)
+    *reinterpret_cast<uint4*>(s_lds + SH_OFF + k * 16) = sh[k];
+}
+
+__device__ __forceinline__ bool is_gcm(uint32_t kind) {
+  return kind == TLSGPU_AES_128_GCM || kind == TLSGPU_AES_256_GCM;
+}
+
+template <bool SEAL, bool RAW, int ROUNDS>
+__global__ __launch_bounds__(kThreads, 1) void gcm_batch_kernel(BatchArgs a) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t laneoff = (lane & 31) * 4;
+  const GhLane gl = gh_lane(lane);
+
+  fill_aes_lds();
+
+  const uint32_t rlo = blockIdx.x * a.records_per_group;
+  const uint32_t rhi = min(a.n, rlo + a.records_per_group);
+  uint32_t cur = 0xFFFFFFFFu;
+  uint32_t pos = rlo;
+  while (pos < rhi) {
+    // session id of this run (wave-uniform; every wave computes the same run)
+    const uint32_t sid = __builtin_amdgcn_readfirstlane(
+        RAW ? reinterpret_cast<const RawJob*>(a.descs)[pos].session
+            : reinterpret_cast<const tlsgpu_record*>(a.descs)[pos].session);
+    uint32_t run_end = pos + 1;
+    while (run_end < rhi) {
+      uint32_t p = run_end + lane;
+      uint32_t s = p < rhi ? (RAW ? reinterpret_cast<const RawJob*>(a.descs)[p].session
+                                  : reinterpret_cast<const tlsgpu_record*>(a.descs)[p].session)
+                           : sid;
+      uint64_t diff = __ballot(p < rhi && s != sid);
+      if (diff) { run_end += __builtin_amdgcn_readfirstlane((uint32_t)__builtin_ctzll(diff)); break; }
+      run_end = min(rhi, run_end + 64);
+    }
+    const DevSession* __restrict__ S = a.sessions + sid;
+    const uint32_t kind = as_const(&S->kind)[0];
+    const bool usable = is_gcm(kind) && (int)as_const(&S->rounds)[0] == ROUNDS;
+    if (usable && sid != cur) {
+      __syncthreads();
+      load_session_tables(a.gcm_tables + sid);
+      __syncthreads();
+      cur = sid;
+    }
+    if (usable) {
+      for (uint32_t r = pos + wave; r < run_end; r += kWaves) {
+        RecCtx rc;
+        int32_t* slot = a.status + r;
+        if (RAW) {
+          parse_raw<SEAL>(reinterpret_cast<const RawJob*>(a.descs)[r], S, rc);
+        } else {
+          if (!parse_tls<SEAL>(load_desc(reinterpret_cast<const tlsgpu_record*>(a.descs) + r), S, a.in, a.out,
+                               slot, lane, rc))
+            continue;
+        }
+        gcm_record<SEAL, ROUNDS>(rc, S, slot, lane, laneoff, gl);
+      }
+    }
+    pos = run_end;
+  }
+}
+
+template <bool SEAL, bool RAW, int ROUNDS>
+static int launch_one(const BatchArgs& a, int groups, hipStream_t s) {
+  hipLaunchKernelGGL((gcm_batch_kernel<SEAL, RAW, ROUNDS>), dim3(groups), dim3(kThreads), 0, s, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_gcm(const BatchArgs& a, bool seal, bool raw, int rounds, int groups, hipStream_t s) {
+  if (a.n == 0) return 0;
+  if (rounds == 10) {
+    if (seal) return raw ? launch_one<true, true, 10>(a, groups, s) : launch_one<true, false, 10>(a, groups, s);
+    return raw ? launch_one<false, true, 10>(a, groups, s) : launch_one<false, false, 10>(a, groups, s);
+  }
+  if (seal) return raw ? launch_one<true, true, 14>(a, groups, s) : launch_one<true, false, 14>(a, groups, s);
+  return raw ? launch_one<false, true, 14>(a, groups, s) : launch_one<false, false, 14>(a, groups, s);
+}
+
+}  // namespace tg

@@ -1,0 +1,82 @@
+// tlsgpu_internal.h — layouts shared by the host engine (engine.cpp) and the
+// HIP kernels (gcm_kernels.hip, chacha_kernels.hip, session_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/tlsgpu.h"
+
+namespace tg {
+
+constexpr int kWave = 64;
+
+// Device session header (one per session id, 512 B, in HBM).  Mirrors the
+// per-direction state LibreSSL keeps in SSL_AEAD_CTX (ssl/ssl_locl.h:527-543)
+// plus the expanded key material aead_aes_gcm_init / _chacha20_poly1305_init
+// derive (e_aes.c:1372-1413, e_chacha20poly1305.c:52-79).
+struct alignas(16) DevSession {
+  uint32_t kind;              // enum tlsgpu_aead, 0 = empty slot
+  uint32_t rounds;            // 10 / 14 (AES)
+  uint32_t tag_len;           // 1..16
+  uint32_t key_len;
+  uint32_t fixed_nonce_len;   // 4 / 12 / 0
+  uint32_t xor_fixed_nonce;   // ChaCha RFC 7905
+  uint32_t nonce_in_record;   // GCM explicit nonce
+  uint32_t version;           // TLS version for the AAD
+  uint8_t fixed_nonce[16];
+  uint32_t rk[60];            // AES round keys, little-endian column words
+  uint8_t chacha_key[32];
+  uint32_t h_le[4];           // H = E_K(0), little-endian words
+  uint32_t reserved[44];
+};
+static_assert(sizeof(DevSession) == 512, "DevSession layout");
+
+// Per-session GHASH tables (GCM sessions only), 16-B aligned, in HBM.
+//   basis[p]      = K * x^p, K = H^64, p = 0..127 (little-endian words); a
+//                   workgroup expands these into the 64 KiB byte-position table
+//                   T[j][b] = (b at byte j) * K in LDS.
+//   shoup[e-1][v] = v * H^e for nibble v (Shoup 4-bit, gcm128.c:255-324
+//                   layout: v's MSB is x^0), e = 1..65, big-endian words.
+constexpr int kPowMax = 65;
+struct alignas(16) DevGcmTables {
+  uint32_t basis[128][4];
+  uint32_t shoup[kPowMax][16][4];
+};
+static_assert(sizeof(DevGcmTables) == 2048 + kPowMax * 256, "DevGcmTables layout");
+
+// Raw AEAD job: one EVP_AEAD_CTX_seal/open call (arbitrary nonce / AAD), used
+// by the per-call drop-in path.  Pointers are device pointers.
+struct RawJob {
+  uint64_t in, out, nonce, aad;
+  uint32_t in_len;     // open: ct||tag length ; seal: plaintext length
+  uint32_t nonce_len;
+  uint32_t aad_len;
+  uint32_t session;
+  uint64_t max_out;    // bytes zero-filled on failure
+};
+
+// Kernel launch parameters for the GCM / ChaCha batch kernels.
+struct BatchArgs {
+  const DevSession* sessions;
+  const DevGcmTables* gcm_tables;   // indexed by session id
+  const void* descs;                // tlsgpu_record[] or RawJob[]
+  uint32_t n;
+  uint32_t records_per_group;       // contiguous range per workgroup
+  const uint8_t* in;
+  uint8_t* out;
+  int32_t* status;
+};
+
+}  // namespace tg
+
+// Kernel launchers (defined in the .hip files).
+namespace tg {
+int launch_gcm(const BatchArgs& a, bool seal, bool raw, int rounds, int groups,
+               hipStream_t s);
+int launch_chacha(const BatchArgs& a, bool seal, bool raw, int groups, hipStream_t s);
+int launch_session_install(DevSession* sessions, DevGcmTables* tables,
+                           const tlsgpu_session_params* d_params, uint32_t first,
+                           uint32_t n, hipStream_t s);
+int launch_fill_synthetic(uint8_t* d_out, uint64_t stride, uint32_t span_len,
+                          uint32_t n, uint64_t seed, uint64_t index0, hipStream_t s);
+}  // namespace tg

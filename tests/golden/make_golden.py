@@ -76,8 +76,10 @@ def parse_chacha(path: str):
 def parse_poly1305(path: str):
     src = open(path).read()
     arrs = {}
-    for m in re.finditer(r"static const unsigned char (\w+)\[\d*\]\s*=\s*\{(.*?)\};", src, re.S):
-        arrs[m.group(1)] = c_byte_list(m.group(2)).hex()
+    for m in re.finditer(r"static const unsigned char (\w+)\[(\d*)\]\s*=\s*\{(.*?)\};", src, re.S):
+        b = c_byte_list(m.group(3))
+        n = int(m.group(2)) if m.group(2) else len(b)
+        arrs[m.group(1)] = (b + bytes(n - len(b))).hex()   # C zero-fills the rest
     return arrs
 
 

@@ -1,0 +1,64 @@
+"""CPU-side checks of the C-ABI library: it loads without a GPU and exports
+every function include/*.h declares (no compute calls here)."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import talos_amd
+    if not os.path.exists(talos_amd.LIBPATH):
+        talos_amd.build()
+    return talos_amd.load_library()
+
+
+def test_library_exports_header_symbols(lib):
+    import talos_amd
+    names = talos_amd.header_symbols()
+    assert "tlsgpu_open_batch" in names and "EVP_AEAD_CTX_open" in names
+    for n in names:
+        assert hasattr(lib, n), n
+
+
+def test_exports_nothing_else():
+    import talos_amd
+    out = subprocess.run(["nm", "-D", "--defined-only", talos_amd.LIBPATH], check=True,
+                         capture_output=True, text=True).stdout
+    exported = sorted(l.split()[-1] for l in out.splitlines() if " T " in l)
+    assert exported == talos_amd.header_symbols()
+
+
+def test_aead_descriptors_without_gpu(lib):
+    """The accessor half of the EVP ABI (evp_aead.c:26-48) needs no device."""
+    import talos_amd as ta
+    want = {ta.AES_128_GCM: (16, 12, 16, 16), ta.AES_256_GCM: (32, 12, 16, 16),
+            ta.CHACHA20_POLY1305: (32, 12, 16, 16), ta.CHACHA20_POLY1305_OLD: (32, 8, 16, 16)}
+    for kind, getter in ta.EvpAead.GETTERS.items():
+        a = getattr(lib, getter)()
+        got = (lib.EVP_AEAD_key_length(a), lib.EVP_AEAD_nonce_length(a),
+               lib.EVP_AEAD_max_overhead(a), lib.EVP_AEAD_max_tag_len(a))
+        assert got == want[kind]
+
+
+def test_record_descriptor_layout():
+    import talos_amd as ta
+    import numpy as np
+    assert ta.RECORD_DTYPE.itemsize == 32
+    r = np.zeros(1, dtype=ta.RECORD_DTYPE)
+    r[0] = (1, 2, 3, 4, ta.len_type(16384, 23))
+    raw = r.view(np.uint8)
+    assert raw[24] == 4 and int.from_bytes(raw[28:32].tobytes(), "little") == (23 << 24) | 16384
+
+
+def test_engine_create_fails_loudly_without_gpu(lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import talos_amd as ta
+    with pytest.raises(ta.TlsGpuError):
+        ta.Engine(0)
