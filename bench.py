@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json metric: GiB/s of device-resident AES-128-GCM TLS record
+decrypt (tls1_enc(s, 0) / EVP_AEAD_CTX_open per record), 16 KiB records, batch
+64 Ki records per GPU (configs[1]; configs[4] = the same per-GPU batch on 8 GPUs).
+
+One step = one tlsgpu_open_batch over the whole resident batch (64 Ki records,
+1 GiB of ciphertext in HBM -> 1 GiB of plaintext in HBM + per-record status).
+Inputs are synthetic (counter-SplitMix64 plaintexts, 1024 sessions x 64 records,
+1/1024 records tampered), sealed on the device beforehand by the validated
+sealer; every step's outputs are verified after the warmup.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config B|C|D]
+  N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+       (one rank per GPU, records split by rank, no collective on the data path;
+        gloo only for the barrier and the max-over-ranks of the timing).
+
+Prints ONE JSON line (rank 0).  `roofline.achieved` = algorithmic bytes per
+launch / average launch time from HIP events on the engine stream;
+`cpu_baseline` = the reference LibreSSL EVP_AEAD_CTX_open (oracle/_ref/libref.so,
+compiled from the reference sources) on a bounded sample on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s device-resident AES-128-GCM TLS record decrypt, 16KiB recs, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+GIB = float(1 << 30)
+
+CONFIGS = {
+    # name: (kind, records per GPU, sessions, record_len or None(zipf), seed, op)
+    "B": ("aes-128-gcm", 65536, 1024, 16384, 0x5EED0001, "open"),
+    "C": ("chacha20-poly1305", 1 << 20, 4096, 1400, 0x5EED0002, "seal+open"),
+    "D": ("aes-256-gcm", 1 << 18, 1024, None, 0x5EED0003, "open"),
+}
+
+
+def algo_bytes_per_record(kind_name: str, length: int, op: str) -> int:
+    """read explicit nonce + ct + tag + 32-B descriptor, write pt + status."""
+    eiv = 8 if "gcm" in kind_name else 0
+    rd = eiv + length + 16 + 32
+    wr = length + 4
+    return rd + wr
+
+
+def cpu_baseline(kind_name: str, rec_len: int, op: str) -> dict | None:
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle
+        if not (os.path.exists(pyoracle.LIBREF) and os.path.exists(pyoracle.CPUBENCH)):
+            return None
+        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        secs = max(1.0, 20.0 / threads)   # ~20 s of CPU work in total
+        nrec = max(threads * 16, 1024)
+        r = pyoracle.run_cpubench(kind_name, "both" if op == "seal+open" else op, rec_len, nrec,
+                                  threads, secs)
+        return {"value": round(r["gib_per_s"], 3), "unit": "GiB/s", "cores": threads,
+                "kind": "reference",
+                "sample": f"LibreSSL 2.4.1 EVP_AEAD_CTX_{op} (AES-NI+PCLMUL) over {nrec} x "
+                          f"{rec_len}-B records, {threads} pthreads x {secs:.1f}s "
+                          f"({r['records']} records timed), oracle/_ref/libref.so"}
+    except Exception as exc:  # baseline is reported, never fatal
+        return {"value": None, "error": str(exc)[:200]}
+
+
+def load_traffic(config: str):
+    """PMC-measured HBM bytes per launch for this kernel, if a profile was committed."""
+    p = os.path.join(ROOT, "profiles", f"pmc_config{config}.json")
+    if os.path.exists(p):
+        try:
+            d = json.load(open(p))
+            return d.get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
+        except Exception:
+            return None, None
+    return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
+    ap.add_argument("--records", type=int, default=0, help="override records per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import talos_amd as ta
+    from talos_amd.workload import Workload, zipf_lengths
+
+    ta.load_library()
+    eng = ta.Engine(local)   # first GPU runtime user in this process
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # gloo: control plane only (barrier / max)
+        dist.init_process_group("gloo")
+
+    kind_name, per_gpu, sessions, rec_len, seed, op = CONFIGS[args.config]
+    if args.records:
+        per_gpu = args.records
+        sessions = max(1, min(sessions, per_gpu // 16))
+    kind = ta.AEAD_NAMES[kind_name]
+    lengths = None
+    if rec_len is None:
+        lengths = zipf_lengths(per_gpu, seed + rank)
+    # weak scaling: rank r owns records [r*per_gpu, (r+1)*per_gpu) of the global batch
+    wl = Workload(eng, kind, per_gpu, sessions, seed ^ (rank * 0x100000001), lengths=lengths,
+                  record_len=rec_len or 0, index0=rank * per_gpu,
+                  tamper_every=1024 if op == "open" else 0)
+    total_len = int(wl.lengths.sum())
+
+    def step(stream=None):
+        if op == "open":
+            wl.open(stream)
+        else:
+            wl.seal(stream)
+            wl.open(stream)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    eng.sync()
+    wl.verify_open()
+
+    def barrier():
+        eng.sync()
+        if dist is not None:
+            dist.barrier()
+
+    ev0, ev1 = ta.Event(eng), ta.Event(eng)
+    barrier()
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        step()
+    ev1.record()
+    eng.sync()
+    t1 = time.perf_counter()
+    dev_ms = ev0.elapsed_ms(ev1)
+    wall_ms = (t1 - t0) * 1e3
+    barrier()
+    wl.verify_open()
+
+    elapsed_s = dev_ms / 1e3
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed_s, wall_ms / 1e3], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed_s, wall_s = float(t[0]), float(t[1])
+    else:
+        wall_s = wall_ms / 1e3
+
+    payload = float(total_len) * world * args.steps          # plaintext bytes, all ranks
+    value = payload / elapsed_s / GIB
+    per_launch_s = dev_ms / 1e3 / args.steps / (2 if op == "seal+open" else 1)
+    algo = sum(algo_bytes_per_record(kind_name, int(l), op) for l in
+               ([rec_len] * per_gpu if lengths is None else lengths.tolist()))
+    achieved = algo / per_launch_s / 1e9
+    traffic, traffic_src = load_traffic(args.config)
+
+    line = {
+        "metric": METRIC if args.config == "B" else
+        f"GiB/s device-resident {kind_name} TLS record {op} (config {args.config})",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed_s * 1e3 / args.steps, 4),
+        "wall_ms_per_step": round(wall_s * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (counter-SplitMix64 plaintexts sealed on device; 1/1024 tampered)"
+        if op == "open" else "synthetic (counter-SplitMix64 plaintexts)",
+        "config": {"workload": f"{kind_name} TLS 1.2 record {op}, "
+                               f"{'16 KiB' if rec_len == 16384 else (str(rec_len) + ' B' if rec_len else 'Zipf 64 B-16 KiB')}"
+                               f" records, {per_gpu} records/GPU, device-resident",
+                   "records_per_gpu": per_gpu, "sessions_per_gpu": sessions,
+                   "payload_bytes_per_gpu": total_len, "parallelism": f"batch split x{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "algorithmic_bytes_per_launch": algo,
+                     "kernel": "gcm_batch_kernel<open>" if "gcm" in kind_name
+                     else "chacha_batch_kernel", "traffic_source": traffic_src},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(kind_name, rec_len or 1400, op)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    ev0.close()
+    ev1.close()
+    wl.free()
+    if dist is not None:
+        dist.destroy_process_group()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
