@@ -55,8 +55,10 @@ enum tlsgpu_aead {
 #define TLSGPU_REC_BAD_MAC (-1)
 #define TLSGPU_REC_PUBLIC_INVALID (-2)
 
-/* Largest record fragment the batch kernels accept (ciphertext bytes). */
-#define TLSGPU_MAX_RECORD (1u << 20)
+/* Largest plaintext per record the batch kernels accept: 65534 AES blocks, so
+ * GCM counters 2..nb+1 stay below 2^16 (TLS records are <= 16 KiB + 2 KiB,
+ * ssl3.h:259-280).  Longer records get TLSGPU_REC_PUBLIC_INVALID. */
+#define TLSGPU_MAX_RECORD (65534u * 16u)
 
 /* One TLS record, 32 bytes, device-resident array.
  * open: in_off -> record fragment after the 5-byte header

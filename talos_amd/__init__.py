@@ -41,7 +41,7 @@ TAG_LEN = 16
 
 REC_BAD_MAC = -1          # tls1_enc returns -1 (bad_record_mac)
 REC_PUBLIC_INVALID = -2   # tls1_enc returns 0
-MAX_RECORD = 1 << 20
+MAX_RECORD = 65534 * 16
 
 # tlsgpu_record (include/tlsgpu.h), 32 bytes
 RECORD_DTYPE = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("seq", "<u8"),

@@ -63,19 +63,28 @@ __device__ __forceinline__ uint32_t taddr(uint32_t w, uint32_t laneoff) {
   return __builtin_amdgcn_perm(w, laneoff, 0x0C0C0000u | ((4u + R) << 8));
 }
 __device__ __forceinline__ uint32_t rotl16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
+// three-input XOR in one VALU op: v_bitop3_b32 with truth table 0x96 (gfx950
+// has no v_xor3_b32; hipcc does not form bitop3 from these ^ chains)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t d;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
 
 #define TE0(w, r) lds_u32(AES_OFF + taddr<r>((w), laneoff))
 #define TE1(w, r) lds_u32(AES_OFF + 128 + taddr<r>((w), laneoff))
 
 // One full AES round on little-endian columns (ShiftRows: row r of output
-// column c comes from input column c+r).
+// column c comes from input column c+r).  kr_c = rotr16(k_c) is folded into the
+// rotated half so a column costs xor3 + alignbit + xor3:
+//   t = Te0[a] ^ Te1[b] ^ rotl16(Te0[c] ^ Te1[d] ^ rotr16(k))
 __device__ __forceinline__ void aes_round(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3,
                                           uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3,
                                           uint32_t laneoff) {
-  uint32_t t0 = TE0(s0, 0) ^ TE1(s1, 1) ^ k0 ^ rotl16(TE0(s2, 2) ^ TE1(s3, 3));
-  uint32_t t1 = TE0(s1, 0) ^ TE1(s2, 1) ^ k1 ^ rotl16(TE0(s3, 2) ^ TE1(s0, 3));
-  uint32_t t2 = TE0(s2, 0) ^ TE1(s3, 1) ^ k2 ^ rotl16(TE0(s0, 2) ^ TE1(s1, 3));
-  uint32_t t3 = TE0(s3, 0) ^ TE1(s0, 1) ^ k3 ^ rotl16(TE0(s1, 2) ^ TE1(s2, 3));
+  uint32_t t0 = xor3(TE0(s0, 0), TE1(s1, 1), rotl16(xor3(TE0(s2, 2), TE1(s3, 3), k0)));
+  uint32_t t1 = xor3(TE0(s1, 0), TE1(s2, 1), rotl16(xor3(TE0(s3, 2), TE1(s0, 3), k1)));
+  uint32_t t2 = xor3(TE0(s2, 0), TE1(s3, 1), rotl16(xor3(TE0(s0, 2), TE1(s1, 3), k2)));
+  uint32_t t3 = xor3(TE0(s3, 0), TE1(s0, 1), rotl16(xor3(TE0(s1, 2), TE1(s2, 3), k3)));
   s0 = t0; s1 = t1; s2 = t2; s3 = t3;
 }
 
@@ -98,12 +107,12 @@ __device__ __forceinline__ void aes_last(uint32_t& s0, uint32_t& s1, uint32_t& s
 
 // Full block encryption (used for E_K(J0)).
 template <int ROUNDS>
-__device__ __forceinline__ void aes_block(uint32_t s[4], cu32* rk,
+__device__ __forceinline__ void aes_block(uint32_t s[4], cu32* rk, cu32* rkr,
                                           uint32_t laneoff) {
   s[0] ^= rk[0]; s[1] ^= rk[1]; s[2] ^= rk[2]; s[3] ^= rk[3];
 #pragma unroll
   for (int r = 1; r < ROUNDS; r++)
-    aes_round(s[0], s[1], s[2], s[3], rk[4 * r], rk[4 * r + 1], rk[4 * r + 2], rk[4 * r + 3],
+    aes_round(s[0], s[1], s[2], s[3], rkr[4 * r], rkr[4 * r + 1], rkr[4 * r + 2], rkr[4 * r + 3],
               laneoff);
   aes_last(s[0], s[1], s[2], s[3], rk + 4 * ROUNDS, laneoff);
 }
@@ -124,10 +133,11 @@ __device__ __forceinline__ CtrConst ctr_setup(const uint32_t j0[4], cu32* rk,
   return c;
 }
 
-// Keystream block for 32-bit counter value ctr (big-endian in bytes 12..15).
+// Keystream block for 32-bit counter value ctr (big-endian in bytes 12..15),
+// general form: only round 1 is shortened.
 template <int ROUNDS>
 __device__ __forceinline__ void aes_ctr(uint32_t ks[4], uint32_t ctr, const CtrConst& c,
-                                        cu32* rk, uint32_t laneoff) {
+                                        cu32* rk, cu32* rkr, uint32_t laneoff) {
   uint32_t v = bswap32(ctr) ^ c.rk03;
   uint32_t s0 = c.k1[0] ^ rotl16(TE1(v, 3));
   uint32_t s1 = c.k1[1] ^ rotl16(TE0(v, 2));
@@ -135,9 +145,58 @@ __device__ __forceinline__ void aes_ctr(uint32_t ks[4], uint32_t ctr, const CtrC
   uint32_t s3 = c.k1[3] ^ TE0(v, 0);
 #pragma unroll
   for (int r = 2; r < ROUNDS; r++)
-    aes_round(s0, s1, s2, s3, rk[4 * r], rk[4 * r + 1], rk[4 * r + 2], rk[4 * r + 3], laneoff);
+    aes_round(s0, s1, s2, s3, rkr[4 * r], rkr[4 * r + 1], rkr[4 * r + 2], rkr[4 * r + 3], laneoff);
   aes_last(s0, s1, s2, s3, rk + 4 * ROUNDS, laneoff);
   ks[0] = s0; ks[1] = s1; ks[2] = s2; ks[3] = s3;
+}
+
+// Per-record constants for counters below 2^16 (every TLS record: the counter
+// runs 2..nb+1 with nb <= 65534).  Counter bytes 12-13 are then zero, so after
+// round 1 only columns 0 and 1 depend on the counter and round 2 needs 8
+// lookups instead of 16; E_K(J0) rides along.  Computed for 64 records at a
+// time (one per lane) and broadcast with readlane when a record is processed.
+struct RecConsts {
+  uint32_t ek0[4];   // E_K(J0)
+  uint32_t k1a, k1b; // round-1 constants of columns 0, 1
+  uint32_t k2[4];    // round-2 constants
+};
+
+template <int ROUNDS>
+__device__ __forceinline__ RecConsts rec_consts(const uint32_t j0[4], cu32* rk, cu32* rkr,
+                                                uint32_t laneoff) {
+  RecConsts r;
+  uint32_t e[4] = {j0[0], j0[1], j0[2], j0[3]};
+  aes_block<ROUNDS>(e, rk, rkr, laneoff);
+  r.ek0[0] = e[0]; r.ek0[1] = e[1]; r.ek0[2] = e[2]; r.ek0[3] = e[3];
+  CtrConst c = ctr_setup(j0, rk, laneoff);
+  const uint32_t v0 = c.rk03;           // counter bytes 12..15 = 0 (bytes 12,13 stay 0)
+  const uint32_t s2 = c.k1[2] ^ TE1(v0, 1);
+  const uint32_t s3 = c.k1[3] ^ TE0(v0, 0);
+  r.k1a = c.k1[0];
+  r.k1b = c.k1[1];
+  r.k2[0] = rotl16(TE0(s2, 2) ^ TE1(s3, 3)) ^ rk[8];
+  r.k2[1] = TE1(s2, 1) ^ rotl16(TE0(s3, 2)) ^ rk[9];
+  r.k2[2] = TE0(s2, 0) ^ TE1(s3, 1) ^ rk[10];
+  r.k2[3] = TE0(s3, 0) ^ rotl16(TE1(s2, 3)) ^ rk[11];
+  return r;
+}
+
+// Fast keystream for ctr < 2^16: round 1 = 2 lookups, round 2 = 8 lookups.
+template <int ROUNDS>
+__device__ __forceinline__ void aes_ctr16(uint32_t ks[4], uint32_t ctr, const RecConsts& c,
+                                          uint32_t rk03, cu32* rk, cu32* rkr, uint32_t laneoff) {
+  const uint32_t v = bswap32(ctr) ^ rk03;
+  const uint32_t s0 = c.k1a ^ rotl16(TE1(v, 3));
+  const uint32_t s1 = c.k1b ^ rotl16(TE0(v, 2));
+  uint32_t t0 = xor3(c.k2[0], TE0(s0, 0), TE1(s1, 1));
+  uint32_t t1 = xor3(c.k2[1], TE0(s1, 0), rotl16(TE1(s0, 3)));
+  uint32_t t2 = c.k2[2] ^ rotl16(TE0(s0, 2) ^ TE1(s1, 3));
+  uint32_t t3 = xor3(c.k2[3], TE1(s0, 1), rotl16(TE0(s1, 2)));
+#pragma unroll
+  for (int r = 3; r < ROUNDS; r++)
+    aes_round(t0, t1, t2, t3, rkr[4 * r], rkr[4 * r + 1], rkr[4 * r + 2], rkr[4 * r + 3], laneoff);
+  aes_last(t0, t1, t2, t3, rk + 4 * ROUNDS, laneoff);
+  ks[0] = t0; ks[1] = t1; ks[2] = t2; ks[3] = t3;
 }
 
 // ---------------------------------------------------------------------------
@@ -186,10 +245,10 @@ __device__ __forceinline__ void mul_k(const uint32_t x[4], uint32_t o[4], const 
     uint4 v1 = lds_u128(KT_OFF + kaddr<1>(y[q], g.cq[q]));
     uint4 v2 = lds_u128(KT_OFF + kaddr<2>(y[q], g.cq[q]));
     uint4 v3 = lds_u128(KT_OFF + kaddr<3>(y[q], g.cq[q]));
-    acc.x ^= v0.x ^ v1.x ^ v2.x ^ v3.x;
-    acc.y ^= v0.y ^ v1.y ^ v2.y ^ v3.y;
-    acc.z ^= v0.z ^ v1.z ^ v2.z ^ v3.z;
-    acc.w ^= v0.w ^ v1.w ^ v2.w ^ v3.w;
+    acc.x = xor3(acc.x, xor3(v0.x, v1.x, v2.x), v3.x);
+    acc.y = xor3(acc.y, xor3(v0.y, v1.y, v2.y), v3.y);
+    acc.z = xor3(acc.z, xor3(v0.z, v1.z, v2.z), v3.z);
+    acc.w = xor3(acc.w, xor3(v0.w, v1.w, v2.w), v3.w);
   }
   o[0] = acc.x; o[1] = acc.y; o[2] = acc.z; o[3] = acc.w;
 }
@@ -244,7 +303,7 @@ __device__ __forceinline__ uint32_t load_u32_bytes(const uint8_t* p) {
 
 __device__ __forceinline__ void load_block(const uint8_t* p, uint32_t nbytes, bool aligned,
                                            uint32_t v[4]) {
-  if (nbytes == 16 && aligned) {
+  if (aligned && nbytes == 16) {
     uint4 t = *reinterpret_cast<const uint4*>(p);
     v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
   } else {
@@ -284,19 +343,34 @@ struct RecCtx {
 };
 
 // GHASH(AAD || C || lengths) with the lane chains described in the header,
-// fused with CTR en/decryption.  Returns the tag check result (open) and
-// writes the tag (seal).
-template <bool SEAL, int ROUNDS>
+// fused with CTR en/decryption.  Checks the tag (open) or writes it (seal).
+// FAST: counters < 2^16 and the per-record constants `rcc` were precomputed
+// (wave-uniform values); otherwise everything is derived here per lane.
+template <bool SEAL, int ROUNDS, bool FAST>
 __device__ void gcm_record(const RecCtx& rc, const DevSession* __restrict__ S,
-                           int32_t* status_slot, uint32_t lane, uint32_t laneoff,
-                           const GhLane& gl) {
+                           const RecConsts& rcc, int32_t* status_slot, uint32_t lane,
+                           uint32_t laneoff, const GhLane& gl) {
   cu32* rk = as_const(S->rk);
+  cu32* rkr = as_const(S->rk_rot);
   const uint32_t n = rc.n;
   const uint32_t nb = (n + 15) >> 4;
+  const uint32_t rk03 = rk[3];
 
-  uint32_t ek0[4] = {rc.j0[0], rc.j0[1], rc.j0[2], rc.j0[3]};
-  aes_block<ROUNDS>(ek0, rk, laneoff);
-  const CtrConst cc = ctr_setup(rc.j0, rk, laneoff);
+  uint32_t ek0[4];
+  CtrConst cc;
+  if (FAST) {
+    ek0[0] = rcc.ek0[0]; ek0[1] = rcc.ek0[1]; ek0[2] = rcc.ek0[2]; ek0[3] = rcc.ek0[3];
+  } else {
+    ek0[0] = rc.j0[0]; ek0[1] = rc.j0[1]; ek0[2] = rc.j0[2]; ek0[3] = rc.j0[3];
+    aes_block<ROUNDS>(ek0, rk, rkr, laneoff);
+    cc = ctr_setup(rc.j0, rk, laneoff);
+  }
+  auto keystream = [&](uint32_t ks[4], uint32_t ctr) {
+    if (FAST)
+      aes_ctr16<ROUNDS>(ks, ctr, rcc, rk03, rk, rkr, laneoff);
+    else
+      aes_ctr<ROUNDS>(ks, ctr, cc, rk, rkr, laneoff);
+  };
   const uint32_t ctr0 = bswap32(rc.j0[3]) + 1u;  // inc32(J0), gcm128.c:815-823
 
   const bool aligned = ((((uintptr_t)rc.src) | ((uintptr_t)rc.dst)) & 15) == 0;
@@ -310,21 +384,55 @@ __device__ void gcm_record(const RecCtx& rc, const DevSession* __restrict__ S,
     x[2] = bswap32(rc.aad_be[2]); x[3] = bswap32(rc.aad_be[3]);
   }
 
-  for (uint32_t base = 0; base < nb; base += kWave) {
+  // Full-block steps, two per iteration (two independent AES chains per lane
+  // keep twice as many LDS lookups in flight), with the next iteration's
+  // ciphertext loads issued before this iteration's AES.
+  const uint32_t nfull_steps = (n >> 4) / kWave;
+  uint32_t base = 0;
+  if (nfull_steps >= 2) {
+    uint32_t c0[4], c1[4];
+    load_block(rc.src + 16u * lane, 16, aligned, c0);
+    load_block(rc.src + 16u * (lane + kWave), 16, aligned, c1);
+    uint32_t t = 0;
+    for (; t + 2 <= nfull_steps; t += 2, base += 2 * kWave) {
+      const uint32_t i = base + lane;
+      uint32_t n0[4] = {0, 0, 0, 0}, n1[4] = {0, 0, 0, 0};
+      if (t + 4 <= nfull_steps) {
+        load_block(rc.src + 16u * (i + 2 * kWave), 16, aligned, n0);
+        load_block(rc.src + 16u * (i + 3 * kWave), 16, aligned, n1);
+      }
+      uint32_t k0[4], k1[4];
+      keystream(k0, ctr0 + i);
+      keystream(k1, ctr0 + i + kWave);
+      uint32_t o0[4] = {c0[0] ^ k0[0], c0[1] ^ k0[1], c0[2] ^ k0[2], c0[3] ^ k0[3]};
+      uint32_t o1[4] = {c1[0] ^ k1[0], c1[1] ^ k1[1], c1[2] ^ k1[2], c1[3] ^ k1[3]};
+      store_block(rc.dst + 16u * i, 16, aligned, o0);
+      store_block(rc.dst + 16u * (i + kWave), 16, aligned, o1);
+      uint32_t xk[4];
+      mul_k(x, xk, gl);
+      const uint32_t* g0 = SEAL ? o0 : c0;
+      const uint32_t* g1 = SEAL ? o1 : c1;
+      x[0] = xk[0] ^ g0[0]; x[1] = xk[1] ^ g0[1]; x[2] = xk[2] ^ g0[2]; x[3] = xk[3] ^ g0[3];
+      mul_k(x, xk, gl);
+      x[0] = xk[0] ^ g1[0]; x[1] = xk[1] ^ g1[1]; x[2] = xk[2] ^ g1[2]; x[3] = xk[3] ^ g1[3];
+#pragma unroll
+      for (int w = 0; w < 4; w++) { c0[w] = n0[w]; c1[w] = n1[w]; }
+    }
+  }
+  // Remaining steps (odd full step, partial wave, partial last block).
+  for (; base < nb; base += kWave) {
     const uint32_t i = base + lane;
     const bool active = i < nb;
     const uint32_t nbytes = active ? min(16u, n - 16u * i) : 0u;
     uint32_t in[4];
     load_block(rc.src + 16u * i, nbytes, aligned, in);
     uint32_t ks[4];
-    aes_ctr<ROUNDS>(ks, ctr0 + i, cc, rk, laneoff);
-    if (nbytes < 16) {  // zero-padded GHASH block for the partial tail
+    keystream(ks, ctr0 + i);
 #pragma unroll
-      for (int w = 0; w < 4; w++) {
-        int32_t b = (int32_t)nbytes - 4 * w;
-        uint32_t keep = b >= 4 ? 0xFFFFFFFFu : (b <= 0 ? 0u : ((1u << (8 * b)) - 1u));
-        ks[w] &= keep;
-      }
+    for (int w = 0; w < 4; w++) {  // zero-padded GHASH block for the partial tail
+      int32_t b = (int32_t)nbytes - 4 * w;
+      uint32_t keep = b >= 4 ? 0xFFFFFFFFu : (b <= 0 ? 0u : ((1u << (8 * b)) - 1u));
+      ks[w] &= keep;
     }
     uint32_t ob[4] = {in[0] ^ ks[0], in[1] ^ ks[1], in[2] ^ ks[2], in[3] ^ ks[3]};
     if (active) store_block(rc.dst + 16u * i, nbytes, aligned, ob);
@@ -410,6 +518,28 @@ __device__ __forceinline__ tlsgpu_record load_desc(const tlsgpu_record* p) {
   return d;
 }
 
+// J0 of record r for this lane (the batched constant pass): fixed IV(4) ||
+// explicit nonce(8) || 0x00000001 — the explicit nonce is the record's first
+// 8 bytes on open and the sequence number on seal (t1_enc.c:887-892, 941-948).
+template <bool SEAL>
+__device__ __forceinline__ void lane_j0(const tlsgpu_record* D, uint32_t r, uint32_t run_end,
+                                        const DevSession* __restrict__ S, const uint8_t* in,
+                                        uint32_t j0[4]) {
+  j0[0] = as_const(S->fixed_nonce)[0];
+  j0[1] = j0[2] = 0;
+  j0[3] = 0x01000000u;
+  if (r >= run_end) return;
+  const tlsgpu_record d = D[r];
+  if (SEAL) {
+    j0[1] = bswap32((uint32_t)(d.seq >> 32));
+    j0[2] = bswap32((uint32_t)d.seq);
+  } else if ((d.len_type & 0xFFFFFFu) >= 8) {
+    const uint8_t* p = in + d.in_off;
+    j0[1] = load_u32_bytes(p);
+    j0[2] = load_u32_bytes(p + 4);
+  }
+}
+
 // Build the per-record context from a TLS descriptor (t1_enc.c:832-975).
 // Returns false (and writes the status) when tls1_enc would return 0.
 template <bool SEAL>
@@ -422,6 +552,11 @@ __device__ __forceinline__ bool parse_tls(const tlsgpu_record& d, const DevSessi
   uint8_t* op = out + d.out_off;
   uint8_t explicit_nonce[8];
   uint32_t tag_len = as_const(&S->tag_len)[0];
+  if (SEAL ? len > TLSGPU_MAX_RECORD : (len < 8 || len - 8 < tag_len ||
+                                          len - 8 - tag_len > TLSGPU_MAX_RECORD)) {
+    if (lane == 0) *status_slot = TLSGPU_REC_PUBLIC_INVALID;
+    return false;
+  }
   if (SEAL) {
     rc.n = len;
     rc.src = ip;
@@ -433,10 +568,6 @@ __device__ __forceinline__ bool parse_tls(const tlsgpu_record& d, const DevSessi
     rc.ok_status = (int32_t)(len + 8 + tag_len);
     rc.zero_len = 0;
   } else {
-    if (len < 8 || len - 8 < tag_len) {
-      if (lane == 0) *status_slot = TLSGPU_REC_PUBLIC_INVALID;
-      return false;
-    }
     for (int k = 0; k < 8; k++) explicit_nonce[k] = ip[k];
     rc.n = len - 8 - tag_len;
     rc.src = ip + 8;
@@ -599,18 +730,39 @@ __global__ __launch_bounds__(kThreads, 1) void gcm_batch_kernel(BatchArgs a) {
       __syncthreads();
       cur = sid;
     }
-    if (usable) {
+    if (usable && RAW) {
+      const RecConsts none = {};
       for (uint32_t r = pos + wave; r < run_end; r += kWaves) {
         RecCtx rc;
-        int32_t* slot = a.status + r;
-        if (RAW) {
-          parse_raw<SEAL>(reinterpret_cast<const RawJob*>(a.descs)[r], S, rc);
-        } else {
-          if (!parse_tls<SEAL>(load_desc(reinterpret_cast<const tlsgpu_record*>(a.descs) + r), S, a.in, a.out,
-                               slot, lane, rc))
-            continue;
+        parse_raw<SEAL>(reinterpret_cast<const RawJob*>(a.descs)[r], S, rc);
+        gcm_record<SEAL, ROUNDS, false>(rc, S, none, a.status + r, lane, laneoff, gl);
+      }
+    } else if (usable) {
+      cu32* rk = as_const(S->rk);
+      cu32* rkr = as_const(S->rk_rot);
+      const tlsgpu_record* D = reinterpret_cast<const tlsgpu_record*>(a.descs);
+      // this wave's records are pos + wave + 16 j; constants for 64 of them at once
+      for (uint32_t chunk = pos + wave; chunk < run_end; chunk += kWaves * kWave) {
+        uint32_t j0[4];
+        lane_j0<SEAL>(D, chunk + kWaves * lane, run_end, S, a.in, j0);
+        const RecConsts mine = rec_consts<ROUNDS>(j0, rk, rkr, laneoff);
+        for (uint32_t j = 0; j < (uint32_t)kWave; j++) {
+          const uint32_t r = chunk + kWaves * j;
+          if (r >= run_end) break;
+          RecCtx rc;
+          int32_t* slot = a.status + r;
+          if (!parse_tls<SEAL>(load_desc(D + r), S, a.in, a.out, slot, lane, rc)) continue;
+          // parse_tls guarantees n <= TLSGPU_MAX_RECORD, so the counters
+          // 2..nb+1 stay below 2^16 and the FAST form applies
+          RecConsts rcc;
+#pragma unroll
+          for (int w = 0; w < 4; w++) rcc.ek0[w] = __builtin_amdgcn_readlane(mine.ek0[w], j);
+          rcc.k1a = __builtin_amdgcn_readlane(mine.k1a, j);
+          rcc.k1b = __builtin_amdgcn_readlane(mine.k1b, j);
+#pragma unroll
+          for (int w = 0; w < 4; w++) rcc.k2[w] = __builtin_amdgcn_readlane(mine.k2[w], j);
+          gcm_record<SEAL, ROUNDS, true>(rc, S, rcc, slot, lane, laneoff, gl);
         }
-        gcm_record<SEAL, ROUNDS>(rc, S, slot, lane, laneoff, gl);
       }
     }
     pos = run_end;

@@ -124,7 +124,10 @@ __global__ void install_sessions(DevSession* __restrict__ sessions,
   }
   uint32_t rk_be[60];
   s.rounds = (uint32_t)expand_key(p.key, (int)p.key_len, rk_be);
-  for (int k = 0; k < 4 * ((int)s.rounds + 1); k++) s.rk[k] = bswap32(rk_be[k]);
+  for (int k = 0; k < 4 * ((int)s.rounds + 1); k++) {
+    s.rk[k] = bswap32(rk_be[k]);
+    s.rk_rot[k] = __builtin_amdgcn_alignbit(s.rk[k], s.rk[k], 16);
+  }
   uint8_t hb[16] = {};
   aes_encrypt_bytes(rk_be, (int)s.rounds, hb);  // H = E_K(0^128)
   U128 H{0, 0};

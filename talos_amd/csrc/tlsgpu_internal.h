@@ -10,7 +10,7 @@ namespace tg {
 
 constexpr int kWave = 64;
 
-// Device session header (one per session id, 512 B, in HBM).  Mirrors the
+// Device session header (one per session id, 1 KiB, in HBM).  Mirrors the
 // per-direction state LibreSSL keeps in SSL_AEAD_CTX (ssl/ssl_locl.h:527-543)
 // plus the expanded key material aead_aes_gcm_init / _chacha20_poly1305_init
 // derive (e_aes.c:1372-1413, e_chacha20poly1305.c:52-79).
@@ -27,9 +27,11 @@ struct alignas(16) DevSession {
   uint32_t rk[60];            // AES round keys, little-endian column words
   uint8_t chacha_key[32];
   uint32_t h_le[4];           // H = E_K(0), little-endian words
-  uint32_t reserved[44];
+  uint32_t rk_rot[60];        // rotr16(rk[i]): round keys pre-rotated for the
+                              // xor3 + alignbit + xor3 column form
+  uint32_t reserved[112];
 };
-static_assert(sizeof(DevSession) == 512, "DevSession layout");
+static_assert(sizeof(DevSession) == 1024, "DevSession layout");
 
 // Per-session GHASH tables (GCM sessions only), 16-B aligned, in HBM.
 //   basis[p]      = K * x^p, K = H^64, p = 0..127 (little-endian words); a
