@@ -27,6 +27,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -90,36 +92,36 @@ def main():
     ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
     ap.add_argument("--records", type=int, default=0, help="override records per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", default="device", choices=["device", "host"],
+                    help="host: pinned host buffers + H2D/D2H overlap (PCIe-inclusive rate)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-
     import talos_amd as ta
+    from talos_amd.dist import ControlPlane, device_for, env_rank, shard_by_bytes
     from talos_amd.workload import Workload, zipf_lengths
 
+    world, rank, local = env_rank()
     ta.load_library()
-    eng = ta.Engine(local)   # first GPU runtime user in this process
-
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # gloo: control plane only (barrier / max)
-        dist.init_process_group("gloo")
+    eng = ta.Engine(device_for(local, ta.device_count()))  # first GPU runtime user
+    cp = ControlPlane(world)   # gloo control plane: barrier + max over ranks only
 
     kind_name, per_gpu, sessions, rec_len, seed, op = CONFIGS[args.config]
     if args.records:
         per_gpu = args.records
         sessions = max(1, min(sessions, per_gpu // 16))
     kind = ta.AEAD_NAMES[kind_name]
-    lengths = None
-    if rec_len is None:
-        lengths = zipf_lengths(per_gpu, seed + rank)
-    # weak scaling: rank r owns records [r*per_gpu, (r+1)*per_gpu) of the global batch
-    wl = Workload(eng, kind, per_gpu, sessions, seed ^ (rank * 0x100000001), lengths=lengths,
-                  record_len=rec_len or 0, index0=rank * per_gpu,
-                  tamper_every=1024 if op == "open" else 0)
+    # weak scaling: the global batch has world * per_gpu records; rank r owns a
+    # contiguous equal-byte slice, no data-path collective
+    glob = (np.full(world * per_gpu, rec_len, dtype=np.int64) if rec_len else
+            zipf_lengths(world * per_gpu, seed))
+    lo, hi = shard_by_bytes(glob, world, rank)
+    lengths = None if rec_len else glob[lo:hi]
+    wl = Workload(eng, kind, hi - lo, max(1, sessions * (hi - lo) // per_gpu),
+                  seed ^ (rank * 0x100000001), lengths=lengths, record_len=rec_len or 0,
+                  index0=lo, tamper_every=1024 if op == "open" else 0)
     total_len = int(wl.lengths.sum())
+    if args.mode == "host":
+        return host_mode(args, eng, wl, kind_name, total_len)
 
     def step(stream=None):
         if op == "open":
@@ -135,8 +137,7 @@ def main():
 
     def barrier():
         eng.sync()
-        if dist is not None:
-            dist.barrier()
+        cp.barrier()
 
     ev0, ev1 = ta.Event(eng), ta.Event(eng)
     barrier()
@@ -152,20 +153,14 @@ def main():
     barrier()
     wl.verify_open()
 
-    elapsed_s = dev_ms / 1e3
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed_s, wall_ms / 1e3], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed_s, wall_s = float(t[0]), float(t[1])
-    else:
-        wall_s = wall_ms / 1e3
+    elapsed_s, wall_s = cp.max([dev_ms / 1e3, wall_ms / 1e3])
+    total_payload = cp.sum([float(total_len)])[0]
 
-    payload = float(total_len) * world * args.steps          # plaintext bytes, all ranks
+    payload = total_payload * args.steps                      # plaintext bytes, all ranks
     value = payload / elapsed_s / GIB
     per_launch_s = dev_ms / 1e3 / args.steps / (2 if op == "seal+open" else 1)
     algo = sum(algo_bytes_per_record(kind_name, int(l), op) for l in
-               ([rec_len] * per_gpu if lengths is None else lengths.tolist()))
+               ([rec_len] * wl.n if lengths is None else lengths.tolist()))
     achieved = algo / per_launch_s / 1e9
     traffic, traffic_src = load_traffic(args.config)
 
@@ -203,8 +198,33 @@ def main():
     ev0.close()
     ev1.close()
     wl.free()
-    if dist is not None:
-        dist.destroy_process_group()
+    cp.close()
+    eng.close()
+
+
+def host_mode(args, eng, wl, kind_name, total_len):
+    """PCIe-inclusive rate: pinned host fragments in, pinned host plaintext out."""
+    import talos_amd as ta
+    from talos_amd.pipeline import HostPipeline
+    pipe = HostPipeline(wl)
+    for _ in range(max(1, args.warmup)):
+        pipe.run()
+    wl.verify_open()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pipe.run()
+    dt = time.perf_counter() - t0
+    for i in (0, wl.n // 2, wl.n - 1):
+        if not wl.tampered[i]:
+            assert pipe.host_plaintext(i) == wl.d_pt.download(int(wl.lengths[i]),
+                                                              int(wl.pt_off[i])).tobytes()
+    print(json.dumps({"metric": f"GiB/s host-resident {kind_name} TLS record open "
+                                "(pinned H2D + kernel + D2H, 4 streams, 32 chunks)",
+                      "value": round(total_len * args.steps / dt / GIB, 3), "unit": "GiB/s",
+                      "steps": args.steps, "records": wl.n,
+                      "ms_per_step": round(dt * 1e3 / args.steps, 3)}), flush=True)
+    pipe.close()
+    wl.free()
     eng.close()
 
 

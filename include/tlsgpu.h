@@ -95,6 +95,9 @@ typedef struct tlsgpu_session_params {
 typedef struct tlsgpu_engine tlsgpu_engine;
 typedef struct tlsgpu_sessions tlsgpu_sessions;
 
+/* Number of visible GPUs (0 when no device / no driver). */
+int tlsgpu_device_count(int *count);
+
 /* Engine = one GPU + one HIP stream + scratch pools. */
 int tlsgpu_engine_create(int device, tlsgpu_engine **out);
 void tlsgpu_engine_destroy(tlsgpu_engine *e);

@@ -99,6 +99,7 @@ def load_library(path: str = LIBPATH) -> C.CDLL:
     lib = C.CDLL(path, mode=os.RTLD_LOCAL | os.RTLD_NOW)
     vp, u32, u64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int
     sigs = {
+        "tlsgpu_device_count": (i32, [C.POINTER(i32)]),
         "tlsgpu_engine_create": (i32, [i32, C.POINTER(vp)]),
         "tlsgpu_engine_destroy": (None, [vp]),
         "tlsgpu_engine_stream": (vp, [vp]),
@@ -151,6 +152,12 @@ def _check(rc: int, what: str) -> None:
     if rc != 0:
         msg = load_library().tlsgpu_last_error()
         raise TlsGpuError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    rc = load_library().tlsgpu_device_count(C.byref(n))
+    return n.value if rc == 0 else 0
 
 
 class Engine:

@@ -63,6 +63,13 @@ struct tlsgpu_sessions {
   bool have[5];                // any session of kind k installed
 };
 
+extern "C" int tlsgpu_device_count(int* count) {
+  if (!count) return fail(TLSGPU_EINVAL, "null out");
+  *count = 0;
+  HIPCHK(hipGetDeviceCount(count));
+  return TLSGPU_OK;
+}
+
 extern "C" int tlsgpu_engine_create(int device, tlsgpu_engine** out) {
   if (!out) return fail(TLSGPU_EINVAL, "null out");
   *out = nullptr;

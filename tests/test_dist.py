@@ -1,0 +1,73 @@
+"""Multi-GPU control plane and batch split, exercised with gloo on the CPU
+(world_size 2), as SURVEY.md §8e prescribes: contiguous equal-byte shards, no
+data-path collective, barrier + max-over-ranks timing only."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from talos_amd.dist import ControlPlane, device_for, shard_by_bytes
+
+
+def test_shard_equal_records():
+    lens = np.full(524288, 16384)
+    cuts = [shard_by_bytes(lens, 8, r) for r in range(8)]
+    assert cuts[0] == (0, 65536) and cuts[-1] == (458752, 524288)
+    assert all(b - a == 65536 for a, b in cuts)
+
+
+def test_shard_zipf_balanced_and_disjoint():
+    from talos_amd.workload import zipf_lengths
+    lens = zipf_lengths(100000, seed=3)
+    for world in (2, 4, 8):
+        cuts = [shard_by_bytes(lens, world, r) for r in range(world)]
+        assert cuts[0][0] == 0 and cuts[-1][1] == len(lens)
+        assert all(cuts[i][1] == cuts[i + 1][0] for i in range(world - 1))
+        per = [int(lens[a:b].sum()) for a, b in cuts]
+        assert max(per) - min(per) <= 2 * 16384
+
+
+def test_device_for_wraps():
+    assert [device_for(r, 8) for r in range(8)] == list(range(8))
+    assert [device_for(r, 1) for r in range(4)] == [0, 0, 0, 0]
+    with pytest.raises(RuntimeError):
+        device_for(0, 0)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    cp = ControlPlane(world)
+    cp.barrier()
+    mx = cp.max([1.0 + rank, 10.0 - rank])
+    sm = cp.sum([float(rank)])
+    lens = np.full(1000, 1400)
+    lo, hi = shard_by_bytes(lens, world, rank)
+    cp.barrier()
+    cp.close()
+    q.put((rank, mx, sm, lo, hi))
+
+
+def test_gloo_world2_control_plane():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert [r[1] for r in res] == [[2.0, 10.0], [2.0, 10.0]]
+    assert [r[2] for r in res] == [[1.0], [1.0]]
+    assert [(r[3], r[4]) for r in res] == [(0, 500), (500, 1000)]
