@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Summarise a scripts/pmc.sh run into profiles/pmc_<name>.json.
+
+HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and
+WRITE_SIZE (KB) come from separate --pmc passes; on gfx950 FETCH_SIZE reports
+half the bytes of a wide coalesced streaming read, so it is doubled.
+usage: pmc_summary.py RUN_DIR KERNEL_PREFIX OUT_JSON [label]
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+run, prefix, out = sys.argv[1], sys.argv[2], sys.argv[3]
+label = sys.argv[4] if len(sys.argv) > 4 else ""
+vals = collections.defaultdict(list)
+durs = []
+for f in sorted(glob.glob(os.path.join(run, "pmc*", "pmc_counter_collection.csv"))):
+    for r in csv.DictReader(open(f)):
+        if r["Kernel_Name"].startswith(prefix):
+            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+for f in sorted(glob.glob(os.path.join(run, "pmc*", "pmc_kernel_trace.csv"))):
+    for r in csv.DictReader(open(f)):
+        if r["Kernel_Name"].startswith(prefix):
+            durs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+mean = {k: sum(v) / len(v) for k, v in vals.items()}
+res = {"kernel": prefix, "label": label, "launches_sampled": len(durs),
+       "mean_duration_ns_profiled": sum(durs) / len(durs) if durs else None,
+       "counters_per_launch_mean": mean}
+if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
+    res["hbm_read_bytes_per_launch"] = mean["FETCH_SIZE"] * 1024 * 2
+    res["hbm_write_bytes_per_launch"] = mean["WRITE_SIZE"] * 1024
+    res["hbm_bytes_per_launch"] = res["hbm_read_bytes_per_launch"] + res["hbm_write_bytes_per_launch"]
+    res["correction"] = "FETCH_SIZE x2 (gfx950 half-count of wide streaming reads), KB x1024"
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps(res, indent=1))
