@@ -88,6 +88,41 @@ __device__ __forceinline__ void aes_round(uint32_t& s0, uint32_t& s1, uint32_t& 
   s0 = t0; s1 = t1; s2 = t2; s3 = t3;
 }
 
+// Two independent blocks per call, written so the 32 lookups of a round are
+// issued together and the scheduler is told to keep them together: 32 address
+// perms, 32 DS reads, then the 24 combining ops (T19 sched_group_barrier).
+__device__ __forceinline__ void aes_round2(uint32_t (&a)[4], uint32_t (&b)[4], uint32_t k0,
+                                           uint32_t k1, uint32_t k2, uint32_t k3,
+                                           uint32_t laneoff) {
+  uint32_t ta[16], tb[16];
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    ta[4 * c + 0] = TE0(a[c], 0);
+    ta[4 * c + 1] = TE1(a[(c + 1) & 3], 1);
+    ta[4 * c + 2] = TE0(a[(c + 2) & 3], 2);
+    ta[4 * c + 3] = TE1(a[(c + 3) & 3], 3);
+  }
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    tb[4 * c + 0] = TE0(b[c], 0);
+    tb[4 * c + 1] = TE1(b[(c + 1) & 3], 1);
+    tb[4 * c + 2] = TE0(b[(c + 2) & 3], 2);
+    tb[4 * c + 3] = TE1(b[(c + 3) & 3], 3);
+  }
+  const uint32_t k[4] = {k0, k1, k2, k3};
+#pragma unroll
+  for (int c = 0; c < 4; c++)
+    a[c] = xor3(ta[4 * c], ta[4 * c + 1], rotl16(xor3(ta[4 * c + 2], ta[4 * c + 3], k[c])));
+#pragma unroll
+  for (int c = 0; c < 4; c++)
+    b[c] = xor3(tb[4 * c], tb[4 * c + 1], rotl16(xor3(tb[4 * c + 2], tb[4 * c + 3], k[c])));
+  __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);  // A addresses
+  __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);  // A lookups
+  __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);  // B addresses
+  __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);  // B lookups
+  __builtin_amdgcn_sched_group_barrier(0x002, 24, 0);  // combine
+}
+
 // Final round: SubBytes/ShiftRows only.  S[x] is byte 1 (and 2) of Te0_le[x]
 // and byte 3 of Te1_le[x].
 __device__ __forceinline__ uint32_t last_col(uint32_t a, uint32_t b, uint32_t c, uint32_t d,
@@ -197,6 +232,32 @@ __device__ __forceinline__ void aes_ctr16(uint32_t ks[4], uint32_t ctr, const Re
     aes_round(t0, t1, t2, t3, rkr[4 * r], rkr[4 * r + 1], rkr[4 * r + 2], rkr[4 * r + 3], laneoff);
   aes_last(t0, t1, t2, t3, rk + 4 * ROUNDS, laneoff);
   ks[0] = t0; ks[1] = t1; ks[2] = t2; ks[3] = t3;
+}
+
+// Two keystream blocks (counters c0, c1) with interleaved rounds.
+template <int ROUNDS>
+__device__ __forceinline__ void aes_ctr16x2(uint32_t ka[4], uint32_t kb[4], uint32_t c0,
+                                            uint32_t c1, const RecConsts& c, uint32_t rk03,
+                                            cu32* rk, cu32* rkr, uint32_t laneoff) {
+  const uint32_t va = bswap32(c0) ^ rk03, vb = bswap32(c1) ^ rk03;
+  const uint32_t a0 = c.k1a ^ rotl16(TE1(va, 3)), a1 = c.k1b ^ rotl16(TE0(va, 2));
+  const uint32_t b0 = c.k1a ^ rotl16(TE1(vb, 3)), b1 = c.k1b ^ rotl16(TE0(vb, 2));
+  uint32_t A[4], B[4];
+  A[0] = xor3(c.k2[0], TE0(a0, 0), TE1(a1, 1));
+  A[1] = xor3(c.k2[1], TE0(a1, 0), rotl16(TE1(a0, 3)));
+  A[2] = c.k2[2] ^ rotl16(TE0(a0, 2) ^ TE1(a1, 3));
+  A[3] = xor3(c.k2[3], TE1(a0, 1), rotl16(TE0(a1, 2)));
+  B[0] = xor3(c.k2[0], TE0(b0, 0), TE1(b1, 1));
+  B[1] = xor3(c.k2[1], TE0(b1, 0), rotl16(TE1(b0, 3)));
+  B[2] = c.k2[2] ^ rotl16(TE0(b0, 2) ^ TE1(b1, 3));
+  B[3] = xor3(c.k2[3], TE1(b0, 1), rotl16(TE0(b1, 2)));
+#pragma unroll
+  for (int r = 3; r < ROUNDS; r++)
+    aes_round2(A, B, rkr[4 * r], rkr[4 * r + 1], rkr[4 * r + 2], rkr[4 * r + 3], laneoff);
+  aes_last(A[0], A[1], A[2], A[3], rk + 4 * ROUNDS, laneoff);
+  aes_last(B[0], B[1], B[2], B[3], rk + 4 * ROUNDS, laneoff);
+#pragma unroll
+  for (int w = 0; w < 4; w++) { ka[w] = A[w]; kb[w] = B[w]; }
 }
 
 // ---------------------------------------------------------------------------
@@ -402,8 +463,12 @@ __device__ void gcm_record(const RecCtx& rc, const DevSession* __restrict__ S,
         load_block(rc.src + 16u * (i + 3 * kWave), 16, aligned, n1);
       }
       uint32_t k0[4], k1[4];
-      keystream(k0, ctr0 + i);
-      keystream(k1, ctr0 + i + kWave);
+      if (FAST) {
+        aes_ctr16x2<ROUNDS>(k0, k1, ctr0 + i, ctr0 + i + kWave, rcc, rk03, rk, rkr, laneoff);
+      } else {
+        keystream(k0, ctr0 + i);
+        keystream(k1, ctr0 + i + kWave);
+      }
       uint32_t o0[4] = {c0[0] ^ k0[0], c0[1] ^ k0[1], c0[2] ^ k0[2], c0[3] ^ k0[3]};
       uint32_t o1[4] = {c1[0] ^ k1[0], c1[1] ^ k1[1], c1[2] ^ k1[2], c1[3] ^ k1[3]};
       store_block(rc.dst + 16u * i, 16, aligned, o0);
