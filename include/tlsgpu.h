@@ -124,6 +124,20 @@ int tlsgpu_open_batch(tlsgpu_sessions *t, const tlsgpu_record *d_recs, uint32_t 
 int tlsgpu_seal_batch(tlsgpu_sessions *t, const tlsgpu_record *d_recs, uint32_t n,
     const uint8_t *d_in, uint8_t *d_out, int32_t *d_status, void *stream);
 
+/* GCM TLS batch kernel selection (process-wide; results are identical).
+ * TLSGPU_GCM_BITSLICE (default): bitsliced AES-CTR on the VALU for pairs of
+ * 16-byte-aligned records of >= 16 KiB in the same session run, LDS T-tables
+ * for everything else.  TLSGPU_GCM_TTABLE: T-tables only.  The environment
+ * variable TLSGPU_GCM_IMPL=bitslice|ttable sets the initial value. */
+enum tlsgpu_gcm_impl { TLSGPU_GCM_BITSLICE = 0, TLSGPU_GCM_TTABLE = 1 };
+int tlsgpu_set_gcm_impl(int impl);
+int tlsgpu_get_gcm_impl(void);
+
+/* Diagnostic: ECB-encrypt nblocks 16-byte blocks (device memory) under the
+ * AES key of GCM session `session` with the bitsliced AES core. */
+int tlsgpu_aes_ecb_bitsliced(tlsgpu_sessions *t, uint32_t session, const uint8_t *d_in,
+    uint8_t *d_out, uint32_t nblocks, void *stream);
+
 /* Deterministic synthetic bytes, counter-based SplitMix64 keyed by
  * (seed, index0 + i) for each of n spans of span_len bytes at d_out + i*stride
  * (same stream as the oracle's oracle_fill_bytes; used by bench/tests). */

@@ -112,6 +112,9 @@ def load_library(path: str = LIBPATH) -> C.CDLL:
         "tlsgpu_seal_batch": (i32, [vp, vp, u32, vp, vp, vp, vp]),
         "tlsgpu_fill_synthetic": (i32, [vp, vp, u64, u32, u32, u64, u64, vp]),
         "tlsgpu_last_error": (C.c_char_p, []),
+        "tlsgpu_set_gcm_impl": (i32, [i32]),
+        "tlsgpu_get_gcm_impl": (i32, []),
+        "tlsgpu_aes_ecb_bitsliced": (i32, [vp, u32, vp, vp, u32, vp]),
         "tlsgpu_malloc": (i32, [vp, C.c_size_t, C.POINTER(vp)]),
         "tlsgpu_free": (i32, [vp, vp]),
         "tlsgpu_host_alloc": (i32, [vp, C.c_size_t, C.POINTER(vp)]),
@@ -293,6 +296,27 @@ class SessionTable:
         if self.handle:
             self.lib.tlsgpu_sessions_destroy(self.handle)
             self.handle = None
+
+
+GCM_BITSLICE, GCM_TTABLE = 0, 1
+
+
+def set_gcm_impl(impl: int | str) -> None:
+    """Select the GCM TLS batch kernel (tlsgpu_set_gcm_impl): "bitslice" or "ttable"."""
+    if isinstance(impl, str):
+        impl = {"bitslice": GCM_BITSLICE, "ttable": GCM_TTABLE}[impl]
+    _check(load_library().tlsgpu_set_gcm_impl(impl), "tlsgpu_set_gcm_impl")
+
+
+def get_gcm_impl() -> str:
+    return "ttable" if load_library().tlsgpu_get_gcm_impl() == GCM_TTABLE else "bitslice"
+
+
+def aes_ecb_bitsliced(table: "SessionTable", session: int, d_in: int, d_out: int, nblocks: int,
+                      stream: int | None = None) -> None:
+    """Diagnostic: bitsliced AES-ECB of nblocks device blocks under a GCM session's key."""
+    _check(table.lib.tlsgpu_aes_ecb_bitsliced(table.handle, session, d_in, d_out, nblocks, stream),
+           "tlsgpu_aes_ecb_bitsliced")
 
 
 def len_type(length: int, rtype: int) -> int:

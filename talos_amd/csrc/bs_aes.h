@@ -22,14 +22,19 @@ namespace tg {
     asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:" #imm : "=v"(_d) : "v"(a), "v"(b), "v"(c)); \
     _d;                                                                              \
   })
+// same with a wave-uniform third operand in an SGPR (round-key words)
+#define bop3s(a, b, c, imm)                                                           \
+  ({                                                                                 \
+    uint32_t _d;                                                                     \
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:" #imm : "=v"(_d) : "v"(a), "v"(b), "s"(c)); \
+    _d;                                                                              \
+  })
 
 }  // namespace tg
 
 #include "bs_sbox.h"
 
 namespace tg {
-
-typedef __attribute__((address_space(4))) const uint32_t bs_cu32;
 
 // 16 S-boxes in place.
 __device__ __forceinline__ void bs_subbytes(uint32_t (&st)[128]) {
@@ -39,6 +44,9 @@ __device__ __forceinline__ void bs_subbytes(uint32_t (&st)[128]) {
     uint32_t o7, o6, o5, o4, o3, o2, o1, o0;
     TG_BS_SBOX(p[7], p[6], p[5], p[4], p[3], p[2], p[1], p[0], o7, o6, o5, o4, o3, o2, o1, o0);
     p[7] = o7; p[6] = o6; p[5] = o5; p[4] = o4; p[3] = o3; p[2] = o2; p[1] = o1; p[0] = o0;
+    // one S-box at a time: its ~40 temporaries die before the next starts
+    // (two waves per SIMD supply the issue parallelism, not interleaving)
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -57,99 +65,122 @@ __device__ __forceinline__ void bs_shiftrows(uint32_t (&st)[128]) {
   for (int i = 0; i < 128; i++) st[i] = t[i];
 }
 
-// MixColumns on one column (bytes a[0..3], 8 planes each) + AddRoundKey:
+// Round-key masks come from a KM policy: km.mask(r, i) = 0 or ~0, bit i
+// (= 8 * byte + bit) of round key r.  The kernels derive them with one SALU
+// s_bfe_i32 each from the round-key words, which sit in SGPRs.
+template <class KM>
+__device__ __forceinline__ void bs_masks8(const KM& km, int r, int i, uint32_t (&m)[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) m[k] = km.mask(r, i + k);
+}
+
+// One output plane of MixColumns + AddRoundKey:
 //   out_i = xtime(a_i ^ a_{i+1}) ^ a_{i+1} ^ (a_{i+2} ^ a_{i+3})
 // xtime on planes: x[0]=t[7], x[1]=t[0]^t[7], x[2]=t[1], x[3]=t[2]^t[7],
-// x[4]=t[3]^t[7], x[5]=t[4], x[6]=t[5], x[7]=t[6].
-__device__ __forceinline__ void bs_mixcolumn(uint32_t* a0, uint32_t* a1, uint32_t* a2,
-                                             uint32_t* a3, bs_cu32* km) {
-  uint32_t* a[4] = {a0, a1, a2, a3};
+// x[4]=t[3]^t[7], x[5]=t[4], x[6]=t[5], x[7]=t[6] (t_i = a_i ^ a_{i+1}).
+// Bits 1, 3, 4 take two bitop3 with the key mask folded in, the others one
+// bitop3 + one XOR.
+__device__ __forceinline__ uint32_t bs_mc_bit(const uint32_t (&t)[4][8], uint32_t n, int i, int k,
+                                              uint32_t km) {
+  const uint32_t t2 = t[(i + 2) & 3][k];
+  if (k == 1 || k == 3 || k == 4) return bop3s(bop3(t[i][k - 1], t[i][7], n, 0x96), t2, km, 0x96);
+  return bop3(k == 0 ? t[i][7] : t[i][k - 1], n, t2, 0x96) ^ km;
+}
+
+// MixColumns on column C (bytes a_i = st[32C + 8i + k]) + AddRoundKey of
+// round r.  Outputs are produced in the order 3, 0, 1, 2 so that each input
+// byte dies as soon as its last reader (out_{i-1} reads a_i) is done.
+template <int C, class KM>
+__device__ __forceinline__ void bs_mixcolumn(uint32_t (&st)[128], const KM& km, int r) {
   uint32_t t[4][8];
 #pragma unroll
   for (int i = 0; i < 4; i++)
 #pragma unroll
-    for (int k = 0; k < 8; k++) t[i][k] = a[i][k] ^ a[(i + 1) & 3][k];
-  uint32_t o[4][8];
+    for (int k = 0; k < 8; k++) t[i][k] = st[32 * C + 8 * i + k] ^ st[32 * C + 8 * ((i + 1) & 3) + k];
+  uint32_t m[8], o3[8];
+  bs_masks8(km, r, 32 * C + 24, m);
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const uint32_t* ti = t[i];
-    const uint32_t* t2 = t[(i + 2) & 3];
-    const uint32_t* n = a[(i + 1) & 3];
+  for (int k = 0; k < 8; k++) o3[k] = bs_mc_bit(t, st[32 * C + k], 3, k, m[k]);
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      uint32_t v;
-      if (k == 1 || k == 3 || k == 4)
-        v = bop3(bop3(ti[k - 1], ti[7], n[k], 0x96), t2[k], km[8 * i + k], 0x96);
-      else
-        v = bop3(k == 0 ? ti[7] : ti[k - 1], n[k], t2[k], 0x96) ^ km[8 * i + k];
-      o[i][k] = v;
-    }
+  for (int i = 0; i < 3; i++) {
+    bs_masks8(km, r, 32 * C + 8 * i, m);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      st[32 * C + 8 * i + k] = bs_mc_bit(t, st[32 * C + 8 * (i + 1) + k], i, k, m[k]);
   }
 #pragma unroll
-  for (int i = 0; i < 4; i++)
-#pragma unroll
-    for (int k = 0; k < 8; k++) a[i][k] = o[i][k];
+  for (int k = 0; k < 8; k++) st[32 * C + 24 + k] = o3[k];
 }
 
-__device__ __forceinline__ void bs_ark(uint32_t (&st)[128], bs_cu32* km) {
+template <class KM>
+__device__ __forceinline__ void bs_ark(uint32_t (&st)[128], const KM& km, int r) {
 #pragma unroll
-  for (int i = 0; i < 128; i++) st[i] ^= km[i];
+  for (int i = 0; i < 128; i += 8) {
+    uint32_t m[8];
+    bs_masks8(km, r, i, m);
+#pragma unroll
+    for (int k = 0; k < 8; k++) st[i + k] ^= m[k];
+  }
 }
 
-// Full encryption of the 32 blocks in `st` with bitsliced round-key masks
-// rkm[r*128 + 8*b + k] (0 or 0xFFFFFFFF).  The final AddRoundKey is left to
-// the caller (it folds into the ciphertext XOR on normal-layout words) when
-// skip_last_ark is set.
-template <int ROUNDS, bool SKIP_LAST_ARK>
-__device__ __forceinline__ void bs_encrypt(uint32_t (&st)[128], bs_cu32* rkm) {
-  bs_ark(st, rkm);
+// Full encryption of the 32 blocks in `st`.  The final AddRoundKey is left to
+// the caller when SKIP_LAST_ARK (it folds into the ciphertext XOR on
+// normal-layout words).
+template <int ROUNDS, bool SKIP_LAST_ARK, class KM>
+__device__ __forceinline__ void bs_encrypt(uint32_t (&st)[128], const KM& km) {
+  bs_ark(st, km, 0);
 #pragma unroll 1
   for (int r = 1; r < ROUNDS; r++) {
     bs_subbytes(st);
     bs_shiftrows(st);
-#pragma unroll
-    for (int c = 0; c < 4; c++)
-      bs_mixcolumn(st + 32 * c, st + 32 * c + 8, st + 32 * c + 16, st + 32 * c + 24,
-                   rkm + 128 * r + 32 * c);
+    bs_mixcolumn<0>(st, km, r);
+    bs_mixcolumn<1>(st, km, r);
+    bs_mixcolumn<2>(st, km, r);
+    bs_mixcolumn<3>(st, km, r);
   }
   bs_subbytes(st);
   bs_shiftrows(st);
-  if (!SKIP_LAST_ARK) bs_ark(st, rkm + 128 * ROUNDS);
+  if (!SKIP_LAST_ARK) bs_ark(st, km, ROUNDS);
 }
 
-// 32x32 bit transpose of x[0..31] in place (x[i] bit j <-> x[j] bit i).
+// 32x32 bit transpose of st[O..O+31] in place (x[i] bit j <-> x[j] bit i).
 // Stages 16 and 8 are byte moves (v_perm_b32), stages 4/2/1 swap-moves.
-__device__ __forceinline__ void transpose32(uint32_t* x) {
-  // stage 16: swap the high half of x[i] with the low half of x[i+16]
+template <int S, int O>
+__device__ __forceinline__ void transpose_stage(uint32_t (&x)[128]) {
 #pragma unroll
-  for (int i = 0; i < 16; i++) {
-    uint32_t a = x[i], b = x[i + 16];
-    x[i] = __builtin_amdgcn_perm(b, a, 0x05040100u);       // [a.lo16, b.lo16]
-    x[i + 16] = __builtin_amdgcn_perm(b, a, 0x07060302u);  // [a.hi16, b.hi16]
-  }
-  // stage 8
+  for (int g = 0; g < 32; g += 2 * S)
 #pragma unroll
-  for (int g = 0; g < 32; g += 16)
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      uint32_t a = x[g + i], b = x[g + i + 8];
-      x[g + i] = __builtin_amdgcn_perm(b, a, 0x06020400u);      // [a0, b0, a2, b2]
-      x[g + i + 8] = __builtin_amdgcn_perm(b, a, 0x07030501u);  // [a1, b1, a3, b3]
-    }
-  // stages 4, 2, 1
-#pragma unroll
-  for (int s = 4; s >= 1; s >>= 1) {
-    const uint32_t m = s == 4 ? 0x0F0F0F0Fu : s == 2 ? 0x33333333u : 0x55555555u;
-#pragma unroll
-    for (int g = 0; g < 32; g += 2 * s)
-#pragma unroll
-      for (int i = 0; i < s; i++) {
-        uint32_t a = x[g + i], b = x[g + i + s];
-        uint32_t t = ((a >> s) ^ b) & m;
-        x[g + i + s] = b ^ t;
-        x[g + i] = a ^ (t << s);
+    for (int i = 0; i < S; i++) {
+      const uint32_t a = x[O + g + i], b = x[O + g + i + S];
+      if (S == 16) {
+        x[O + g + i] = __builtin_amdgcn_perm(b, a, 0x05040100u);      // [a.lo16, b.lo16]
+        x[O + g + i + S] = __builtin_amdgcn_perm(b, a, 0x07060302u);  // [a.hi16, b.hi16]
+      } else if (S == 8) {
+        x[O + g + i] = __builtin_amdgcn_perm(b, a, 0x06020400u);      // [a0, b0, a2, b2]
+        x[O + g + i + S] = __builtin_amdgcn_perm(b, a, 0x07030501u);  // [a1, b1, a3, b3]
+      } else {
+        const uint32_t m = S == 4 ? 0x0F0F0F0Fu : S == 2 ? 0x33333333u : 0x55555555u;
+        const uint32_t t = ((a >> S) ^ b) & m;
+        x[O + g + i + S] = b ^ t;
+        x[O + g + i] = a ^ (t << S);
       }
-  }
+    }
+}
+
+template <int O>
+__device__ __forceinline__ void transpose32(uint32_t (&x)[128]) {
+  transpose_stage<16, O>(x);
+  transpose_stage<8, O>(x);
+  transpose_stage<4, O>(x);
+  transpose_stage<2, O>(x);
+  transpose_stage<1, O>(x);
+}
+
+__device__ __forceinline__ void transpose_all(uint32_t (&x)[128]) {
+  transpose32<0>(x);
+  transpose32<32>(x);
+  transpose32<64>(x);
+  transpose32<96>(x);
 }
 
 }  // namespace tg

@@ -178,6 +178,35 @@ extern "C" int tlsgpu_sessions_install(tlsgpu_sessions* t, uint32_t first, uint3
   return TLSGPU_OK;
 }
 
+static int initial_gcm_impl() {
+  const char* v = getenv("TLSGPU_GCM_IMPL");
+  if (v && strcmp(v, "ttable") == 0) return TLSGPU_GCM_TTABLE;
+  return TLSGPU_GCM_BITSLICE;
+}
+static std::atomic<int> g_gcm_impl{initial_gcm_impl()};
+
+extern "C" int tlsgpu_set_gcm_impl(int impl) {
+  if (impl != TLSGPU_GCM_BITSLICE && impl != TLSGPU_GCM_TTABLE)
+    return fail(TLSGPU_EINVAL, "unknown gcm impl %d", impl);
+  g_gcm_impl.store(impl);
+  return TLSGPU_OK;
+}
+extern "C" int tlsgpu_get_gcm_impl(void) { return g_gcm_impl.load(); }
+
+extern "C" int tlsgpu_aes_ecb_bitsliced(tlsgpu_sessions* t, uint32_t session, const uint8_t* d_in,
+                                        uint8_t* d_out, uint32_t nblocks, void* stream) {
+  if (!t || (nblocks && (!d_in || !d_out))) return fail(TLSGPU_EINVAL, "bad arguments");
+  if (session >= t->capacity ||
+      (t->kinds[session] != TLSGPU_AES_128_GCM && t->kinds[session] != TLSGPU_AES_256_GCM))
+    return fail(TLSGPU_EINVAL, "session %u is not an installed AES-GCM session", session);
+  HIPCHK(hipSetDevice(t->eng->device));
+  int rounds = t->kinds[session] == TLSGPU_AES_128_GCM ? 10 : 14;
+  if (launch_bs_ecb(t->d_sess, session, rounds, d_in, d_out, nblocks,
+                    stream ? (hipStream_t)stream : t->eng->stream))
+    return fail(TLSGPU_EHIP, "bs ecb launch: %s", hipGetErrorString(hipGetLastError()));
+  return TLSGPU_OK;
+}
+
 static int groups_for(const tlsgpu_engine* e, uint32_t n, uint32_t* per_group) {
   // one persistent 16-wave workgroup per CU, contiguous record ranges
   uint32_t groups = (uint32_t)e->num_cus;
@@ -202,10 +231,15 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   int groups = groups_for(t->eng, n, &a.records_per_group);
   // records whose session is empty/invalid keep this status
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)d_status, (int)TLSGPU_REC_PUBLIC_INVALID, n, s));
-  if (t->have[TLSGPU_AES_128_GCM] && launch_gcm(a, seal, raw, 10, groups, s))
-    return fail(TLSGPU_EHIP, "gcm-128 launch: %s", hipGetErrorString(hipGetLastError()));
-  if (t->have[TLSGPU_AES_256_GCM] && launch_gcm(a, seal, raw, 14, groups, s))
-    return fail(TLSGPU_EHIP, "gcm-256 launch: %s", hipGetErrorString(hipGetLastError()));
+  const bool bs = !raw && g_gcm_impl.load() == TLSGPU_GCM_BITSLICE;
+  for (int rounds : {10, 14}) {
+    if (!t->have[rounds == 10 ? TLSGPU_AES_128_GCM : TLSGPU_AES_256_GCM]) continue;
+    int rc = bs ? launch_gcm_bs(a, seal, rounds, groups, s)
+                : launch_gcm(a, seal, raw, rounds, groups, s);
+    if (rc)
+      return fail(TLSGPU_EHIP, "gcm-%d launch: %s", rounds == 10 ? 128 : 256,
+                  hipGetErrorString(hipGetLastError()));
+  }
   if ((t->have[TLSGPU_CHACHA20_POLY1305] || t->have[TLSGPU_CHACHA20_POLY1305_OLD]) &&
       launch_chacha(a, seal, raw, groups, s))
     return fail(TLSGPU_EHIP, "chacha launch: %s", hipGetErrorString(hipGetLastError()));

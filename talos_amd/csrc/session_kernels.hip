@@ -139,6 +139,10 @@ __global__ void install_sessions(DevSession* __restrict__ sessions,
   sessions[id] = s;
 
   DevGcmTables* t = &tables[id];
+  for (int r = 0; r <= (int)s.rounds; r++)
+    for (int b = 0; b < 16; b++)
+      for (int k = 0; k < 8; k++)
+        t->bsrk[r][8 * b + k] = 0u - ((s.rk[4 * r + b / 4] >> (8 * (b % 4) + k)) & 1u);
   U128 pw = H;  // H^e
   U128 k64{0, 0};
   for (int e = 1; e <= kPowMax; e++) {

@@ -39,12 +39,15 @@ static_assert(sizeof(DevSession) == 1024, "DevSession layout");
 //                   T[j][b] = (b at byte j) * K in LDS.
 //   shoup[e-1][v] = v * H^e for nibble v (Shoup 4-bit, gcm128.c:255-324
 //                   layout: v's MSB is x^0), e = 1..65, big-endian words.
+//   bsrk[r][8b+k] = 0 or ~0: bit k of byte b of round key r, the AddRoundKey
+//                   masks of the bitsliced AES path (bs_aes.h), read by s_load.
 constexpr int kPowMax = 65;
 struct alignas(16) DevGcmTables {
   uint32_t basis[128][4];
   uint32_t shoup[kPowMax][16][4];
+  uint32_t bsrk[15][128];
 };
-static_assert(sizeof(DevGcmTables) == 2048 + kPowMax * 256, "DevGcmTables layout");
+static_assert(sizeof(DevGcmTables) == 2048 + kPowMax * 256 + 15 * 512, "DevGcmTables layout");
 
 // Raw AEAD job: one EVP_AEAD_CTX_seal/open call (arbitrary nonce / AAD), used
 // by the per-call drop-in path.  Pointers are device pointers.
@@ -75,6 +78,9 @@ struct BatchArgs {
 namespace tg {
 int launch_gcm(const BatchArgs& a, bool seal, bool raw, int rounds, int groups,
                hipStream_t s);
+int launch_gcm_bs(const BatchArgs& a, bool seal, int rounds, int groups, hipStream_t s);
+int launch_bs_ecb(const DevSession* sessions, uint32_t session, int rounds, const void* d_in,
+                  void* d_out, uint32_t nblocks, hipStream_t s);
 int launch_chacha(const BatchArgs& a, bool seal, bool raw, int groups, hipStream_t s);
 int launch_session_install(DevSession* sessions, DevGcmTables* tables,
                            const tlsgpu_session_params* d_params, uint32_t first,

@@ -181,6 +181,68 @@ def test_batch_seal_open_all_lengths(ta, engine, oracle, name):
     _run_seal_open(ta, engine, oracle, [KINDS[name]] * 3, LENGTHS, seed=11)
 
 
+@pytest.fixture
+def gcm_impl(ta):
+    """Run a test under one GCM kernel and restore the default afterwards."""
+    prev = ta.get_gcm_impl()
+    yield lambda impl: ta.set_gcm_impl(impl)
+    ta.set_gcm_impl(prev)
+
+
+@pytest.mark.parametrize("impl", ["bitslice", "ttable"])
+@pytest.mark.parametrize("name", ["aes-128-gcm", "aes-256-gcm"])
+def test_batch_gcm_impls_all_lengths(ta, engine, oracle, gcm_impl, impl, name):
+    gcm_impl(impl)
+    _run_seal_open(ta, engine, oracle, [KINDS[name]] * 2, LENGTHS, seed=21)
+
+
+# Long records: pairs of >= 16 KiB aligned records take the bitsliced passes
+# (1024 blocks each); remainders and unpaired / misaligned records the T-tables.
+BS_LENGTHS = [16384, 16384, 32768, 40000, 16384, 16400, 50000, 16384, 16384, 100, 16384,
+              16384, 65536 + 17, 16384, 16384]
+
+
+@pytest.mark.parametrize("shift", [0, 3])
+@pytest.mark.parametrize("name", ["aes-128-gcm", "aes-256-gcm"])
+def test_batch_bitsliced_long_records(ta, engine, oracle, gcm_impl, name, shift):
+    gcm_impl("bitslice")
+    _run_seal_open(ta, engine, oracle, [KINDS[name]] * 2, BS_LENGTHS, seed=22,
+                   in_shift=shift, out_shift=shift)
+
+
+@pytest.mark.parametrize("name", ["aes-128-gcm", "aes-256-gcm"])
+def test_bitsliced_aes_core_ecb(ta, engine, oracle, name):
+    """The bitsliced AES core against the oracle's AES (aes_core.c) on random
+    blocks, plus the FIPS-197 C.1 / C.3 known answers."""
+    rnd = random.Random(31)
+    kind = KINDS[name]
+    klen = po.KEY_LEN[kind]
+    fips_key = bytes(range(klen))
+    fips_pt = bytes.fromhex("00112233445566778899aabbccddeeff")
+    fips_ct = {16: "69c4e0d86a7b0430d8cdb78070b4c55a",
+               32: "8ea2b7ca516745bfeafc49904b496089"}[klen]
+    keys = [fips_key] + [bytes(rnd.getrandbits(8) for _ in range(klen)) for _ in range(2)]
+    table = ta.SessionTable(engine, len(keys))
+    table.install(0, [ta.SessionParams(kind, k, bytes(4)) for k in keys])
+    nblocks = 2048 + 37   # a partial lane group at the end
+    for sid, key in enumerate(keys):
+        blocks = bytearray(rnd.getrandbits(8) for _ in range(16 * nblocks))
+        blocks[:16] = fips_pt
+        d_in = ta.DeviceBuffer(engine, len(blocks))
+        d_out = ta.DeviceBuffer(engine, len(blocks))
+        d_in.upload(bytes(blocks))
+        ta.aes_ecb_bitsliced(table, sid, d_in.ptr, d_out.ptr, nblocks)
+        engine.sync()
+        got = d_out.download().tobytes()
+        if sid == 0:
+            assert got[:16].hex() == fips_ct
+        for b in range(0, nblocks, 97):
+            assert got[16 * b:16 * b + 16] == oracle.aes_encrypt(key, bytes(blocks[16 * b:16 * b + 16])), b
+        d_in.free()
+        d_out.free()
+    table.close()
+
+
 @pytest.mark.parametrize("name", ["aes-128-gcm", "chacha20-poly1305"])
 def test_batch_misaligned(ta, engine, oracle, name):
     _run_seal_open(ta, engine, oracle, [KINDS[name]] * 2, [0, 5, 16, 33, 1400, 4099],
