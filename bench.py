@@ -139,6 +139,9 @@ def main():
         eng.sync()
         cp.barrier()
 
+    phase = bool(os.environ.get("TLSGPU_PHASE_STATS"))
+    if phase:
+        ta.debug_phase_stats(eng, reset=True)
     ev0, ev1 = ta.Event(eng), ta.Event(eng)
     barrier()
     t0 = time.perf_counter()
@@ -150,6 +153,15 @@ def main():
     t1 = time.perf_counter()
     dev_ms = ev0.elapsed_ms(ev1)
     wall_ms = (t1 - t0) * 1e3
+    if phase:  # diagnostic: per-phase shader cycles of the hybrid kernel, per step
+        st = ta.debug_phase_stats(eng, reset=True)
+        names = {1: "bs-aes", 2: "bs-consume", 3: "bs-finish", 4: "bs-barrier", 5: "tables",
+                 9: "tt-x4", 10: "tt-rest", 11: "tt-finish", 12: "tt-barrier"}
+        for i, nm in names.items():
+            if st[2 * i + 1]:
+                print(f"phase {nm:11s} cycles/step {st[2*i]/args.steps:14.0f} events/step "
+                      f"{st[2*i+1]/args.steps:9.0f} cycles/event {st[2*i]/st[2*i+1]:9.0f}",
+                      file=sys.stderr)
     barrier()
     wl.verify_open()
 

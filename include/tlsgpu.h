@@ -125,13 +125,27 @@ int tlsgpu_seal_batch(tlsgpu_sessions *t, const tlsgpu_record *d_recs, uint32_t 
     const uint8_t *d_in, uint8_t *d_out, int32_t *d_status, void *stream);
 
 /* GCM TLS batch kernel selection (process-wide; results are identical).
- * TLSGPU_GCM_BITSLICE (default): bitsliced AES-CTR on the VALU for pairs of
- * 16-byte-aligned records of >= 16 KiB in the same session run, LDS T-tables
- * for everything else.  TLSGPU_GCM_TTABLE: T-tables only.  The environment
- * variable TLSGPU_GCM_IMPL=bitslice|ttable sets the initial value. */
-enum tlsgpu_gcm_impl { TLSGPU_GCM_BITSLICE = 0, TLSGPU_GCM_TTABLE = 1 };
+ * TLSGPU_GCM_QUEUE (default): a prep pass computes every record's E_K(J0) and
+ * round-1/2 constants, then 16 T-table waves per CU (AES rounds as LDS
+ * lookups) pull records from a per-session-run queue.
+ * TLSGPU_GCM_TTABLE: T-table waves with in-kernel constants, static split.
+ * TLSGPU_GCM_HYBRID: 4 bitsliced waves (AES-CTR on the VALU, pairs of
+ * 16-byte-aligned records of >= 16 KiB) beside 4 T-table waves per CU.
+ * TLSGPU_GCM_BITSLICE: 8 bitsliced waves per CU.
+ * The environment variable TLSGPU_GCM_IMPL=queue|ttable|hybrid|bitslice sets
+ * the initial value.  The per-call EVP path always uses TTABLE. */
+enum tlsgpu_gcm_impl {
+  TLSGPU_GCM_BITSLICE = 0, TLSGPU_GCM_TTABLE = 1, TLSGPU_GCM_HYBRID = 2, TLSGPU_GCM_QUEUE = 3
+};
 int tlsgpu_set_gcm_impl(int impl);
 int tlsgpu_get_gcm_impl(void);
+
+/* Diagnostic: hybrid-kernel phase timing.  With TLSGPU_PHASE_STATS=1 in the
+ * environment, the first call allocates 32 device counters (shader cycles and
+ * event counts per phase, summed over waves) that later hybrid launches fill;
+ * each call synchronizes the device, copies them to out32 (may be NULL) and
+ * optionally resets them.  Fails when the variable is not set. */
+int tlsgpu_debug_phase_stats(tlsgpu_engine *e, unsigned long long *out32, int reset);
 
 /* Diagnostic: ECB-encrypt nblocks 16-byte blocks (device memory) under the
  * AES key of GCM session `session` with the bitsliced AES core. */

@@ -115,6 +115,7 @@ def load_library(path: str = LIBPATH) -> C.CDLL:
         "tlsgpu_set_gcm_impl": (i32, [i32]),
         "tlsgpu_get_gcm_impl": (i32, []),
         "tlsgpu_aes_ecb_bitsliced": (i32, [vp, u32, vp, vp, u32, vp]),
+        "tlsgpu_debug_phase_stats": (i32, [vp, C.POINTER(C.c_ulonglong), i32]),
         "tlsgpu_malloc": (i32, [vp, C.c_size_t, C.POINTER(vp)]),
         "tlsgpu_free": (i32, [vp, vp]),
         "tlsgpu_host_alloc": (i32, [vp, C.c_size_t, C.POINTER(vp)]),
@@ -298,18 +299,29 @@ class SessionTable:
             self.handle = None
 
 
-GCM_BITSLICE, GCM_TTABLE = 0, 1
+GCM_BITSLICE, GCM_TTABLE, GCM_HYBRID, GCM_QUEUE = 0, 1, 2, 3
+_GCM_IMPLS = {"bitslice": GCM_BITSLICE, "ttable": GCM_TTABLE, "hybrid": GCM_HYBRID,
+              "queue": GCM_QUEUE}
 
 
 def set_gcm_impl(impl: int | str) -> None:
-    """Select the GCM TLS batch kernel (tlsgpu_set_gcm_impl): "bitslice" or "ttable"."""
+    """Select the GCM TLS batch kernel (tlsgpu_set_gcm_impl): queue|ttable|hybrid|bitslice."""
     if isinstance(impl, str):
-        impl = {"bitslice": GCM_BITSLICE, "ttable": GCM_TTABLE}[impl]
+        impl = _GCM_IMPLS[impl]
     _check(load_library().tlsgpu_set_gcm_impl(impl), "tlsgpu_set_gcm_impl")
 
 
 def get_gcm_impl() -> str:
-    return "ttable" if load_library().tlsgpu_get_gcm_impl() == GCM_TTABLE else "bitslice"
+    v = load_library().tlsgpu_get_gcm_impl()
+    return {i: n for n, i in _GCM_IMPLS.items()}[v]
+
+
+def debug_phase_stats(engine: "Engine", reset: bool = True) -> list[int]:
+    """Diagnostic (TLSGPU_PHASE_STATS=1): 16 x (cycles, events) of the hybrid kernel's phases."""
+    out = (C.c_ulonglong * 32)()
+    _check(engine.lib.tlsgpu_debug_phase_stats(engine.handle, out, int(reset)),
+           "tlsgpu_debug_phase_stats")
+    return list(out)
 
 
 def aes_ecb_bitsliced(table: "SessionTable", session: int, d_in: int, d_out: int, nblocks: int,

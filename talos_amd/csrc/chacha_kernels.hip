@@ -291,6 +291,7 @@ __global__ __launch_bounds__(256) void chacha_batch_kernel(BatchArgs a) {
   uint32_t tag_len;
   if (RAW) {
     const RawJob j = reinterpret_cast<const RawJob*>(a.descs)[r];
+    if (j.session >= a.n_sessions) return;
     S = a.sessions + j.session;
     uint32_t kind = S->kind;
     if (kind != TLSGPU_CHACHA20_POLY1305 && kind != TLSGPU_CHACHA20_POLY1305_OLD) return;
@@ -324,6 +325,7 @@ __global__ __launch_bounds__(256) void chacha_batch_kernel(BatchArgs a) {
     rc.zero_len = j.max_out;
   } else {
     const tlsgpu_record d = reinterpret_cast<const tlsgpu_record*>(a.descs)[r];
+    if (d.session >= a.n_sessions) return;  // status stays PUBLIC_INVALID
     S = a.sessions + d.session;
     uint32_t kind = S->kind;
     if (kind != TLSGPU_CHACHA20_POLY1305 && kind != TLSGPU_CHACHA20_POLY1305_OLD) return;

@@ -181,12 +181,14 @@ extern "C" int tlsgpu_sessions_install(tlsgpu_sessions* t, uint32_t first, uint3
 static int initial_gcm_impl() {
   const char* v = getenv("TLSGPU_GCM_IMPL");
   if (v && strcmp(v, "ttable") == 0) return TLSGPU_GCM_TTABLE;
-  return TLSGPU_GCM_BITSLICE;
+  if (v && strcmp(v, "bitslice") == 0) return TLSGPU_GCM_BITSLICE;
+  if (v && strcmp(v, "hybrid") == 0) return TLSGPU_GCM_HYBRID;
+  return TLSGPU_GCM_QUEUE;
 }
 static std::atomic<int> g_gcm_impl{initial_gcm_impl()};
 
 extern "C" int tlsgpu_set_gcm_impl(int impl) {
-  if (impl != TLSGPU_GCM_BITSLICE && impl != TLSGPU_GCM_TTABLE)
+  if (impl < TLSGPU_GCM_BITSLICE || impl > TLSGPU_GCM_QUEUE)
     return fail(TLSGPU_EINVAL, "unknown gcm impl %d", impl);
   g_gcm_impl.store(impl);
   return TLSGPU_OK;
@@ -218,6 +220,37 @@ static int groups_for(const tlsgpu_engine* e, uint32_t n, uint32_t* per_group) {
   return (int)groups;
 }
 
+static uint32_t initial_bs_reserve() {
+  const char* v = getenv("TLSGPU_BS_RESERVE");
+  long r = v ? strtol(v, nullptr, 10) : 12;
+  return (uint32_t)(r < 2 ? 2 : r);
+}
+static uint32_t g_bs_reserve = initial_bs_reserve();
+// Diagnostic phase timing of the hybrid kernel (TLSGPU_PHASE_STATS=1): 32
+// counters in device memory, read with tlsgpu_debug_phase_stats.
+static unsigned long long* g_phase_stats = nullptr;
+static int g_phase_stats_dev = -1;
+extern "C" int tlsgpu_debug_phase_stats(tlsgpu_engine* e, unsigned long long* out32, int reset) {
+  if (!e) return fail(TLSGPU_EINVAL, "null engine");
+  HIPCHK(hipSetDevice(e->device));
+  if (!g_phase_stats) {
+    const char* v = getenv("TLSGPU_PHASE_STATS");
+    if (!v || !*v || *v == '0') return fail(TLSGPU_EINVAL, "TLSGPU_PHASE_STATS not set");
+    HIPCHK(hipMalloc((void**)&g_phase_stats, 64 * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(g_phase_stats, 0, 64 * sizeof(unsigned long long)));
+    g_phase_stats_dev = e->device;
+  }
+  HIPCHK(hipDeviceSynchronize());
+  if (out32) HIPCHK(hipMemcpy(out32, g_phase_stats, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  if (reset) HIPCHK(hipMemset(g_phase_stats, 0, 64 * sizeof(unsigned long long)));
+  return TLSGPU_OK;
+}
+
+static uint32_t g_hy_flags = []() {
+  const char* v = getenv("TLSGPU_HY_FLAGS");
+  return v ? (uint32_t)strtoul(v, nullptr, 0) & 7u : 0u;
+}();
+
 static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const uint8_t* d_in,
                      uint8_t* d_out, int32_t* d_status, hipStream_t s, bool seal, bool raw) {
   BatchArgs a;
@@ -228,18 +261,39 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   a.in = d_in;
   a.out = d_out;
   a.status = d_status;
+  a.n_sessions = t->capacity;
+  a.bs_reserve = g_bs_reserve;
+  a.hy_flags = g_hy_flags;
+  a.dbg = g_phase_stats;
   int groups = groups_for(t->eng, n, &a.records_per_group);
   // records whose session is empty/invalid keep this status
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)d_status, (int)TLSGPU_REC_PUBLIC_INVALID, n, s));
-  const bool bs = !raw && g_gcm_impl.load() == TLSGPU_GCM_BITSLICE;
+  const int impl = raw ? TLSGPU_GCM_TTABLE : g_gcm_impl.load();
+  RecPre* pre = nullptr;  // per-record constants of the queue kernels, stream-ordered
+  if (impl != TLSGPU_GCM_TTABLE && (t->have[TLSGPU_AES_128_GCM] || t->have[TLSGPU_AES_256_GCM]))
+    HIPCHK(hipMallocAsync((void**)&pre, sizeof(RecPre) * (size_t)n, s));
   for (int rounds : {10, 14}) {
     if (!t->have[rounds == 10 ? TLSGPU_AES_128_GCM : TLSGPU_AES_256_GCM]) continue;
-    int rc = bs ? launch_gcm_bs(a, seal, rounds, groups, s)
-                : launch_gcm(a, seal, raw, rounds, groups, s);
-    if (rc)
+    int rc;
+    if (impl == TLSGPU_GCM_TTABLE) {
+      rc = launch_gcm(a, seal, raw, rounds, groups, s);
+    } else {
+      rc = launch_gcm_prep(a, pre, seal, rounds, s);
+      if (rc == 0) {
+        if (impl == TLSGPU_GCM_QUEUE)
+          rc = launch_gcm_queue(a, pre, seal, rounds, groups, s);
+        else
+          rc = (rounds == 10 ? launch_gcm_hy10 : launch_gcm_hy14)(
+              a, pre, seal, impl == TLSGPU_GCM_HYBRID ? 4 : 8, groups, s);
+      }
+    }
+    if (rc) {
+      if (pre) (void)hipFreeAsync(pre, s);
       return fail(TLSGPU_EHIP, "gcm-%d launch: %s", rounds == 10 ? 128 : 256,
                   hipGetErrorString(hipGetLastError()));
+    }
   }
+  if (pre) HIPCHK(hipFreeAsync(pre, s));
   if ((t->have[TLSGPU_CHACHA20_POLY1305] || t->have[TLSGPU_CHACHA20_POLY1305_OLD]) &&
       launch_chacha(a, seal, raw, groups, s))
     return fail(TLSGPU_EHIP, "chacha launch: %s", hipGetErrorString(hipGetLastError()));

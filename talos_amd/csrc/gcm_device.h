@@ -1,0 +1,1079 @@
+// gcm_device.h — device-side building blocks shared by the AES-GCM kernels
+// (gcm_kernels.hip: T-table batch kernel; gcm_bs_kernels.hip: bitsliced and
+// hybrid kernels).  Layout and mapping notes: gcm_kernels.hip header and
+// DESIGN.md §4.  Each translation unit gets its own copy of the LDS array.
+#pragma once
+#include <utility>
+
+#include "aes_common.h"
+#include "bs_aes.h"
+#include "tlsgpu_internal.h"
+
+namespace tg {
+
+static __device__ const WordTable g_te0 = kTe0;
+
+constexpr int kThreads = 1024;
+constexpr int kWaves = kThreads / kWave;
+constexpr uint32_t AES_OFF = 0;
+constexpr uint32_t KT_OFF = 65536;
+constexpr uint32_t SH_OFF = 131072;
+constexpr uint32_t R4_OFF = SH_OFF + kPowMax * 256;
+constexpr uint32_t Q_OFF = R4_OFF + 64;      // hybrid kernel: per-run record queue
+constexpr uint32_t DBG_OFF = Q_OFF + 16;     // hybrid kernel: phase counters (diagnostic)
+constexpr uint32_t LDS_BYTES = DBG_OFF + 32 * 8;
+
+__shared__ __attribute__((aligned(16))) uint8_t s_lds[LDS_BYTES];
+
+// Wave-uniform data (session header, round keys, descriptors) is read through
+// the constant address space so it lands in SGPRs via s_load.
+typedef __attribute__((address_space(4))) const uint32_t cu32;
+template <typename T>
+__device__ __forceinline__ cu32* as_const(const T* p) { return (cu32*)(p); }
+
+// ---------------------------------------------------------------------------
+// LDS access helpers
+__device__ __forceinline__ uint32_t lds_u32(uint32_t off) {
+  return *reinterpret_cast<const uint32_t*>(s_lds + off);
+}
+__device__ __forceinline__ uint4 lds_u128(uint32_t off) {
+  return *reinterpret_cast<const uint4*>(s_lds + off);
+}
+
+// address of Te0[byte r of w] for this lane: [0, 0, byte, lane bank]
+template <int R>
+__device__ __forceinline__ uint32_t taddr(uint32_t w, uint32_t laneoff) {
+  return __builtin_amdgcn_perm(w, laneoff, 0x0C0C0000u | ((4u + R) << 8));
+}
+__device__ __forceinline__ uint32_t rotl16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
+// three-input XOR in one VALU op: v_bitop3_b32 with truth table 0x96 (gfx950
+// has no v_xor3_b32; hipcc does not form bitop3 from these ^ chains)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t d;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
+#define TE0(w, r) lds_u32(AES_OFF + taddr<r>((w), laneoff))
+#define TE1(w, r) lds_u32(AES_OFF + 128 + taddr<r>((w), laneoff))
+
+// One full AES round on little-endian columns (ShiftRows: row r of output
+// column c comes from input column c+r).  kr_c = rotr16(k_c) is folded into the
+// rotated half so a column costs xor3 + alignbit + xor3:
+//   t = Te0[a] ^ Te1[b] ^ rotl16(Te0[c] ^ Te1[d] ^ rotr16(k))
+__device__ __forceinline__ void aes_round(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3,
+                                          uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3,
+                                          uint32_t laneoff) {
+  uint32_t t0 = xor3(TE0(s0, 0), TE1(s1, 1), rotl16(xor3(TE0(s2, 2), TE1(s3, 3), k0)));
+  uint32_t t1 = xor3(TE0(s1, 0), TE1(s2, 1), rotl16(xor3(TE0(s3, 2), TE1(s0, 3), k1)));
+  uint32_t t2 = xor3(TE0(s2, 0), TE1(s3, 1), rotl16(xor3(TE0(s0, 2), TE1(s1, 3), k2)));
+  uint32_t t3 = xor3(TE0(s3, 0), TE1(s0, 1), rotl16(xor3(TE0(s1, 2), TE1(s2, 3), k3)));
+  s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+}
+
+// Two independent blocks per call, written so the 32 lookups of a round are
+// issued together and the scheduler is told to keep them together: 32 address
+// perms, 32 DS reads, then the 24 combining ops (T19 sched_group_barrier).
+__device__ __forceinline__ void aes_round2(uint32_t (&a)[4], uint32_t (&b)[4], uint32_t k0,
+                                           uint32_t k1, uint32_t k2, uint32_t k3,
+                                           uint32_t laneoff) {
+  uint32_t ta[16], tb[16];
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    ta[4 * c + 0] = TE0(a[c], 0);
+    ta[4 * c + 1] = TE1(a[(c + 1) & 3], 1);
+    ta[4 * c + 2] = TE0(a[(c + 2) & 3], 2);
+    ta[4 * c + 3] = TE1(a[(c + 3) & 3], 3);
+  }
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    tb[4 * c + 0] = TE0(b[c], 0);
+    tb[4 * c + 1] = TE1(b[(c + 1) & 3], 1);
+    tb[4 * c + 2] = TE0(b[(c + 2) & 3], 2);
+    tb[4 * c + 3] = TE1(b[(c + 3) & 3], 3);
+  }
+  const uint32_t k[4] = {k0, k1, k2, k3};
+#pragma unroll
+  for (int c = 0; c < 4; c++)
+    a[c] = xor3(ta[4 * c], ta[4 * c + 1], rotl16(xor3(ta[4 * c + 2], ta[4 * c + 3], k[c])));
+#pragma unroll
+  for (int c = 0; c < 4; c++)
+    b[c] = xor3(tb[4 * c], tb[4 * c + 1], rotl16(xor3(tb[4 * c + 2], tb[4 * c + 3], k[c])));
+  __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);  // A addresses
+  __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);  // A lookups
+  __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);  // B addresses
+  __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);  // B lookups
+  __builtin_amdgcn_sched_group_barrier(0x002, 24, 0);  // combine
+}
+
+// Final round: SubBytes/ShiftRows only.  S[x] is byte 1 (and 2) of Te0_le[x]
+// and byte 3 of Te1_le[x].
+__device__ __forceinline__ uint32_t last_col(uint32_t a, uint32_t b, uint32_t c, uint32_t d,
+                                             uint32_t k, uint32_t laneoff) {
+  uint32_t lo = __builtin_amdgcn_perm(TE0(b, 1), TE0(a, 0), 0x0C0C0501u);
+  uint32_t hi = __builtin_amdgcn_perm(TE1(d, 3), TE0(c, 2), 0x07020C0Cu);
+  return lo ^ hi ^ k;
+}
+__device__ __forceinline__ void aes_last(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3,
+                                         cu32* rk, uint32_t laneoff) {
+  uint32_t t0 = last_col(s0, s1, s2, s3, rk[0], laneoff);
+  uint32_t t1 = last_col(s1, s2, s3, s0, rk[1], laneoff);
+  uint32_t t2 = last_col(s2, s3, s0, s1, rk[2], laneoff);
+  uint32_t t3 = last_col(s3, s0, s1, s2, rk[3], laneoff);
+  s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+}
+
+// Full block encryption (used for E_K(J0)).
+template <int ROUNDS>
+__device__ __forceinline__ void aes_block(uint32_t s[4], cu32* rk, cu32* rkr,
+                                          uint32_t laneoff) {
+  s[0] ^= rk[0]; s[1] ^= rk[1]; s[2] ^= rk[2]; s[3] ^= rk[3];
+#pragma unroll
+  for (int r = 1; r < ROUNDS; r++)
+    aes_round(s[0], s[1], s[2], s[3], rkr[4 * r], rkr[4 * r + 1], rkr[4 * r + 2], rkr[4 * r + 3],
+              laneoff);
+  aes_last(s[0], s[1], s[2], s[3], rk + 4 * ROUNDS, laneoff);
+}
+
+// Per-record CTR constants: J0 columns 0..2 through AddRoundKey 0 and the
+// constant three quarters of round 1 (only column 3 carries the counter).
+struct CtrConst { uint32_t k1[4]; uint32_t rk03; };
+
+__device__ __forceinline__ CtrConst ctr_setup(const uint32_t j0[4], cu32* rk,
+                                              uint32_t laneoff) {
+  uint32_t s0 = j0[0] ^ rk[0], s1 = j0[1] ^ rk[1], s2 = j0[2] ^ rk[2];
+  CtrConst c;
+  c.k1[0] = TE0(s0, 0) ^ TE1(s1, 1) ^ rotl16(TE0(s2, 2)) ^ rk[4];
+  c.k1[1] = TE0(s1, 0) ^ TE1(s2, 1) ^ rotl16(TE1(s0, 3)) ^ rk[5];
+  c.k1[2] = TE0(s2, 0) ^ rotl16(TE0(s0, 2) ^ TE1(s1, 3)) ^ rk[6];
+  c.k1[3] = TE1(s0, 1) ^ rotl16(TE0(s1, 2) ^ TE1(s2, 3)) ^ rk[7];
+  c.rk03 = rk[3];
+  return c;
+}
+
+// Keystream block for 32-bit counter value ctr (big-endian in bytes 12..15),
+// general form: only round 1 is shortened.
+template <int ROUNDS>
+__device__ __forceinline__ void aes_ctr(uint32_t ks[4], uint32_t ctr, const CtrConst& c,
+                                        cu32* rk, cu32* rkr, uint32_t laneoff) {
+  uint32_t v = bswap32(ctr) ^ c.rk03;
+  uint32_t s0 = c.k1[0] ^ rotl16(TE1(v, 3));
+  uint32_t s1 = c.k1[1] ^ rotl16(TE0(v, 2));
+  uint32_t s2 = c.k1[2] ^ TE1(v, 1);
+  uint32_t s3 = c.k1[3] ^ TE0(v, 0);
+#pragma unroll
+  for (int r = 2; r < ROUNDS; r++)
+    aes_round(s0, s1, s2, s3, rkr[4 * r], rkr[4 * r + 1], rkr[4 * r + 2], rkr[4 * r + 3], laneoff);
+  aes_last(s0, s1, s2, s3, rk + 4 * ROUNDS, laneoff);
+  ks[0] = s0; ks[1] = s1; ks[2] = s2; ks[3] = s3;
+}
+
+// Per-record constants for counters below 2^16 (every TLS record: the counter
+// runs 2..nb+1 with nb <= 65534).  Counter bytes 12-13 are then zero, so after
+// round 1 only columns 0 and 1 depend on the counter and round 2 needs 8
+// lookups instead of 16; E_K(J0) rides along.  Computed for 64 records at a
+// time (one per lane) and broadcast with readlane when a record is processed.
+struct RecConsts {
+  uint32_t ek0[4];   // E_K(J0)
+  uint32_t k1a, k1b; // round-1 constants of columns 0, 1
+  uint32_t k2[4];    // round-2 constants
+};
+
+template <int ROUNDS>
+__device__ __forceinline__ RecConsts rec_consts(const uint32_t j0[4], cu32* rk, cu32* rkr,
+                                                uint32_t laneoff) {
+  RecConsts r;
+  uint32_t e[4] = {j0[0], j0[1], j0[2], j0[3]};
+  aes_block<ROUNDS>(e, rk, rkr, laneoff);
+  r.ek0[0] = e[0]; r.ek0[1] = e[1]; r.ek0[2] = e[2]; r.ek0[3] = e[3];
+  CtrConst c = ctr_setup(j0, rk, laneoff);
+  const uint32_t v0 = c.rk03;           // counter bytes 12..15 = 0 (bytes 12,13 stay 0)
+  const uint32_t s2 = c.k1[2] ^ TE1(v0, 1);
+  const uint32_t s3 = c.k1[3] ^ TE0(v0, 0);
+  r.k1a = c.k1[0];
+  r.k1b = c.k1[1];
+  r.k2[0] = rotl16(TE0(s2, 2) ^ TE1(s3, 3)) ^ rk[8];
+  r.k2[1] = TE1(s2, 1) ^ rotl16(TE0(s3, 2)) ^ rk[9];
+  r.k2[2] = TE0(s2, 0) ^ TE1(s3, 1) ^ rk[10];
+  r.k2[3] = TE0(s3, 0) ^ rotl16(TE1(s2, 3)) ^ rk[11];
+  return r;
+}
+
+// Fast keystream for ctr < 2^16: round 1 = 2 lookups, round 2 = 8 lookups.
+template <int ROUNDS>
+__device__ __forceinline__ void aes_ctr16(uint32_t ks[4], uint32_t ctr, const RecConsts& c,
+                                          uint32_t rk03, cu32* rk, cu32* rkr, uint32_t laneoff) {
+  const uint32_t v = bswap32(ctr) ^ rk03;
+  const uint32_t s0 = c.k1a ^ rotl16(TE1(v, 3));
+  const uint32_t s1 = c.k1b ^ rotl16(TE0(v, 2));
+  uint32_t t0 = xor3(c.k2[0], TE0(s0, 0), TE1(s1, 1));
+  uint32_t t1 = xor3(c.k2[1], TE0(s1, 0), rotl16(TE1(s0, 3)));
+  uint32_t t2 = c.k2[2] ^ rotl16(TE0(s0, 2) ^ TE1(s1, 3));
+  uint32_t t3 = xor3(c.k2[3], TE1(s0, 1), rotl16(TE0(s1, 2)));
+#pragma unroll
+  for (int r = 3; r < ROUNDS; r++)
+    aes_round(t0, t1, t2, t3, rkr[4 * r], rkr[4 * r + 1], rkr[4 * r + 2], rkr[4 * r + 3], laneoff);
+  aes_last(t0, t1, t2, t3, rk + 4 * ROUNDS, laneoff);
+  ks[0] = t0; ks[1] = t1; ks[2] = t2; ks[3] = t3;
+}
+
+// Two keystream blocks (counters c0, c1) with interleaved rounds.
+template <int ROUNDS>
+__device__ __forceinline__ void aes_ctr16x2(uint32_t ka[4], uint32_t kb[4], uint32_t c0,
+                                            uint32_t c1, const RecConsts& c, uint32_t rk03,
+                                            cu32* rk, cu32* rkr, uint32_t laneoff) {
+  const uint32_t va = bswap32(c0) ^ rk03, vb = bswap32(c1) ^ rk03;
+  const uint32_t a0 = c.k1a ^ rotl16(TE1(va, 3)), a1 = c.k1b ^ rotl16(TE0(va, 2));
+  const uint32_t b0 = c.k1a ^ rotl16(TE1(vb, 3)), b1 = c.k1b ^ rotl16(TE0(vb, 2));
+  uint32_t A[4], B[4];
+  A[0] = xor3(c.k2[0], TE0(a0, 0), TE1(a1, 1));
+  A[1] = xor3(c.k2[1], TE0(a1, 0), rotl16(TE1(a0, 3)));
+  A[2] = c.k2[2] ^ rotl16(TE0(a0, 2) ^ TE1(a1, 3));
+  A[3] = xor3(c.k2[3], TE1(a0, 1), rotl16(TE0(a1, 2)));
+  B[0] = xor3(c.k2[0], TE0(b0, 0), TE1(b1, 1));
+  B[1] = xor3(c.k2[1], TE0(b1, 0), rotl16(TE1(b0, 3)));
+  B[2] = c.k2[2] ^ rotl16(TE0(b0, 2) ^ TE1(b1, 3));
+  B[3] = xor3(c.k2[3], TE1(b0, 1), rotl16(TE0(b1, 2)));
+#pragma unroll
+  for (int r = 3; r < ROUNDS; r++)
+    aes_round2(A, B, rkr[4 * r], rkr[4 * r + 1], rkr[4 * r + 2], rkr[4 * r + 3], laneoff);
+  aes_last(A[0], A[1], A[2], A[3], rk + 4 * ROUNDS, laneoff);
+  aes_last(B[0], B[1], B[2], B[3], rk + 4 * ROUNDS, laneoff);
+#pragma unroll
+  for (int w = 0; w < 4; w++) { ka[w] = A[w]; kb[w] = B[w]; }
+}
+
+// ---------------------------------------------------------------------------
+// GHASH helpers
+struct GhLane {
+  bool c2, c1;       // word-rotation selects for m = lane % 16
+  uint32_t r;        // byte rotation
+  uint32_t cq[4];    // slot bytes: cq[q].byte[i] = ((4q + i + m) & 15) * 16
+};
+
+__device__ __forceinline__ GhLane gh_lane(uint32_t lane) {
+  GhLane g;
+  uint32_t m = lane & 15;
+  g.c2 = (m >> 3) & 1;
+  g.c1 = (m >> 2) & 1;
+  g.r = m & 3;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) v |= (((4 * q + i + m) & 15) << 4) << (8 * i);
+    g.cq[q] = v;
+  }
+  return g;
+}
+
+template <int K>
+__device__ __forceinline__ uint32_t kaddr(uint32_t y, uint32_t cq) {
+  return __builtin_amdgcn_perm(y, cq, 0x0C0C0000u | ((4u + K) << 8) | K);
+}
+
+// out = x * H^64 using the LDS byte-position table (LE words).
+__device__ __forceinline__ void mul_k(const uint32_t x[4], uint32_t o[4], const GhLane& g) {
+  uint32_t a0 = g.c2 ? x[2] : x[0], a1 = g.c2 ? x[3] : x[1];
+  uint32_t a2 = g.c2 ? x[0] : x[2], a3 = g.c2 ? x[1] : x[3];
+  uint32_t b0 = g.c1 ? a1 : a0, b1 = g.c1 ? a2 : a1, b2 = g.c1 ? a3 : a2, b3 = g.c1 ? a0 : a3;
+  uint32_t y[4];
+  y[0] = __builtin_amdgcn_alignbyte(b1, b0, g.r);
+  y[1] = __builtin_amdgcn_alignbyte(b2, b1, g.r);
+  y[2] = __builtin_amdgcn_alignbyte(b3, b2, g.r);
+  y[3] = __builtin_amdgcn_alignbyte(b0, b3, g.r);
+  uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    uint4 v0 = lds_u128(KT_OFF + kaddr<0>(y[q], g.cq[q]));
+    uint4 v1 = lds_u128(KT_OFF + kaddr<1>(y[q], g.cq[q]));
+    uint4 v2 = lds_u128(KT_OFF + kaddr<2>(y[q], g.cq[q]));
+    uint4 v3 = lds_u128(KT_OFF + kaddr<3>(y[q], g.cq[q]));
+    acc.x = xor3(acc.x, xor3(v0.x, v1.x, v2.x), v3.x);
+    acc.y = xor3(acc.y, xor3(v0.y, v1.y, v2.y), v3.y);
+    acc.z = xor3(acc.z, xor3(v0.z, v1.z, v2.z), v3.z);
+    acc.w = xor3(acc.w, xor3(v0.w, v1.w, v2.w), v3.w);
+  }
+  o[0] = acc.x; o[1] = acc.y; o[2] = acc.z; o[3] = acc.w;
+}
+
+// Two independent chains at once: o_a = x_a * H^64, o_b = x_b * H^64, with all
+// 32 lookups issued before any is combined (the chains' latencies overlap).
+__device__ __forceinline__ void mul_k2(const uint32_t xa[4], const uint32_t xb[4], uint32_t oa[4],
+                                       uint32_t ob[4], const GhLane& g) {
+  uint32_t addr[2][16];
+  const uint32_t* xs[2] = {xa, xb};
+#pragma unroll
+  for (int c = 0; c < 2; c++) {
+    const uint32_t* x = xs[c];
+    uint32_t a0 = g.c2 ? x[2] : x[0], a1 = g.c2 ? x[3] : x[1];
+    uint32_t a2 = g.c2 ? x[0] : x[2], a3 = g.c2 ? x[1] : x[3];
+    uint32_t b0 = g.c1 ? a1 : a0, b1 = g.c1 ? a2 : a1, b2 = g.c1 ? a3 : a2, b3 = g.c1 ? a0 : a3;
+    uint32_t y[4];
+    y[0] = __builtin_amdgcn_alignbyte(b1, b0, g.r);
+    y[1] = __builtin_amdgcn_alignbyte(b2, b1, g.r);
+    y[2] = __builtin_amdgcn_alignbyte(b3, b2, g.r);
+    y[3] = __builtin_amdgcn_alignbyte(b0, b3, g.r);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      addr[c][4 * q + 0] = KT_OFF + kaddr<0>(y[q], g.cq[q]);
+      addr[c][4 * q + 1] = KT_OFF + kaddr<1>(y[q], g.cq[q]);
+      addr[c][4 * q + 2] = KT_OFF + kaddr<2>(y[q], g.cq[q]);
+      addr[c][4 * q + 3] = KT_OFF + kaddr<3>(y[q], g.cq[q]);
+    }
+  }
+  // two halves of 8 lookups per chain: at most 16 reads (64 VGPRs) in flight
+  uint4 acc[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    uint4 v[2][8];
+#pragma unroll
+    for (int m = 0; m < 8; m++) {
+      v[0][m] = lds_u128(addr[0][8 * h + m]);
+      v[1][m] = lds_u128(addr[1][8 * h + m]);
+    }
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      uint4 t;
+      t.x = xor3(v[c][0].x, v[c][1].x, v[c][2].x);
+      t.y = xor3(v[c][0].y, v[c][1].y, v[c][2].y);
+      t.z = xor3(v[c][0].z, v[c][1].z, v[c][2].z);
+      t.w = xor3(v[c][0].w, v[c][1].w, v[c][2].w);
+#pragma unroll
+      for (int m = 3; m < 7; m += 2) {
+        t.x = xor3(t.x, v[c][m].x, v[c][m + 1].x);
+        t.y = xor3(t.y, v[c][m].y, v[c][m + 1].y);
+        t.z = xor3(t.z, v[c][m].z, v[c][m + 1].z);
+        t.w = xor3(t.w, v[c][m].w, v[c][m + 1].w);
+      }
+      if (h == 0) {
+        acc[c].x = t.x ^ v[c][7].x; acc[c].y = t.y ^ v[c][7].y;
+        acc[c].z = t.z ^ v[c][7].z; acc[c].w = t.w ^ v[c][7].w;
+      } else {
+        acc[c].x = xor3(acc[c].x, t.x, v[c][7].x); acc[c].y = xor3(acc[c].y, t.y, v[c][7].y);
+        acc[c].z = xor3(acc[c].z, t.z, v[c][7].z); acc[c].w = xor3(acc[c].w, t.w, v[c][7].w);
+      }
+    }
+  }
+  oa[0] = acc[0].x; oa[1] = acc[0].y; oa[2] = acc[0].z; oa[3] = acc[0].w;
+  ob[0] = acc[1].x; ob[1] = acc[1].y; ob[2] = acc[1].z; ob[3] = acc[1].w;
+}
+
+// z = x * H^e (Shoup 4-bit, gcm128.c:333-393), all in big-endian words.
+__device__ __forceinline__ void mul_shoup(const uint32_t X[4], uint32_t e, uint32_t Z[4]) {
+  const uint32_t base = SH_OFF + (e - 1) * 256;
+  uint32_t n0 = X[3] & 0xF;
+  uint4 m = lds_u128(base + n0 * 16);
+  uint32_t z0 = m.x, z1 = m.y, z2 = m.z, z3 = m.w;
+#pragma unroll
+  for (int k = 1; k < 32; k++) {
+    uint32_t nib = (X[3 - k / 8] >> (4 * (k % 8))) & 0xF;
+    uint32_t rem = z3 & 0xF;
+    z3 = __builtin_amdgcn_alignbit(z2, z3, 4);
+    z2 = __builtin_amdgcn_alignbit(z1, z2, 4);
+    z1 = __builtin_amdgcn_alignbit(z0, z1, 4);
+    z0 = (z0 >> 4) ^ lds_u32(R4_OFF + rem * 4);
+    uint4 t = lds_u128(base + nib * 16);
+    z0 ^= t.x; z1 ^= t.y; z2 ^= t.z; z3 ^= t.w;
+  }
+  Z[0] = z0; Z[1] = z1; Z[2] = z2; Z[3] = z3;
+}
+
+// Two independent Shoup multiplies, interleaved; e == 0 gives zero.
+__device__ __forceinline__ void mul_shoup2(const uint32_t A[4], uint32_t ea, uint32_t ZA[4],
+                                           const uint32_t B[4], uint32_t eb, uint32_t ZB[4]) {
+  // empty chains (e == 0) read the H^1 table and are masked to zero at the end
+  const uint32_t base_a = SH_OFF + (ea ? ea - 1 : 0) * 256, base_b = SH_OFF + (eb ? eb - 1 : 0) * 256;
+  const uint32_t ma = ea ? 0xFFFFFFFFu : 0u, mb = eb ? 0xFFFFFFFFu : 0u;
+  uint4 m = lds_u128(base_a + (A[3] & 0xF) * 16);
+  uint4 n = lds_u128(base_b + (B[3] & 0xF) * 16);
+  uint32_t a0 = m.x, a1 = m.y, a2 = m.z, a3 = m.w;
+  uint32_t b0 = n.x, b1 = n.y, b2 = n.z, b3 = n.w;
+#pragma unroll
+  for (int k = 1; k < 32; k++) {
+    const uint32_t na = (A[3 - k / 8] >> (4 * (k % 8))) & 0xF;
+    const uint32_t nb = (B[3 - k / 8] >> (4 * (k % 8))) & 0xF;
+    const uint32_t ra = a3 & 0xF, rb = b3 & 0xF;
+    const uint4 ta = lds_u128(base_a + na * 16), tb = lds_u128(base_b + nb * 16);
+    const uint32_t qa = lds_u32(R4_OFF + ra * 4), qb = lds_u32(R4_OFF + rb * 4);
+    a3 = __builtin_amdgcn_alignbit(a2, a3, 4);
+    a2 = __builtin_amdgcn_alignbit(a1, a2, 4);
+    a1 = __builtin_amdgcn_alignbit(a0, a1, 4);
+    a0 = (a0 >> 4) ^ qa;
+    b3 = __builtin_amdgcn_alignbit(b2, b3, 4);
+    b2 = __builtin_amdgcn_alignbit(b1, b2, 4);
+    b1 = __builtin_amdgcn_alignbit(b0, b1, 4);
+    b0 = (b0 >> 4) ^ qb;
+    a0 ^= ta.x; a1 ^= ta.y; a2 ^= ta.z; a3 ^= ta.w;
+    b0 ^= tb.x; b1 ^= tb.y; b2 ^= tb.z; b3 ^= tb.w;
+  }
+  ZA[0] = a0 & ma; ZA[1] = a1 & ma; ZA[2] = a2 & ma; ZA[3] = a3 & ma;
+  ZB[0] = b0 & mb; ZB[1] = b1 & mb; ZB[2] = b2 & mb; ZB[3] = b3 & mb;
+}
+
+// Serial GHASH over a byte string with H (all lanes redundantly, rare path:
+// non-96-bit IVs and RAW-mode AAD).  x is big-endian words.  When final_mul
+// is false the last block is only XORed in (no trailing multiply).
+__device__ void ghash_serial(uint32_t x[4], const uint8_t* p, uint64_t len, bool final_mul) {
+  for (uint64_t off = 0; off < len; off += 16) {
+    uint32_t b[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      if (off + k < len) b[k >> 2] |= (uint32_t)p[off + k] << (24 - 8 * (k & 3));
+    x[0] ^= b[0]; x[1] ^= b[1]; x[2] ^= b[2]; x[3] ^= b[3];
+    if (off + 16 < len || final_mul) {
+      uint32_t z[4];
+      mul_shoup(x, 1, z);
+      x[0] = z[0]; x[1] = z[1]; x[2] = z[2]; x[3] = z[3];
+    }
+  }
+}
+
+__device__ __forceinline__ void be_from_le(const uint32_t* l, uint32_t* b) {
+  b[0] = bswap32(l[0]); b[1] = bswap32(l[1]); b[2] = bswap32(l[2]); b[3] = bswap32(l[3]);
+}
+
+// ---------------------------------------------------------------------------
+// Memory helpers (records are byte-aligned in general).
+__device__ __forceinline__ uint32_t load_u32_bytes(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+__device__ __forceinline__ void load_block(const uint8_t* p, uint32_t nbytes, bool aligned,
+                                           uint32_t v[4]) {
+  if (aligned && nbytes == 16) {
+    uint4 t = *reinterpret_cast<const uint4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else {
+    v[0] = v[1] = v[2] = v[3] = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++)
+      if (k < nbytes) v[k >> 2] |= (uint32_t)p[k] << (8 * (k & 3));
+  }
+}
+
+__device__ __forceinline__ void store_block(uint8_t* p, uint32_t nbytes, bool aligned,
+                                            const uint32_t v[4]) {
+  if (nbytes == 16 && aligned) {
+    *reinterpret_cast<uint4*>(p) = make_uint4(v[0], v[1], v[2], v[3]);
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++)
+      if (k < nbytes) p[k] = (uint8_t)(v[k >> 2] >> (8 * (k & 3)));
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// Per-record context after parsing (TLS descriptor or raw job).
+struct RecCtx {
+  const uint8_t* src;     // open: ciphertext ; seal: plaintext
+  uint8_t* dst;           // open: plaintext  ; seal: ciphertext
+  const uint8_t* tag_in;  // open: received tag (tag_len bytes)
+  uint32_t tag_byte;      // open: tag_in[lane] for lane < tag_len, loaded at parse
+                          // time so the tag check never waits on HBM
+  uint8_t* tag_out;       // seal: where the tag goes
+  uint32_t n;             // plaintext length
+  uint32_t j0[4];         // J0 (LE words)
+  uint32_t aad_be[4];     // AAD' = Horner of the AAD blocks without the final
+                          // multiply (gcm128.c:826-881 folded), BE words
+  uint64_t aad_len;       // bytes of AAD (for the lengths block)
+  uint64_t zero_len;      // bytes of dst zero-filled on failure
+  int32_t ok_status;      // status written on success
+};
+
+// Close the lane chains of a record: the lengths block BE64(aad bits) ||
+// BE64(ct bits) joins lane (nb % 64)'s chain at j = nb (gcm128.c:1477-1500),
+// then each lane's value still needs the weight H^e, e = nb + 1 - (index of
+// the chain's last element).  Returns the BE chain value and e (0 = empty).
+__device__ __forceinline__ uint32_t gcm_close_chain(const RecCtx& rc, uint32_t (&x)[4],
+                                                    uint32_t (&xb)[4], uint32_t lane,
+                                                    const GhLane& gl) {
+  const uint32_t n = rc.n;
+  const uint32_t nb = (n + 15) >> 4;
+  const uint32_t lstar = nb & 63;
+  uint32_t xk[4];
+  mul_k(x, xk, gl);
+  if (lane == lstar) {
+    uint64_t ab = rc.aad_len * 8, cb = (uint64_t)n * 8;
+    x[0] = xk[0] ^ bswap32((uint32_t)(ab >> 32));
+    x[1] = xk[1] ^ bswap32((uint32_t)ab);
+    x[2] = xk[2] ^ bswap32((uint32_t)(cb >> 32));
+    x[3] = xk[3] ^ bswap32((uint32_t)cb);
+  }
+  int32_t jlast;
+  if (lane == lstar) {
+    jlast = (int32_t)nb;
+  } else if (lane < nb) {
+    jlast = (int32_t)(lane + ((nb - 1 - lane) & ~63u));
+  } else {
+    jlast = (rc.aad_len != 0 && lane == 63) ? -1 : -2;  // -2: empty chain
+  }
+  be_from_le(x, xb);
+  return jlast == -2 ? 0u : (uint32_t)((int32_t)nb + 1 - jlast);
+}
+
+// Sum the weighted lane values across the wave, form the tag (GHASH ^ E_K(J0))
+// and check it (open, constant time over the tag bytes, zero-fill on failure:
+// e_aes.c:1492-1506, evp_aead.c:137-143) or write it (seal, e_aes.c:1452-1456).
+template <bool SEAL>
+__device__ __forceinline__ void gcm_tag(const RecCtx& rc, uint32_t (&y)[4], const uint32_t ek0[4],
+                                        const DevSession* __restrict__ S, int32_t* status_slot,
+                                        uint32_t lane) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    y[0] ^= __shfl_xor(y[0], m);
+    y[1] ^= __shfl_xor(y[1], m);
+    y[2] ^= __shfl_xor(y[2], m);
+    y[3] ^= __shfl_xor(y[3], m);
+  }
+  // tag = GHASH ^ E_K(J0)  (y is BE words, ek0 LE words)
+  uint32_t tag[4] = {bswap32(y[0]) ^ ek0[0], bswap32(y[1]) ^ ek0[1], bswap32(y[2]) ^ ek0[2],
+                     bswap32(y[3]) ^ ek0[3]};
+  const uint32_t tag_len = as_const(&S->tag_len)[0];
+  const uint32_t tw = lane >> 2;
+  const uint32_t tword = tw == 0 ? tag[0] : tw == 1 ? tag[1] : tw == 2 ? tag[2] : tag[3];
+  const uint32_t tbyte = (tword >> (8 * (lane & 3))) & 0xFF;
+  if (SEAL) {
+    if (lane < tag_len) rc.tag_out[lane] = (uint8_t)tbyte;
+    if (lane == 0) *status_slot = rc.ok_status;
+  } else {
+    uint32_t diff = 0;
+    if (lane < tag_len) diff = rc.tag_byte ^ tbyte;
+    bool bad = __any(diff != 0);  // constant-time in the data: every lane compares
+    if (bad) {
+      for (uint64_t o = lane; o < rc.zero_len; o += kWave) rc.dst[o] = 0;
+    }
+    if (lane == 0) *status_slot = bad ? TLSGPU_REC_BAD_MAC : rc.ok_status;
+  }
+}
+
+// Finish one record (chains -> weights -> tag).
+template <bool SEAL>
+__device__ __forceinline__ void gcm_finish(const RecCtx& rc, uint32_t (&x)[4], const uint32_t ek0[4],
+                                           const DevSession* __restrict__ S, int32_t* status_slot,
+                                           uint32_t lane, const GhLane& gl) {
+  uint32_t xb[4], y[4] = {0, 0, 0, 0};
+  const uint32_t e = gcm_close_chain(rc, x, xb, lane, gl);
+  if (e != 0) mul_shoup(xb, e, y);
+  gcm_tag<SEAL>(rc, y, ek0, S, status_slot, lane);
+}
+
+// Finish two records with their Shoup multiplies interleaved (two independent
+// 32-step LDS chains per lane instead of two back-to-back ones).
+template <bool SEAL>
+__device__ __forceinline__ void gcm_finish2(const RecCtx (&rc)[2], uint32_t (&x)[2][4],
+                                            const uint32_t (&ek)[2][4],
+                                            const DevSession* __restrict__ S, int32_t* slot_a,
+                                            int32_t* slot_b, uint32_t lane, const GhLane& gl) {
+  uint32_t xb[2][4], y[2][4];
+  const uint32_t ea = gcm_close_chain(rc[0], x[0], xb[0], lane, gl);
+  const uint32_t eb = gcm_close_chain(rc[1], x[1], xb[1], lane, gl);
+  mul_shoup2(xb[0], ea, y[0], xb[1], eb, y[1]);
+  gcm_tag<SEAL>(rc[0], y[0], ek[0], S, slot_a, lane);
+  gcm_tag<SEAL>(rc[1], y[1], ek[1], S, slot_b, lane);
+}
+
+// CTR en/decryption of blocks [start, nb) fused with the lane GHASH chains x
+// (start is a multiple of 64: block i belongs to lane i % 64's chain).
+// FAST: counters < 2^16 and the per-record constants `rcc` were precomputed
+// (wave-uniform values); otherwise `cc` (ctr_setup) is used.
+template <bool SEAL, int ROUNDS, bool FAST>
+__device__ __forceinline__ void gcm_blocks(const RecCtx& rc, const DevSession* __restrict__ S,
+                                           const RecConsts& rcc, const CtrConst& cc,
+                                           uint32_t (&x)[4], uint32_t start, uint32_t lane,
+                                           uint32_t laneoff, const GhLane& gl) {
+  cu32* rk = as_const(S->rk);
+  cu32* rkr = as_const(S->rk_rot);
+  const uint32_t n = rc.n;
+  const uint32_t nb = (n + 15) >> 4;
+  const uint32_t rk03 = rk[3];
+  auto keystream = [&](uint32_t ks[4], uint32_t ctr) {
+    if (FAST)
+      aes_ctr16<ROUNDS>(ks, ctr, rcc, rk03, rk, rkr, laneoff);
+    else
+      aes_ctr<ROUNDS>(ks, ctr, cc, rk, rkr, laneoff);
+  };
+  const uint32_t ctr0 = bswap32(rc.j0[3]) + 1u;  // inc32(J0), gcm128.c:815-823
+  const bool aligned = ((((uintptr_t)rc.src) | ((uintptr_t)rc.dst)) & 15) == 0;
+
+  // Full-block steps, two per iteration (two independent AES chains per lane
+  // keep twice as many LDS lookups in flight), with the next iteration's
+  // ciphertext loads issued before this iteration's AES.
+  const uint32_t nfull_steps = (n >> 4) / kWave;
+  uint32_t base = start;
+  if (nfull_steps >= start / kWave + 2) {
+    uint32_t c0[4], c1[4];
+    load_block(rc.src + 16u * (start + lane), 16, aligned, c0);
+    load_block(rc.src + 16u * (start + lane + kWave), 16, aligned, c1);
+    uint32_t t = start / kWave;
+    for (; t + 2 <= nfull_steps; t += 2, base += 2 * kWave) {
+      const uint32_t i = base + lane;
+      uint32_t n0[4] = {0, 0, 0, 0}, n1[4] = {0, 0, 0, 0};
+      if (t + 4 <= nfull_steps) {
+        load_block(rc.src + 16u * (i + 2 * kWave), 16, aligned, n0);
+        load_block(rc.src + 16u * (i + 3 * kWave), 16, aligned, n1);
+      }
+      uint32_t k0[4], k1[4];
+      if (FAST) {
+        aes_ctr16x2<ROUNDS>(k0, k1, ctr0 + i, ctr0 + i + kWave, rcc, rk03, rk, rkr, laneoff);
+      } else {
+        keystream(k0, ctr0 + i);
+        keystream(k1, ctr0 + i + kWave);
+      }
+      uint32_t o0[4] = {c0[0] ^ k0[0], c0[1] ^ k0[1], c0[2] ^ k0[2], c0[3] ^ k0[3]};
+      uint32_t o1[4] = {c1[0] ^ k1[0], c1[1] ^ k1[1], c1[2] ^ k1[2], c1[3] ^ k1[3]};
+      store_block(rc.dst + 16u * i, 16, aligned, o0);
+      store_block(rc.dst + 16u * (i + kWave), 16, aligned, o1);
+      uint32_t xk[4];
+      mul_k(x, xk, gl);
+      const uint32_t* g0 = SEAL ? o0 : c0;
+      const uint32_t* g1 = SEAL ? o1 : c1;
+      x[0] = xk[0] ^ g0[0]; x[1] = xk[1] ^ g0[1]; x[2] = xk[2] ^ g0[2]; x[3] = xk[3] ^ g0[3];
+      mul_k(x, xk, gl);
+      x[0] = xk[0] ^ g1[0]; x[1] = xk[1] ^ g1[1]; x[2] = xk[2] ^ g1[2]; x[3] = xk[3] ^ g1[3];
+#pragma unroll
+      for (int w = 0; w < 4; w++) { c0[w] = n0[w]; c1[w] = n1[w]; }
+    }
+  }
+  // Remaining steps (odd full step, partial wave, partial last block).
+  for (; base < nb; base += kWave) {
+    const uint32_t i = base + lane;
+    const bool active = i < nb;
+    const uint32_t nbytes = active ? min(16u, n - 16u * i) : 0u;
+    uint32_t in[4];
+    load_block(rc.src + 16u * i, nbytes, aligned, in);
+    uint32_t ks[4];
+    keystream(ks, ctr0 + i);
+#pragma unroll
+    for (int w = 0; w < 4; w++) {  // zero-padded GHASH block for the partial tail
+      int32_t b = (int32_t)nbytes - 4 * w;
+      uint32_t keep = b >= 4 ? 0xFFFFFFFFu : (b <= 0 ? 0u : ((1u << (8 * b)) - 1u));
+      ks[w] &= keep;
+    }
+    uint32_t ob[4] = {in[0] ^ ks[0], in[1] ^ ks[1], in[2] ^ ks[2], in[3] ^ ks[3]};
+    if (active) store_block(rc.dst + 16u * i, nbytes, aligned, ob);
+    uint32_t xk[4];
+    mul_k(x, xk, gl);
+    if (active) {
+      const uint32_t* c = SEAL ? ob : in;
+      x[0] = xk[0] ^ c[0]; x[1] = xk[1] ^ c[1]; x[2] = xk[2] ^ c[2]; x[3] = xk[3] ^ c[3];
+    }
+  }
+
+}
+
+// GHASH(AAD || C || lengths) with the lane chains described in the header,
+// fused with CTR en/decryption.  Checks the tag (open) or writes it (seal).
+template <bool SEAL, int ROUNDS, bool FAST>
+__device__ void gcm_record(const RecCtx& rc, const DevSession* __restrict__ S,
+                           const RecConsts& rcc, int32_t* status_slot, uint32_t lane,
+                           uint32_t laneoff, const GhLane& gl) {
+  cu32* rk = as_const(S->rk);
+  cu32* rkr = as_const(S->rk_rot);
+  uint32_t ek0[4];
+  CtrConst cc;
+  if (FAST) {
+    ek0[0] = rcc.ek0[0]; ek0[1] = rcc.ek0[1]; ek0[2] = rcc.ek0[2]; ek0[3] = rcc.ek0[3];
+  } else {
+    ek0[0] = rc.j0[0]; ek0[1] = rc.j0[1]; ek0[2] = rc.j0[2]; ek0[3] = rc.j0[3];
+    aes_block<ROUNDS>(ek0, rk, rkr, laneoff);
+    cc = ctr_setup(rc.j0, rk, laneoff);
+  }
+  // Horner chain state (LE words).  The AAD' element sits at j = -1, i.e. in
+  // lane 63's chain one H^64 step before C_63.
+  uint32_t x[4] = {0, 0, 0, 0};
+  if (rc.aad_len != 0 && lane == 63) {
+    x[0] = bswap32(rc.aad_be[0]); x[1] = bswap32(rc.aad_be[1]);
+    x[2] = bswap32(rc.aad_be[2]); x[3] = bswap32(rc.aad_be[3]);
+  }
+  gcm_blocks<SEAL, ROUNDS, FAST>(rc, S, rcc, cc, x, 0, lane, laneoff, gl);
+  gcm_finish<SEAL>(rc, x, ek0, S, status_slot, lane, gl);
+}
+
+// ---------------------------------------------------------------------------
+// L2 prefetch: one dword of each 128-B line of [p, p + bytes), N lines per
+// lane.  Ordinary (cached) loads whose values are handed to an empty asm at
+// prefetch_done(), so the compiler counts them in vmcnt and waits for them
+// only there; as the wave's oldest loads they have long completed by then.
+template <int N>
+struct Prefetch {
+  uint32_t v[N];
+};
+template <int N>
+__device__ __forceinline__ Prefetch<N> l2_prefetch(const uint8_t* p, uint32_t bytes, uint32_t lane) {
+  Prefetch<N> f;
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    const uint32_t off = (uint32_t)(k * 64 + lane) * 128u;
+    f.v[k] = off < bytes ? *reinterpret_cast<const uint32_t*>(p + off) : 0u;
+  }
+  return f;
+}
+template <int N>
+__device__ __forceinline__ void prefetch_done(const Prefetch<N>& f) {
+#pragma unroll
+  for (int k = 0; k < N; k++) asm volatile("" ::"v"(f.v[k]));
+}
+
+// ---------------------------------------------------------------------------
+// Phase timing (diagnostic, BatchArgs::dbg != null, env TLSGPU_PHASE_STATS):
+// shader-clock cycles per phase summed over waves, dbg[2i] = cycles,
+// dbg[2i+1] = events.
+struct PhaseClock {
+  unsigned long long* dbg;
+  uint64_t t;
+  __device__ __forceinline__ PhaseClock(unsigned long long* d) : dbg(d), t(d ? __builtin_amdgcn_s_memtime() : 0) {}
+  // counters live in LDS (DBG_OFF) during the launch; the kernel flushes them
+  __device__ __forceinline__ void lap(int i, uint32_t lane) {
+    if (dbg) {
+      const uint64_t n = __builtin_amdgcn_s_memtime();
+      if (lane == 0) {
+        unsigned long long* c = reinterpret_cast<unsigned long long*>(s_lds + DBG_OFF);
+        atomicAdd(c + 2 * i, (unsigned long long)(n - t));
+        atomicAdd(c + 2 * i + 1, 1ull);
+      }
+      t = __builtin_amdgcn_s_memtime();
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------
+// NB-block T-table keystream (the hybrid kernel's T-table waves run alone on
+// their SIMD's LDS share, so they keep 16 * NB lookups in flight per round).
+template <int NB>
+__device__ __forceinline__ void aes_roundN(uint32_t (&s)[NB][4], uint32_t k0, uint32_t k1,
+                                           uint32_t k2, uint32_t k3, uint32_t laneoff) {
+  uint32_t t[NB][16];
+#pragma unroll
+  for (int b = 0; b < NB; b++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      t[b][4 * c + 0] = TE0(s[b][c], 0);
+      t[b][4 * c + 1] = TE1(s[b][(c + 1) & 3], 1);
+      t[b][4 * c + 2] = TE0(s[b][(c + 2) & 3], 2);
+      t[b][4 * c + 3] = TE1(s[b][(c + 3) & 3], 3);
+    }
+  const uint32_t k[4] = {k0, k1, k2, k3};
+#pragma unroll
+  for (int b = 0; b < NB; b++)
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+      s[b][c] = xor3(t[b][4 * c], t[b][4 * c + 1], rotl16(xor3(t[b][4 * c + 2], t[b][4 * c + 3], k[c])));
+#pragma unroll
+  for (int b = 0; b < NB; b++) {
+    __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);  // addresses of block b
+    __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);  // its lookups
+  }
+  __builtin_amdgcn_sched_group_barrier(0x002, 12 * NB, 0);  // combine
+}
+
+// NB keystream blocks for counters ctr[b] < 2^16 (aes_ctr16 generalised).
+template <int NB, int ROUNDS>
+__device__ __forceinline__ void aes_ctr16xN(uint32_t (&ks)[NB][4], const uint32_t (&ctr)[NB],
+                                            const RecConsts& c, uint32_t rk03, cu32* rk,
+                                            cu32* rkr, uint32_t laneoff) {
+  uint32_t A[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; b++) {
+    const uint32_t v = bswap32(ctr[b]) ^ rk03;
+    const uint32_t s0 = c.k1a ^ rotl16(TE1(v, 3)), s1 = c.k1b ^ rotl16(TE0(v, 2));
+    A[b][0] = xor3(c.k2[0], TE0(s0, 0), TE1(s1, 1));
+    A[b][1] = xor3(c.k2[1], TE0(s1, 0), rotl16(TE1(s0, 3)));
+    A[b][2] = c.k2[2] ^ rotl16(TE0(s0, 2) ^ TE1(s1, 3));
+    A[b][3] = xor3(c.k2[3], TE1(s0, 1), rotl16(TE0(s1, 2)));
+  }
+#pragma unroll
+  for (int r = 3; r < ROUNDS; r++)
+    aes_roundN<NB>(A, rkr[4 * r], rkr[4 * r + 1], rkr[4 * r + 2], rkr[4 * r + 3], laneoff);
+#pragma unroll
+  for (int b = 0; b < NB; b++) {
+    aes_last(A[b][0], A[b][1], A[b][2], A[b][3], rk + 4 * ROUNDS, laneoff);
+#pragma unroll
+    for (int w = 0; w < 4; w++) ks[b][w] = A[b][w];
+  }
+}
+
+// Full NB-step groups of a 16-B-aligned record from block `start` on (FAST
+// constants only): 4 keystream blocks per lane in flight, the next group's
+// ciphertext loads issued first.  Advances `start` past the groups done; the
+// caller finishes the record with gcm_blocks.
+template <bool SEAL, int ROUNDS, int NB>
+__device__ __forceinline__ void gcm_blocks_xN(const RecCtx& rc, const DevSession* __restrict__ S,
+                                              const RecConsts& rcc, uint32_t (&x)[4],
+                                              uint32_t& start, uint32_t lane, uint32_t laneoff,
+                                              const GhLane& gl) {
+  if (((((uintptr_t)rc.src) | ((uintptr_t)rc.dst)) & 15) != 0) return;
+  cu32* rk = as_const(S->rk);
+  cu32* rkr = as_const(S->rk_rot);
+  const uint32_t rk03 = rk[3];
+  const uint32_t ctr0 = bswap32(rc.j0[3]) + 1u;
+  const uint32_t nfull_steps = (rc.n >> 4) / kWave;
+  uint32_t t = start / kWave;
+  if (t + NB > nfull_steps) return;
+  uint32_t c[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; b++) {
+    const uint4 v = *reinterpret_cast<const uint4*>(rc.src + 16u * (start + kWave * b + lane));
+    c[b][0] = v.x; c[b][1] = v.y; c[b][2] = v.z; c[b][3] = v.w;
+  }
+  for (; t + NB <= nfull_steps; t += NB, start += NB * kWave) {
+    const uint32_t i = start + lane;
+    uint32_t nx[NB][4];
+    if (t + 2 * NB <= nfull_steps) {
+#pragma unroll
+      for (int b = 0; b < NB; b++) {
+        const uint4 v = *reinterpret_cast<const uint4*>(rc.src + 16u * (i + kWave * (NB + b)));
+        nx[b][0] = v.x; nx[b][1] = v.y; nx[b][2] = v.z; nx[b][3] = v.w;
+      }
+    }
+    uint32_t ctr[NB], k[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; b++) ctr[b] = ctr0 + i + kWave * b;
+    aes_ctr16xN<NB, ROUNDS>(k, ctr, rcc, rk03, rk, rkr, laneoff);
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+      uint32_t o[4] = {c[b][0] ^ k[b][0], c[b][1] ^ k[b][1], c[b][2] ^ k[b][2], c[b][3] ^ k[b][3]};
+      *reinterpret_cast<uint4*>(rc.dst + 16u * (i + kWave * b)) = make_uint4(o[0], o[1], o[2], o[3]);
+      const uint32_t* g = SEAL ? o : c[b];
+      uint32_t xk[4];
+      mul_k(x, xk, gl);
+      x[0] = xk[0] ^ g[0]; x[1] = xk[1] ^ g[1]; x[2] = xk[2] ^ g[2]; x[3] = xk[3] ^ g[3];
+    }
+#pragma unroll
+    for (int b = 0; b < NB; b++)
+#pragma unroll
+      for (int w = 0; w < 4; w++) c[b][w] = nx[b][w];
+  }
+}
+
+// gcm_record<SEAL, ROUNDS, true> with the NB-wide full-block loop first.
+template <bool SEAL, int ROUNDS, int NB = 4>
+__device__ void gcm_record_x4(const RecCtx& rc, const DevSession* __restrict__ S,
+                              const RecConsts& rcc, int32_t* status_slot, uint32_t lane,
+                              uint32_t laneoff, const GhLane& gl,
+                              unsigned long long* dbg = nullptr) {
+  PhaseClock pc(dbg);
+  uint32_t x[4] = {0, 0, 0, 0};
+  if (rc.aad_len != 0 && lane == 63) {
+    x[0] = bswap32(rc.aad_be[0]); x[1] = bswap32(rc.aad_be[1]);
+    x[2] = bswap32(rc.aad_be[2]); x[3] = bswap32(rc.aad_be[3]);
+  }
+  uint32_t start = 0;
+  gcm_blocks_xN<SEAL, ROUNDS, NB>(rc, S, rcc, x, start, lane, laneoff, gl);
+  pc.lap(9, lane);
+  const CtrConst none = {};
+  gcm_blocks<SEAL, ROUNDS, true>(rc, S, rcc, none, x, start, lane, laneoff, gl);
+  pc.lap(10, lane);
+  gcm_finish<SEAL>(rc, x, rcc.ek0, S, status_slot, lane, gl);
+  pc.lap(11, lane);
+}
+
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+         __builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+__device__ __forceinline__ tlsgpu_record load_desc(const tlsgpu_record* p) {
+  cu32* w = as_const(p);
+  tlsgpu_record d;
+  d.in_off = ((uint64_t)w[1] << 32) | w[0];
+  d.out_off = ((uint64_t)w[3] << 32) | w[2];
+  d.seq = ((uint64_t)w[5] << 32) | w[4];
+  d.session = w[6];
+  d.len_type = w[7];
+  return d;
+}
+
+// J0 of record r for this lane (the batched constant pass): fixed IV(4) ||
+// explicit nonce(8) || 0x00000001 — the explicit nonce is the record's first
+// 8 bytes on open and the sequence number on seal (t1_enc.c:887-892, 941-948).
+template <bool SEAL>
+__device__ __forceinline__ void lane_j0(const tlsgpu_record* D, uint32_t r, uint32_t run_end,
+                                        const DevSession* __restrict__ S, const uint8_t* in,
+                                        uint32_t j0[4]) {
+  j0[0] = as_const(S->fixed_nonce)[0];
+  j0[1] = j0[2] = 0;
+  j0[3] = 0x01000000u;
+  if (r >= run_end) return;
+  const tlsgpu_record d = D[r];
+  if (SEAL) {
+    j0[1] = bswap32((uint32_t)(d.seq >> 32));
+    j0[2] = bswap32((uint32_t)d.seq);
+  } else if ((d.len_type & 0xFFFFFFu) >= 8) {
+    const uint8_t* p = in + d.in_off;
+    j0[1] = load_u32_bytes(p);
+    j0[2] = load_u32_bytes(p + 4);
+  }
+}
+
+// Build the per-record context from a TLS descriptor (t1_enc.c:832-975).
+// Returns false (and writes the status) when tls1_enc would return 0.
+template <bool SEAL>
+__device__ __forceinline__ bool parse_tls(const tlsgpu_record& d, const DevSession* __restrict__ S,
+                                          const uint8_t* in, uint8_t* out, int32_t* status_slot,
+                                          uint32_t lane, RecCtx& rc) {
+  uint32_t len = d.len_type & 0xFFFFFFu;
+  uint32_t type = d.len_type >> 24;
+  const uint8_t* ip = in + d.in_off;
+  uint8_t* op = out + d.out_off;
+  uint8_t explicit_nonce[8];
+  uint32_t tag_len = as_const(&S->tag_len)[0];
+  if (SEAL ? len > TLSGPU_MAX_RECORD : (len < 8 || len - 8 < tag_len ||
+                                          len - 8 - tag_len > TLSGPU_MAX_RECORD)) {
+    if (lane == 0) *status_slot = TLSGPU_REC_PUBLIC_INVALID;
+    return false;
+  }
+  if (SEAL) {
+    rc.n = len;
+    rc.src = ip;
+    rc.dst = op + 8;
+    rc.tag_out = op + 8 + len;
+    rc.tag_in = nullptr;
+    for (int k = 0; k < 8; k++) explicit_nonce[k] = (uint8_t)(d.seq >> (56 - 8 * k));
+    if (lane < 8) op[lane] = (uint8_t)(d.seq >> (56 - 8 * lane));  // explicit nonce into the record
+    rc.ok_status = (int32_t)(len + 8 + tag_len);
+    rc.zero_len = 0;
+  } else {
+    for (int k = 0; k < 8; k++) explicit_nonce[k] = ip[k];
+    rc.n = len - 8 - tag_len;
+    rc.src = ip + 8;
+    rc.dst = op;
+    rc.tag_in = ip + 8 + rc.n;
+    rc.tag_byte = lane < tag_len ? rc.tag_in[lane] : 0u;
+    rc.tag_out = nullptr;
+    rc.ok_status = (int32_t)rc.n;
+    rc.zero_len = rc.n;
+  }
+  // nonce = fixed_iv(4) || explicit(8); J0 = nonce || 0x00000001
+  rc.j0[0] = as_const(S->fixed_nonce)[0];
+  rc.j0[1] = (uint32_t)explicit_nonce[0] | ((uint32_t)explicit_nonce[1] << 8) |
+             ((uint32_t)explicit_nonce[2] << 16) | ((uint32_t)explicit_nonce[3] << 24);
+  rc.j0[2] = (uint32_t)explicit_nonce[4] | ((uint32_t)explicit_nonce[5] << 8) |
+             ((uint32_t)explicit_nonce[6] << 16) | ((uint32_t)explicit_nonce[7] << 24);
+  rc.j0[3] = 0x01000000u;
+  // AAD = seq(8) || type || version(2) || length(2), one zero-padded block
+  uint32_t v = as_const(&S->version)[0];
+  rc.aad_be[0] = (uint32_t)(d.seq >> 32);
+  rc.aad_be[1] = (uint32_t)d.seq;
+  rc.aad_be[2] = (type << 24) | ((v & 0xFFFF) << 8) | ((rc.n >> 8) & 0xFF);
+  rc.aad_be[3] = (rc.n & 0xFF) << 24;
+  rc.aad_len = 13;
+  return true;
+}
+
+// Raw EVP_AEAD job (arbitrary nonce and AAD; e_aes.c:1424-1510).  The host
+// already applied the argument checks of evp_aead.c / e_aes.c.
+template <bool SEAL>
+__device__ __forceinline__ void parse_raw(const RawJob& j, const DevSession* __restrict__ S,
+                                          RecCtx& rc) {
+  const uint8_t* ip = (const uint8_t*)j.in;
+  uint8_t* op = (uint8_t*)j.out;
+  const uint8_t* nonce = (const uint8_t*)j.nonce;
+  uint32_t tag_len = as_const(&S->tag_len)[0];
+  if (SEAL) {
+    rc.n = j.in_len;
+    rc.src = ip;
+    rc.dst = op;
+    rc.tag_out = op + j.in_len;
+    rc.tag_in = nullptr;
+    rc.ok_status = (int32_t)(j.in_len + tag_len);
+  } else {
+    rc.n = j.in_len - tag_len;
+    rc.src = ip;
+    rc.dst = op;
+    rc.tag_in = ip + rc.n;
+    const uint32_t ln = threadIdx.x & 63;
+    rc.tag_byte = ln < tag_len ? rc.tag_in[ln] : 0u;
+    rc.tag_out = nullptr;
+    rc.ok_status = (int32_t)rc.n;
+  }
+  rc.zero_len = j.max_out;
+  if (j.nonce_len == 12) {
+    rc.j0[0] = load_u32_bytes(nonce);
+    rc.j0[1] = load_u32_bytes(nonce + 4);
+    rc.j0[2] = load_u32_bytes(nonce + 8);
+    rc.j0[3] = 0x01000000u;
+  } else {  // J0 = GHASH(IV || pad || 0^64 || [len(IV)]_64)  (gcm128.c:770-812)
+    uint32_t xb[4] = {0, 0, 0, 0};
+    ghash_serial(xb, nonce, j.nonce_len, true);
+    uint64_t bits = (uint64_t)j.nonce_len * 8;
+    xb[2] ^= (uint32_t)(bits >> 32);
+    xb[3] ^= (uint32_t)bits;
+    uint32_t z[4];
+    mul_shoup(xb, 1, z);
+    rc.j0[0] = bswap32(z[0]); rc.j0[1] = bswap32(z[1]);
+    rc.j0[2] = bswap32(z[2]); rc.j0[3] = bswap32(z[3]);
+  }
+  rc.aad_be[0] = rc.aad_be[1] = rc.aad_be[2] = rc.aad_be[3] = 0;
+  rc.aad_len = j.aad_len;
+  if (j.aad_len) ghash_serial(rc.aad_be, (const uint8_t*)j.aad, j.aad_len, false);
+}
+
+// ---------------------------------------------------------------------------
+// Workgroup prologue / session table staging
+template <int NT>
+__device__ void fill_aes_lds() {
+  for (uint32_t t = threadIdx.x; t < 1024; t += NT) {  // 1024 x 64 B = 64 KiB
+    const uint32_t row = t >> 2, part = t & 3;
+    uint32_t v = g_te0.v[row];
+    if (part >= 2) v = rotl32(v, 8);  // Te1 = rotl8(Te0)
+    uint4 w = make_uint4(v, v, v, v);
+    uint4* dst = reinterpret_cast<uint4*>(s_lds + AES_OFF + row * 256 + part * 64);
+    dst[0] = w; dst[1] = w; dst[2] = w; dst[3] = w;
+  }
+  const uint32_t t = threadIdx.x;
+  if (t < 16) {  // rem_4bit >> 32 (gcm128.c:327-331), derived by four x-shifts
+    uint64_t hi = 0, lo = t;
+    for (int k = 0; k < 4; k++) {
+      uint64_t c = lo & 1;
+      lo = (lo >> 1) | (hi << 63);
+      hi = (hi >> 1) ^ (c ? 0xE100000000000000ull : 0);
+    }
+    *reinterpret_cast<uint32_t*>(s_lds + R4_OFF + t * 4) = (uint32_t)(hi >> 32);
+  }
+}
+
+// Expand the session's 128 basis vectors K*x^p into T[j][b] and copy the
+// Shoup tables of H^1..H^65.
+template <int NT>
+__device__ void load_session_tables(const DevGcmTables* __restrict__ tab) {
+  const uint32_t bl = threadIdx.x & 63;
+  for (uint32_t jj = threadIdx.x >> 6; jj < 16; jj += NT / kWave) {
+    const uint32_t j = __builtin_amdgcn_readfirstlane(jj);  // byte position
+    uint32_t lo[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 6; k++) {   // bit k of the byte <-> x^(8j + 7 - k)
+      uint32_t msk = 0u - ((bl >> k) & 1u);
+      cu32* bv = as_const(tab->basis[8 * j + 7 - k]);
+      lo[0] ^= bv[0] & msk; lo[1] ^= bv[1] & msk; lo[2] ^= bv[2] & msk; lo[3] ^= bv[3] & msk;
+    }
+    cu32* b6 = as_const(tab->basis[8 * j + 1]);
+    cu32* b7 = as_const(tab->basis[8 * j + 0]);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      uint32_t m6 = (q & 1) ? 0xFFFFFFFFu : 0u, m7 = (q & 2) ? 0xFFFFFFFFu : 0u;
+      uint4 v = make_uint4(lo[0] ^ (b6[0] & m6) ^ (b7[0] & m7), lo[1] ^ (b6[1] & m6) ^ (b7[1] & m7),
+                           lo[2] ^ (b6[2] & m6) ^ (b7[2] & m7), lo[3] ^ (b6[3] & m6) ^ (b7[3] & m7));
+      uint32_t b = bl + 64u * q;
+      *reinterpret_cast<uint4*>(s_lds + KT_OFF + b * 256 + j * 16) = v;
+    }
+  }
+  const uint4* sh = reinterpret_cast<const uint4*>(&tab->shoup[0][0][0]);
+  for (uint32_t k = threadIdx.x; k < kPowMax * 16; k += NT)
+    *reinterpret_cast<uint4*>(s_lds + SH_OFF + k * 16) = sh[k];
+}
+
+// Bitsliced round-key masks from the round-key words (SGPRs): s_bfe_i32
+// sign-extends the key bit into 0 / ~0.
+struct SgprMasks {
+  cu32* rk;
+  __device__ __forceinline__ uint32_t mask(int r, int i) const {
+    return (uint32_t)__builtin_amdgcn_sbfe((int32_t)rk[4 * r + (i >> 5)], (uint32_t)(i & 31), 1u);
+  }
+};
+
+__device__ __forceinline__ bool is_gcm(uint32_t kind) {
+  return kind == TLSGPU_AES_128_GCM || kind == TLSGPU_AES_256_GCM;
+}
+
+}  // namespace tg

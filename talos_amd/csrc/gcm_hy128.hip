@@ -1,0 +1,26 @@
+// gcm_hy128.hip — AES-128-GCM instantiations of gcm_hy_kernel with
+// bitsliced waves: 4 of 8 (TLSGPU_GCM_HYBRID) or all 8 (TLSGPU_GCM_BITSLICE).
+#include "gcm_hybrid.h"
+
+namespace tg {
+
+int launch_gcm_hy10(const BatchArgs& a, const RecPre* pre, bool seal, int bs_waves, int groups,
+                     hipStream_t s) {
+  if (a.n == 0) return 0;
+  const dim3 g(groups), b(kHyThreads);
+#ifdef TG_DEV_OPEN128
+  if (seal || 10 != 10 || bs_waves != kHyBsWaves) return -1;
+  hipLaunchKernelGGL((gcm_hy_kernel<false, 10, kHyThreads, kHyBsWaves, 4>), g, b, 0, s, a, pre);
+#else
+  if (bs_waves == kHyBsWaves) {
+    if (seal) hipLaunchKernelGGL((gcm_hy_kernel<true, 10, kHyThreads, kHyBsWaves, 4>), g, b, 0, s, a, pre);
+    else hipLaunchKernelGGL((gcm_hy_kernel<false, 10, kHyThreads, kHyBsWaves, 4>), g, b, 0, s, a, pre);
+  } else {
+    if (seal) hipLaunchKernelGGL((gcm_hy_kernel<true, 10, kHyThreads, 8, 4>), g, b, 0, s, a, pre);
+    else hipLaunchKernelGGL((gcm_hy_kernel<false, 10, kHyThreads, 8, 4>), g, b, 0, s, a, pre);
+  }
+#endif
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace tg

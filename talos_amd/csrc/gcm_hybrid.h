@@ -1,0 +1,455 @@
+// gcm_hybrid.h — AES-GCM TLS record kernels driven by a per-run record queue
+// and per-record constants from a prep pass:
+//   * gcm_prep_kernel: E_K(J0) and the round-1/2 constants of every record;
+//   * gcm_hy_kernel<NT, BSW, NB>: NT threads, the first BSW waves bitsliced
+//     (record pairs, AES-CTR keystream on the VALU, bs_aes.h), the others
+//     T-table waves (single records, NB blocks per lane in flight).
+// Instantiated per variant in gcm_queue.hip / gcm_hy128.hip / gcm_hy256.hip so
+// that the (slow to compile) bitsliced instantiations build in parallel.
+#pragma once
+#include <utility>
+
+#include "gcm_device.h"
+
+namespace tg {
+
+
+__device__ __forceinline__ uint32_t xor3s(uint32_t a, uint32_t b, uint32_t k) {
+  return bop3s(a, b, k, 0x96);
+}
+
+// Counter-block planes for pass p (blocks 1024p .. 1024p + 1023 of both
+// records).  Bytes 0..11 = the records' nonces (uniform per half), bytes 12-13
+// zero, bytes 14-15 = the big-endian counter u + 64 (j & 15), u = 2 + lane +
+// 1024 p < 2^16 (TLSGPU_MAX_RECORD): low 6 bits constant per lane, bits 6..9
+// a rotated slot pattern, bits 10..15 select between U_hi and U_hi + 1.
+__device__ __forceinline__ void bs_ctr_planes(uint32_t (&st)[128], const uint32_t* ja,
+                                              const uint32_t* jb, uint32_t u) {
+#pragma unroll
+  for (int w = 0; w < 3; w++)
+#pragma unroll
+    for (int bit = 0; bit < 32; bit++) {
+      const uint32_t ma = 0u - ((ja[w] >> bit) & 1u), mb = 0u - ((jb[w] >> bit) & 1u);
+      st[32 * w + bit] = (ma & 0x0000FFFFu) | (mb & 0xFFFF0000u);
+    }
+#pragma unroll
+  for (int k = 0; k < 16; k++) st[96 + k] = 0u;
+#pragma unroll
+  for (int k = 0; k < 6; k++) st[120 + k] = 0u - ((u >> k) & 1u);
+  const uint32_t U = u >> 6, ulo = U & 15u, uhi = U >> 4;
+  st[126] = __builtin_amdgcn_alignbit(0xAAAAAAAAu, 0xAAAAAAAAu, ulo);
+  st[127] = __builtin_amdgcn_alignbit(0xCCCCCCCCu, 0xCCCCCCCCu, ulo);
+  st[112] = __builtin_amdgcn_alignbit(0xF0F0F0F0u, 0xF0F0F0F0u, ulo);
+  st[113] = __builtin_amdgcn_alignbit(0xFF00FF00u, 0xFF00FF00u, ulo);
+  const uint32_t cm = ((0xFFFF0000u >> ulo) & 0xFFFFu) * 0x10001u;  // slots that carry
+  const uint32_t h1 = uhi + 1u;
+#pragma unroll
+  for (int q = 0; q < 6; q++)
+    st[114 + q] = (cm & (0u - ((h1 >> q) & 1u))) | (~cm & (0u - ((uhi >> q) & 1u)));
+}
+
+// One consume step of gcm_pair_hy (see there).
+template <bool SEAL, int T>
+__device__ __forceinline__ void bs_consume(const uint32_t (&st)[128], uint32_t (&ring)[4][2][4],
+                                           uint32_t (&x)[2][4], const RecCtx (&rc)[2],
+                                           const uint32_t (&rkl)[4], uint32_t pb, uint32_t lane,
+                                           const GhLane& gl) {
+  const uint32_t i = pb + 64u * T + lane;
+  uint32_t c[2][4], g[2][4];
+#pragma unroll
+  for (int q = 0; q < 2; q++)
+#pragma unroll
+    for (int w = 0; w < 4; w++) c[q][w] = ring[T & 3][q][w];
+  if (T + 4 < 16) {
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const uint4 v = *reinterpret_cast<const uint4*>(rc[q].src + 16u * (i + 256u));
+      ring[T & 3][q][0] = v.x; ring[T & 3][q][1] = v.y; ring[T & 3][q][2] = v.z; ring[T & 3][q][3] = v.w;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    uint32_t o[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) o[w] = xor3s(c[q][w], st[32 * w + 16 * q + T], rkl[w]);
+    *reinterpret_cast<uint4*>(rc[q].dst + 16u * i) = make_uint4(o[0], o[1], o[2], o[3]);
+#pragma unroll
+    for (int w = 0; w < 4; w++) g[q][w] = SEAL ? o[w] : c[q][w];
+  }
+  uint32_t xa[4], xb[4];
+  mul_k2(x[0], x[1], xa, xb, gl);
+#pragma unroll
+  for (int w = 0; w < 4; w++) { x[0][w] = xa[w] ^ g[0][w]; x[1][w] = xb[w] ^ g[1][w]; }
+}
+
+template <bool SEAL, int... T>
+__device__ __forceinline__ void bs_consume_all(const uint32_t (&st)[128], uint32_t (&ring)[4][2][4],
+                                               uint32_t (&x)[2][4], const RecCtx (&rc)[2],
+                                               const uint32_t (&rkl)[4], uint32_t pb,
+                                               uint32_t lane, const GhLane& gl,
+                                               std::integer_sequence<int, T...>) {
+  (bs_consume<SEAL, T>(st, ring, x, rc, rkl, pb, lane, gl), ...);
+}
+
+// Two records of one session, both 16-B aligned with >= 1024 full blocks.
+// Whole 1024-block passes run bitsliced; any remainder of either record
+
+// ---------------------------------------------------------------------------
+// Hybrid kernel.  The T-table path is bound by LDS (16
+// lookups per block-round), the bitsliced path by VALU issue; one CU has both.
+// A 512-thread workgroup runs 8 waves, two per SIMD: waves 0-3 are "bitsliced"
+// waves (record pairs through bs_encrypt_ctr, VALU-only AES), waves 4-7 are
+// "T-table" waves (single records, 4 blocks per lane in flight, raised issue
+// priority so the LDS pipe stays fed).  Inside a session run the waves pull
+// records from an LDS counter, so the split follows the measured rates; a
+// bitsliced wave stops taking pairs when fewer than a.bs_reserve records of
+// the run remain (a pair is the coarsest unit; the run ends at a barrier).
+constexpr int kHyThreads = 512;
+constexpr int kHyBsWaves = 4;
+
+// Round-1/2 shortcut for TLS counters (< 2^16): bytes 0..13 of
+// every counter block of a record are the same, so after round 1 columns 2, 3
+// are per-record constants and columns 0, 1 differ only through
+// S(ctr byte 15 ^ rk0) and S(ctr byte 14 ^ rk0):
+//   col 0 = k1a ^ (s, s, 3s, 2s),  col 1 = k1b ^ (s', 3s', 2s', s')
+// (the MixColumns images of one non-zero byte in row 3 / row 2).  Round 2 then
+// needs 8 S-boxes on the VALU; the other 8 are the per-record constants sb2.
+// Slots 0..15 hold record A, 16..31 record B (half-word planes).
+__device__ __forceinline__ uint32_t half_plane(uint32_t wa, uint32_t wb, int bit) {
+  const uint32_t ma = (uint32_t)__builtin_amdgcn_sbfe((int32_t)wa, (uint32_t)bit, 1u);
+  const uint32_t mb = (uint32_t)__builtin_amdgcn_sbfe((int32_t)wb, (uint32_t)bit, 1u);
+  return (ma & 0x0000FFFFu) | (mb & 0xFFFF0000u);
+}
+
+// xtime on 8 planes (p[k] = bit k): {p7, p0^p7, p1, p2^p7, p3^p7, p4, p5, p6}
+__device__ __forceinline__ void bs_xtime(const uint32_t (&p)[8], uint32_t (&o)[8]) {
+  o[0] = p[7]; o[1] = p[0] ^ p[7]; o[2] = p[1]; o[3] = p[2] ^ p[7];
+  o[4] = p[3] ^ p[7]; o[5] = p[4]; o[6] = p[5]; o[7] = p[6];
+}
+
+#define TG_SBOX8(in, out) \
+  TG_BS_SBOX(in[7], in[6], in[5], in[4], in[3], in[2], in[1], in[0], out[7], out[6], out[5], \
+             out[4], out[3], out[2], out[1], out[0])
+
+// Keystream planes of pass p (blocks 1024p .. 1024p + 1023 of records A and B,
+// u = 2 + lane + 1024p) without the final AddRoundKey.
+template <int ROUNDS>
+__device__ __forceinline__ void bs_encrypt_ctr(uint32_t (&st)[128], const RecPre* pa,
+                                               const RecPre* pb, uint32_t u, cu32* rk) {
+  const SgprMasks km{rk};
+  // counter bytes 14 (c14) and 15 (c15) of slot j: u + 64 (j mod 16)
+  uint32_t c14[8], c15[8];
+#pragma unroll
+  for (int k = 0; k < 6; k++) c15[k] = 0u - ((u >> k) & 1u);
+  const uint32_t U = u >> 6, ulo = U & 15u, uhi = U >> 4;
+  c15[6] = __builtin_amdgcn_alignbit(0xAAAAAAAAu, 0xAAAAAAAAu, ulo);
+  c15[7] = __builtin_amdgcn_alignbit(0xCCCCCCCCu, 0xCCCCCCCCu, ulo);
+  c14[0] = __builtin_amdgcn_alignbit(0xF0F0F0F0u, 0xF0F0F0F0u, ulo);
+  c14[1] = __builtin_amdgcn_alignbit(0xFF00FF00u, 0xFF00FF00u, ulo);
+  const uint32_t cm = ((0xFFFF0000u >> ulo) & 0xFFFFu) * 0x10001u;  // slots that carry
+  const uint32_t h1 = uhi + 1u;
+#pragma unroll
+  for (int q = 0; q < 6; q++)
+    c14[2 + q] = (cm & (0u - ((h1 >> q) & 1u))) | (~cm & (0u - ((uhi >> q) & 1u)));
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    c14[k] ^= km.mask(0, 8 * 14 + k);
+    c15[k] ^= km.mask(0, 8 * 15 + k);
+  }
+  uint32_t s14[8], s15[8], x14[8], x15[8];
+  TG_SBOX8(c14, s14);
+  TG_SBOX8(c15, s15);
+  bs_xtime(s14, x14);
+  bs_xtime(s15, x15);
+  cu32* A = as_const(pa);
+  cu32* B = as_const(pb);
+  const uint32_t k1aA = A[4], k1aB = B[4], k1bA = A[5], k1bB = B[5];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    st[8 * 0 + k] = half_plane(k1aA, k1aB, k) ^ s15[k];
+    st[8 * 1 + k] = half_plane(k1aA, k1aB, 8 + k) ^ s15[k];
+    st[8 * 2 + k] = half_plane(k1aA, k1aB, 16 + k) ^ x15[k] ^ s15[k];
+    st[8 * 3 + k] = half_plane(k1aA, k1aB, 24 + k) ^ x15[k];
+    st[8 * 4 + k] = half_plane(k1bA, k1bB, k) ^ s14[k];
+    st[8 * 5 + k] = half_plane(k1bA, k1bB, 8 + k) ^ x14[k] ^ s14[k];
+    st[8 * 6 + k] = half_plane(k1bA, k1bB, 16 + k) ^ x14[k];
+    st[8 * 7 + k] = half_plane(k1bA, k1bB, 24 + k) ^ s14[k];
+  }
+  // round 2: SubBytes of columns 0, 1 on the VALU, columns 2, 3 from sb2
+#pragma unroll
+  for (int b = 0; b < 8; b++) {
+    uint32_t* p = st + 8 * b;
+    uint32_t o7, o6, o5, o4, o3, o2, o1, o0;
+    TG_BS_SBOX(p[7], p[6], p[5], p[4], p[3], p[2], p[1], p[0], o7, o6, o5, o4, o3, o2, o1, o0);
+    p[7] = o7; p[6] = o6; p[5] = o5; p[4] = o4; p[3] = o3; p[2] = o2; p[1] = o1; p[0] = o0;
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  const uint32_t sbA[2] = {A[10], A[11]}, sbB[2] = {B[10], B[11]};
+#pragma unroll
+  for (int b = 8; b < 16; b++)
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      st[8 * b + k] = half_plane(sbA[(b - 8) >> 2], sbB[(b - 8) >> 2], 8 * ((b - 8) & 3) + k);
+  bs_shiftrows(st);
+  bs_mixcolumn<0>(st, km, 2);
+  bs_mixcolumn<1>(st, km, 2);
+  bs_mixcolumn<2>(st, km, 2);
+  bs_mixcolumn<3>(st, km, 2);
+#pragma unroll 1
+  for (int r = 3; r < ROUNDS; r++) {
+    bs_subbytes(st);
+    bs_shiftrows(st);
+    bs_mixcolumn<0>(st, km, r);
+    bs_mixcolumn<1>(st, km, r);
+    bs_mixcolumn<2>(st, km, r);
+    bs_mixcolumn<3>(st, km, r);
+  }
+  bs_subbytes(st);
+  bs_shiftrows(st);
+}
+
+__device__ __forceinline__ RecConsts rec_consts_of(const RecPre* p) {
+  cu32* w = as_const(p);
+  RecConsts c;
+#pragma unroll
+  for (int i = 0; i < 4; i++) c.ek0[i] = w[i];
+  c.k1a = w[4];
+  c.k1b = w[5];
+#pragma unroll
+  for (int i = 0; i < 4; i++) c.k2[i] = w[6 + i];
+  return c;
+}
+
+// Two 16-B-aligned records of one session with >= 1024 full blocks each:
+// whole 1024-block passes bitsliced, any remainder through gcm_blocks.
+template <bool SEAL, int ROUNDS>
+__device__ void gcm_pair_hy(const RecCtx (&rc)[2], const RecPre* pa, const RecPre* pb,
+                            int32_t* slot_a, int32_t* slot_b, const DevSession* __restrict__ S,
+                            uint32_t lane, uint32_t laneoff, const GhLane& gl,
+                            unsigned long long* dbg) {
+  PhaseClock pc(dbg);
+  cu32* rk = as_const(S->rk);
+  const uint32_t rkl[4] = {rk[4 * ROUNDS], rk[4 * ROUNDS + 1], rk[4 * ROUNDS + 2],
+                           rk[4 * ROUNDS + 3]};
+  uint32_t x[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+  if (lane == 63) {  // AAD' at j = -1 (TLS always has the 13-byte AAD)
+#pragma unroll
+    for (int q = 0; q < 2; q++)
+#pragma unroll
+      for (int w = 0; w < 4; w++) x[q][w] = bswap32(rc[q].aad_be[w]);
+  }
+  const uint32_t passes = min(rc[0].n, rc[1].n) >> 14;
+  for (uint32_t p = 0; p < passes; p++) {
+    const uint32_t pb0 = p << 10;
+    // this pass's 2 x 16 KiB to L2 ahead of the ~15K-instruction AES phase
+    const Prefetch<2> pfa = l2_prefetch<2>(rc[0].src + 16u * pb0, rc[0].n - 16u * pb0, lane);
+    const Prefetch<2> pfb = l2_prefetch<2>(rc[1].src + 16u * pb0, rc[1].n - 16u * pb0, lane);
+    uint32_t st[128];
+    bs_encrypt_ctr<ROUNDS>(st, pa, pb, 2u + lane + pb0, rk);
+    pc.lap(1, lane);
+    uint32_t ring[4][2][4];
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const uint4 v = *reinterpret_cast<const uint4*>(rc[q].src + 16u * (pb0 + 64u * t + lane));
+        ring[t][q][0] = v.x; ring[t][q][1] = v.y; ring[t][q][2] = v.z; ring[t][q][3] = v.w;
+      }
+    prefetch_done(pfa);
+    prefetch_done(pfb);
+    transpose_all(st);
+    bs_consume_all<SEAL>(st, ring, x, rc, rkl, pb0, lane, gl,
+                         std::make_integer_sequence<int, 16>{});
+    pc.lap(2, lane);
+  }
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    if (((rc[q].n + 15) >> 4) > (passes << 10)) {
+      const RecConsts rcc = rec_consts_of(q ? pb : pa);
+      const CtrConst none = {};
+      gcm_blocks<SEAL, ROUNDS, true>(rc[q], S, rcc, none, x[q], passes << 10, lane, laneoff, gl);
+    }
+  }
+  uint32_t ek[2][4];
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    ek[0][w] = as_const(pa)[w];
+    ek[1][w] = as_const(pb)[w];
+  }
+  gcm_finish2<SEAL>(rc, x, ek, S, slot_a, slot_b, lane, gl);
+  pc.lap(3, lane);
+}
+
+template <bool SEAL, int ROUNDS, int NB = 4>
+__device__ __forceinline__ void hy_tt_record(const BatchArgs& a, const RecPre* __restrict__ pre,
+                                             uint32_t r, const DevSession* __restrict__ S,
+                                             uint32_t lane, uint32_t laneoff, const GhLane& gl) {
+  const tlsgpu_record* D = reinterpret_cast<const tlsgpu_record*>(a.descs);
+  RecCtx rc;
+  if (!parse_tls<SEAL>(load_desc(D + r), S, a.in, a.out, a.status + r, lane, rc)) return;
+  const RecConsts rcc = rec_consts_of(pre + r);
+  gcm_record_x4<SEAL, ROUNDS, NB>(rc, S, rcc, a.status + r, lane, laneoff, gl, a.dbg);
+}
+
+__device__ __forceinline__ uint32_t queue_take(uint32_t* q, uint32_t k, uint32_t lane) {
+  uint32_t r = 0;
+  if (lane == 0) r = atomicAdd(q, k);
+  return __builtin_amdgcn_readfirstlane(r);
+}
+
+// NT threads, the first BSW waves bitsliced (0: a pure T-table queue kernel,
+// 16 waves of <= 128 VGPRs), T-table waves NB blocks wide.
+template <bool SEAL, int ROUNDS, int NT, int BSW, int NB>
+__global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
+                                                       const RecPre* __restrict__ pre) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t laneoff = (lane & 31) * 4;
+  const GhLane gl = gh_lane(lane);
+  const tlsgpu_record* D = reinterpret_cast<const tlsgpu_record*>(a.descs);
+  const bool bs_role = wave < (uint32_t)BSW;
+  if (BSW && !bs_role) __builtin_amdgcn_s_setprio(1);
+  uint32_t* q = reinterpret_cast<uint32_t*>(s_lds + Q_OFF);
+
+  fill_aes_lds<NT>();
+  if (a.dbg && threadIdx.x < 32) reinterpret_cast<unsigned long long*>(s_lds + DBG_OFF)[threadIdx.x] = 0;
+
+  const uint32_t rlo = blockIdx.x * a.records_per_group;
+  const uint32_t rhi = min(a.n, rlo + a.records_per_group);
+  uint32_t cur = 0xFFFFFFFFu;
+  uint32_t pos = rlo;
+  while (pos < rhi) {
+    const uint32_t sid = __builtin_amdgcn_readfirstlane(D[pos].session);
+    uint32_t run_end = pos + 1;
+    while (run_end < rhi) {
+      uint32_t p = run_end + lane;
+      uint32_t s = p < rhi ? D[p].session : sid;
+      uint64_t diff = __ballot(p < rhi && s != sid);
+      if (diff) { run_end += __builtin_amdgcn_readfirstlane((uint32_t)__builtin_ctzll(diff)); break; }
+      run_end = min(rhi, run_end + 64);
+    }
+    const bool in_range = sid < a.n_sessions;
+    const DevSession* __restrict__ S = a.sessions + (in_range ? sid : 0);
+    const uint32_t kind = as_const(&S->kind)[0];
+    const bool usable = in_range && is_gcm(kind) && (int)as_const(&S->rounds)[0] == ROUNDS;
+    if (usable) {
+      PhaseClock pc(a.dbg);
+      __syncthreads();  // every wave is done with the previous run (queue, tables)
+      pc.lap(bs_role ? 4 : 12, lane);
+      if (threadIdx.x == 0) *q = pos;
+      if (sid != cur) load_session_tables<NT>(a.gcm_tables + sid);
+      cur = sid;
+      __syncthreads();
+      pc.lap(5, lane);
+      const bool idle = (a.hy_flags & (bs_role ? 4u : 2u)) != 0;
+      for (; !idle;) {
+        if (BSW && bs_role) {
+          const uint32_t r = queue_take(q, 2, lane);
+          if (r >= run_end) break;
+          const uint32_t rb = r + 1;
+          if (rb < run_end && run_end - r >= a.bs_reserve && !(a.hy_flags & 1u)) {
+            RecCtx rc[2];
+            const bool oka = parse_tls<SEAL>(load_desc(D + r), S, a.in, a.out, a.status + r, lane,
+                                             rc[0]);
+            const bool okb = parse_tls<SEAL>(load_desc(D + rb), S, a.in, a.out, a.status + rb,
+                                             lane, rc[1]);
+            if (oka && okb && rc[0].n >= 16384 && rc[1].n >= 16384 &&
+                (((uintptr_t)rc[0].src | (uintptr_t)rc[0].dst | (uintptr_t)rc[1].src |
+                  (uintptr_t)rc[1].dst) & 15) == 0) {
+              gcm_pair_hy<SEAL, ROUNDS>(rc, pre + r, pre + rb, a.status + r, a.status + rb, S,
+                                        lane, laneoff, gl, a.dbg);
+            } else {
+              for (uint32_t m = 0; m < 2; m++) {
+                if (!(m ? okb : oka)) continue;
+                const RecConsts rcc = rec_consts_of(pre + r + m);
+                gcm_record_x4<SEAL, ROUNDS, NB>(m ? rc[1] : rc[0], S, rcc, a.status + r + m, lane,
+                                            laneoff, gl);
+              }
+            }
+          } else {
+            hy_tt_record<SEAL, ROUNDS, NB>(a, pre, r, S, lane, laneoff, gl);
+            if (rb < run_end) hy_tt_record<SEAL, ROUNDS, NB>(a, pre, rb, S, lane, laneoff, gl);
+          }
+        } else {
+          const uint32_t r = queue_take(q, 1, lane);
+          if (r >= run_end) break;
+          hy_tt_record<SEAL, ROUNDS, NB>(a, pre, r, S, lane, laneoff, gl);
+        }
+      }
+    }
+    pos = run_end;
+  }
+  if (a.dbg) {
+    __syncthreads();
+    if (threadIdx.x < 32)
+      atomicAdd(a.dbg + threadIdx.x, reinterpret_cast<unsigned long long*>(s_lds + DBG_OFF)[threadIdx.x]);
+  }
+}
+
+// Per-record constants (RecPre) for the hybrid kernel, one thread per record,
+// T-table from LDS (1 KiB, Te1 = rotl8(Te0)).  Follows rec_consts (gcm_device.h).
+template <bool SEAL, int ROUNDS>
+__global__ __launch_bounds__(256) void gcm_prep_kernel(BatchArgs a, RecPre* __restrict__ pre) {
+  __shared__ uint32_t te[256];
+  te[threadIdx.x] = g_te0.v[threadIdx.x];
+  __syncthreads();
+  const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= a.n) return;
+  const tlsgpu_record d = reinterpret_cast<const tlsgpu_record*>(a.descs)[r];
+  if (d.session >= a.n_sessions) return;
+  const DevSession* S = a.sessions + d.session;
+  if (!is_gcm(S->kind) || (int)S->rounds != ROUNDS) return;
+  auto T0 = [&](uint32_t w, int b) { return te[(w >> (8 * b)) & 0xFF]; };
+  auto T1 = [&](uint32_t w, int b) { return rotl32(te[(w >> (8 * b)) & 0xFF], 8); };
+  auto SB = [&](uint32_t w, int b) { return (te[(w >> (8 * b)) & 0xFF] >> 8) & 0xFF; };
+  const uint32_t* rk = S->rk;
+  uint32_t j0[4];
+  j0[0] = *reinterpret_cast<const uint32_t*>(S->fixed_nonce);
+  j0[1] = j0[2] = 0;
+  j0[3] = 0x01000000u;
+  if (SEAL) {
+    j0[1] = bswap32((uint32_t)(d.seq >> 32));
+    j0[2] = bswap32((uint32_t)d.seq);
+  } else if ((d.len_type & 0xFFFFFFu) >= 8) {
+    const uint8_t* p = a.in + d.in_off;
+    j0[1] = load_u32_bytes(p);
+    j0[2] = load_u32_bytes(p + 4);
+  }
+  // E_K(J0)
+  uint32_t s[4] = {j0[0] ^ rk[0], j0[1] ^ rk[1], j0[2] ^ rk[2], j0[3] ^ rk[3]};
+  for (int rr = 1; rr < ROUNDS; rr++) {
+    uint32_t t[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+      t[c] = T0(s[c], 0) ^ T1(s[(c + 1) & 3], 1) ^
+             rotl32(T0(s[(c + 2) & 3], 2) ^ T1(s[(c + 3) & 3], 3), 16) ^ rk[4 * rr + c];
+#pragma unroll
+    for (int c = 0; c < 4; c++) s[c] = t[c];
+  }
+  RecPre o;
+#pragma unroll
+  for (int c = 0; c < 4; c++)
+    o.ek0[c] = (SB(s[c], 0) | (SB(s[(c + 1) & 3], 1) << 8) | (SB(s[(c + 2) & 3], 2) << 16) |
+                (SB(s[(c + 3) & 3], 3) << 24)) ^ rk[4 * ROUNDS + c];
+  // round-1 constants (ctr_setup) and round-2 constants (rec_consts)
+  const uint32_t s0 = j0[0] ^ rk[0], s1 = j0[1] ^ rk[1], s2 = j0[2] ^ rk[2];
+  uint32_t k1[4];
+  k1[0] = T0(s0, 0) ^ T1(s1, 1) ^ rotl32(T0(s2, 2), 16) ^ rk[4];
+  k1[1] = T0(s1, 0) ^ T1(s2, 1) ^ rotl32(T1(s0, 3), 16) ^ rk[5];
+  k1[2] = T0(s2, 0) ^ rotl32(T0(s0, 2) ^ T1(s1, 3), 16) ^ rk[6];
+  k1[3] = T1(s0, 1) ^ rotl32(T0(s1, 2) ^ T1(s2, 3), 16) ^ rk[7];
+  const uint32_t v0 = rk[3];
+  const uint32_t c2 = k1[2] ^ T1(v0, 1), c3 = k1[3] ^ T0(v0, 0);  // round-1 columns 2, 3
+  o.k1a = k1[0];
+  o.k1b = k1[1];
+  o.k2[0] = rotl32(T0(c2, 2) ^ T1(c3, 3), 16) ^ rk[8];
+  o.k2[1] = T1(c2, 1) ^ rotl32(T0(c3, 2), 16) ^ rk[9];
+  o.k2[2] = T0(c2, 0) ^ T1(c3, 1) ^ rk[10];
+  o.k2[3] = T0(c3, 0) ^ rotl32(T1(c2, 3), 16) ^ rk[11];
+  o.sb2[0] = SB(c2, 0) | (SB(c2, 1) << 8) | (SB(c2, 2) << 16) | (SB(c2, 3) << 24);
+  o.sb2[1] = SB(c3, 0) | (SB(c3, 1) << 8) | (SB(c3, 2) << 16) | (SB(c3, 3) << 24);
+  pre[r] = o;
+}
+
+
+}  // namespace tg

@@ -1,0 +1,35 @@
+// gcm_queue.hip — the per-record prep pass and the T-table queue kernel
+// (gcm_hy_kernel<1024 threads, no bitsliced waves, 2 blocks per lane>), the
+// default AES-GCM TLS batch path.
+#include "gcm_hybrid.h"
+
+namespace tg {
+
+int launch_gcm_prep(const BatchArgs& a, RecPre* pre, bool seal, int rounds, hipStream_t s) {
+  if (a.n == 0) return 0;
+  const dim3 g((a.n + 255) / 256), b(256);
+  if (rounds == 10) {
+    if (seal) hipLaunchKernelGGL((gcm_prep_kernel<true, 10>), g, b, 0, s, a, pre);
+    else hipLaunchKernelGGL((gcm_prep_kernel<false, 10>), g, b, 0, s, a, pre);
+  } else {
+    if (seal) hipLaunchKernelGGL((gcm_prep_kernel<true, 14>), g, b, 0, s, a, pre);
+    else hipLaunchKernelGGL((gcm_prep_kernel<false, 14>), g, b, 0, s, a, pre);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_gcm_queue(const BatchArgs& a, const RecPre* pre, bool seal, int rounds, int groups,
+                     hipStream_t s) {
+  if (a.n == 0) return 0;
+  const dim3 g(groups), b(1024);
+  if (rounds == 10) {
+    if (seal) hipLaunchKernelGGL((gcm_hy_kernel<true, 10, 1024, 0, 2>), g, b, 0, s, a, pre);
+    else hipLaunchKernelGGL((gcm_hy_kernel<false, 10, 1024, 0, 2>), g, b, 0, s, a, pre);
+  } else {
+    if (seal) hipLaunchKernelGGL((gcm_hy_kernel<true, 14, 1024, 0, 2>), g, b, 0, s, a, pre);
+    else hipLaunchKernelGGL((gcm_hy_kernel<false, 14, 1024, 0, 2>), g, b, 0, s, a, pre);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace tg

@@ -70,7 +70,25 @@ struct BatchArgs {
   const uint8_t* in;
   uint8_t* out;
   int32_t* status;
+  uint32_t n_sessions;              // descriptors naming a session >= this are invalid
+  uint32_t bs_reserve;              // hybrid kernel: a bitsliced wave takes a record pair
+                                    // only while >= this many records of the run are left
+  uint32_t hy_flags;                // hybrid kernel experiments (env TLSGPU_HY_FLAGS):
+                                    // 1 = no bitsliced pairs, 2 = T-table waves idle,
+                                    // 4 = bitsliced waves idle
+  unsigned long long* dbg;          // phase timing (PhaseClock), normally null
 };
+
+// Per-record constants of the hybrid kernel (gcm_prep_kernel, one per record,
+// 48 B in a stream-ordered scratch buffer; read back with s_load).  All in the
+// little-endian column form of the T-table path (gcm_device.h rec_consts).
+struct alignas(16) RecPre {
+  uint32_t ek0[4];    // E_K(J0), the tag mask
+  uint32_t k1a, k1b;  // counter-independent parts of round-1 columns 0, 1 (incl. rk1)
+  uint32_t k2[4];     // round-2 constants of the T-table fast path
+  uint32_t sb2[2];    // SubBytes of round-1 output columns 2, 3 (bitsliced round 2)
+};
+static_assert(sizeof(RecPre) == 48, "RecPre layout");
 
 }  // namespace tg
 
@@ -78,7 +96,13 @@ struct BatchArgs {
 namespace tg {
 int launch_gcm(const BatchArgs& a, bool seal, bool raw, int rounds, int groups,
                hipStream_t s);
-int launch_gcm_bs(const BatchArgs& a, bool seal, int rounds, int groups, hipStream_t s);
+int launch_gcm_prep(const BatchArgs& a, RecPre* pre, bool seal, int rounds, hipStream_t s);
+int launch_gcm_queue(const BatchArgs& a, const RecPre* pre, bool seal, int rounds, int groups,
+                     hipStream_t s);
+int launch_gcm_hy10(const BatchArgs& a, const RecPre* pre, bool seal, int bs_waves, int groups,
+                    hipStream_t s);
+int launch_gcm_hy14(const BatchArgs& a, const RecPre* pre, bool seal, int bs_waves, int groups,
+                    hipStream_t s);
 int launch_bs_ecb(const DevSession* sessions, uint32_t session, int rounds, const void* d_in,
                   void* d_out, uint32_t nblocks, hipStream_t s);
 int launch_chacha(const BatchArgs& a, bool seal, bool raw, int groups, hipStream_t s);
