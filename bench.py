@@ -156,6 +156,7 @@ def main():
     if phase:  # diagnostic: per-phase shader cycles of the hybrid kernel, per step
         st = ta.debug_phase_stats(eng, reset=True)
         names = {1: "bs-aes", 2: "bs-consume", 3: "bs-finish", 4: "bs-barrier", 5: "tables",
+                 6: "tt-switch",
                  9: "tt-x4", 10: "tt-rest", 11: "tt-finish", 12: "tt-barrier"}
         for i, nm in names.items():
             if st[2 * i + 1]:

@@ -132,10 +132,13 @@ int tlsgpu_seal_batch(tlsgpu_sessions *t, const tlsgpu_record *d_recs, uint32_t 
  * TLSGPU_GCM_HYBRID: 4 bitsliced waves (AES-CTR on the VALU, pairs of
  * 16-byte-aligned records of >= 16 KiB) beside 4 T-table waves per CU.
  * TLSGPU_GCM_BITSLICE: 8 bitsliced waves per CU.
- * The environment variable TLSGPU_GCM_IMPL=queue|ttable|hybrid|bitslice sets
- * the initial value.  The per-call EVP path always uses TTABLE. */
+ * TLSGPU_GCM_FUSED: 8 waves per CU, each running a bitsliced record pair with
+ * a T-table record interleaved into its AES rounds.
+ * The environment variable TLSGPU_GCM_IMPL=queue|ttable|hybrid|bitslice|fused
+ * sets the initial value.  The per-call EVP path always uses TTABLE. */
 enum tlsgpu_gcm_impl {
-  TLSGPU_GCM_BITSLICE = 0, TLSGPU_GCM_TTABLE = 1, TLSGPU_GCM_HYBRID = 2, TLSGPU_GCM_QUEUE = 3
+  TLSGPU_GCM_BITSLICE = 0, TLSGPU_GCM_TTABLE = 1, TLSGPU_GCM_HYBRID = 2, TLSGPU_GCM_QUEUE = 3,
+  TLSGPU_GCM_FUSED = 4
 };
 int tlsgpu_set_gcm_impl(int impl);
 int tlsgpu_get_gcm_impl(void);

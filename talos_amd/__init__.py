@@ -26,7 +26,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-LIBPATH = os.path.join(HERE, "libtlsgpu.so")
+LIBPATH = os.environ.get("TLSGPU_LIBRARY") or os.path.join(HERE, "libtlsgpu.so")  # override: experiments only
 INCLUDE = os.path.join(ROOT, "include")
 
 AES_128_GCM, AES_256_GCM, CHACHA20_POLY1305, CHACHA20_POLY1305_OLD = 1, 2, 3, 4
@@ -299,13 +299,13 @@ class SessionTable:
             self.handle = None
 
 
-GCM_BITSLICE, GCM_TTABLE, GCM_HYBRID, GCM_QUEUE = 0, 1, 2, 3
+GCM_BITSLICE, GCM_TTABLE, GCM_HYBRID, GCM_QUEUE, GCM_FUSED = 0, 1, 2, 3, 4
 _GCM_IMPLS = {"bitslice": GCM_BITSLICE, "ttable": GCM_TTABLE, "hybrid": GCM_HYBRID,
-              "queue": GCM_QUEUE}
+              "queue": GCM_QUEUE, "fused": GCM_FUSED}
 
 
 def set_gcm_impl(impl: int | str) -> None:
-    """Select the GCM TLS batch kernel (tlsgpu_set_gcm_impl): queue|ttable|hybrid|bitslice."""
+    """Select the GCM TLS batch kernel (tlsgpu_set_gcm_impl): queue|ttable|hybrid|bitslice|fused."""
     if isinstance(impl, str):
         impl = _GCM_IMPLS[impl]
     _check(load_library().tlsgpu_set_gcm_impl(impl), "tlsgpu_set_gcm_impl")

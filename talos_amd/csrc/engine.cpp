@@ -183,12 +183,13 @@ static int initial_gcm_impl() {
   if (v && strcmp(v, "ttable") == 0) return TLSGPU_GCM_TTABLE;
   if (v && strcmp(v, "bitslice") == 0) return TLSGPU_GCM_BITSLICE;
   if (v && strcmp(v, "hybrid") == 0) return TLSGPU_GCM_HYBRID;
+  if (v && strcmp(v, "fused") == 0) return TLSGPU_GCM_FUSED;
   return TLSGPU_GCM_QUEUE;
 }
 static std::atomic<int> g_gcm_impl{initial_gcm_impl()};
 
 extern "C" int tlsgpu_set_gcm_impl(int impl) {
-  if (impl < TLSGPU_GCM_BITSLICE || impl > TLSGPU_GCM_QUEUE)
+  if (impl < TLSGPU_GCM_BITSLICE || impl > TLSGPU_GCM_FUSED)
     return fail(TLSGPU_EINVAL, "unknown gcm impl %d", impl);
   g_gcm_impl.store(impl);
   return TLSGPU_OK;
@@ -282,6 +283,8 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
       if (rc == 0) {
         if (impl == TLSGPU_GCM_QUEUE)
           rc = launch_gcm_queue(a, pre, seal, rounds, groups, s);
+        else if (impl == TLSGPU_GCM_FUSED)
+          rc = (rounds == 10 ? launch_gcm_fused10 : launch_gcm_fused14)(a, pre, seal, groups, s);
         else
           rc = (rounds == 10 ? launch_gcm_hy10 : launch_gcm_hy14)(
               a, pre, seal, impl == TLSGPU_GCM_HYBRID ? 4 : 8, groups, s);

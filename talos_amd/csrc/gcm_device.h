@@ -760,19 +760,21 @@ __device__ __forceinline__ void aes_roundN(uint32_t (&s)[NB][4], uint32_t k0, ui
 #pragma unroll
     for (int c = 0; c < 4; c++)
       s[b][c] = xor3(t[b][4 * c], t[b][4 * c + 1], rotl16(xor3(t[b][4 * c + 2], t[b][4 * c + 3], k[c])));
+#ifdef TG_SCHED_HINTS  // measured 3 % slower than the compiler schedule (queue kernel)
 #pragma unroll
   for (int b = 0; b < NB; b++) {
     __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);  // addresses of block b
     __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);  // its lookups
   }
   __builtin_amdgcn_sched_group_barrier(0x002, 12 * NB, 0);  // combine
+#endif
 }
 
 // NB keystream blocks for counters ctr[b] < 2^16 (aes_ctr16 generalised).
-template <int NB, int ROUNDS>
+template <int NB, int ROUNDS, class Hook>
 __device__ __forceinline__ void aes_ctr16xN(uint32_t (&ks)[NB][4], const uint32_t (&ctr)[NB],
                                             const RecConsts& c, uint32_t rk03, cu32* rk,
-                                            cu32* rkr, uint32_t laneoff) {
+                                            cu32* rkr, uint32_t laneoff, Hook&& hook) {
   uint32_t A[NB][4];
 #pragma unroll
   for (int b = 0; b < NB; b++) {
@@ -784,8 +786,10 @@ __device__ __forceinline__ void aes_ctr16xN(uint32_t (&ks)[NB][4], const uint32_
     A[b][3] = xor3(c.k2[3], TE1(s0, 1), rotl16(TE0(s1, 2)));
   }
 #pragma unroll
-  for (int r = 3; r < ROUNDS; r++)
+  for (int r = 3; r < ROUNDS; r++) {
     aes_roundN<NB>(A, rkr[4 * r], rkr[4 * r + 1], rkr[4 * r + 2], rkr[4 * r + 3], laneoff);
+    hook(r);  // work independent of A (GHASH of the previous group) between rounds
+  }
 #pragma unroll
   for (int b = 0; b < NB; b++) {
     aes_last(A[b][0], A[b][1], A[b][2], A[b][3], rk + 4 * ROUNDS, laneoff);
@@ -793,11 +797,19 @@ __device__ __forceinline__ void aes_ctr16xN(uint32_t (&ks)[NB][4], const uint32_
     for (int w = 0; w < 4; w++) ks[b][w] = A[b][w];
   }
 }
+template <int NB, int ROUNDS>
+__device__ __forceinline__ void aes_ctr16xN(uint32_t (&ks)[NB][4], const uint32_t (&ctr)[NB],
+                                            const RecConsts& c, uint32_t rk03, cu32* rk,
+                                            cu32* rkr, uint32_t laneoff) {
+  aes_ctr16xN<NB, ROUNDS>(ks, ctr, c, rk03, rk, rkr, laneoff, [](int) {});
+}
 
 // Full NB-step groups of a 16-B-aligned record from block `start` on (FAST
-// constants only): 4 keystream blocks per lane in flight, the next group's
-// ciphertext loads issued first.  Advances `start` past the groups done; the
-// caller finishes the record with gcm_blocks.
+// constants only): NB keystream blocks per lane in flight, the next group's
+// input loads issued first, and the GHASH of each group's NB blocks folded
+// into the AES rounds of the following group (the chain's LDS round trips then
+// overlap the AES lookups instead of trailing them).  Advances `start` past
+// the groups done; the caller finishes the record with gcm_blocks.
 template <bool SEAL, int ROUNDS, int NB>
 __device__ __forceinline__ void gcm_blocks_xN(const RecCtx& rc, const DevSession* __restrict__ S,
                                               const RecConsts& rcc, uint32_t (&x)[4],
@@ -811,12 +823,26 @@ __device__ __forceinline__ void gcm_blocks_xN(const RecCtx& rc, const DevSession
   const uint32_t nfull_steps = (rc.n >> 4) / kWave;
   uint32_t t = start / kWave;
   if (t + NB > nfull_steps) return;
-  uint32_t c[NB][4];
+  uint32_t c[NB][4], gp[NB][4];
 #pragma unroll
   for (int b = 0; b < NB; b++) {
     const uint4 v = *reinterpret_cast<const uint4*>(rc.src + 16u * (start + kWave * b + lane));
     c[b][0] = v.x; c[b][1] = v.y; c[b][2] = v.z; c[b][3] = v.w;
   }
+  auto ghash_step = [&](int b) {
+    uint32_t xk[4];
+    mul_k(x, xk, gl);
+    x[0] = xk[0] ^ gp[b][0]; x[1] = xk[1] ^ gp[b][1]; x[2] = xk[2] ^ gp[b][2]; x[3] = xk[3] ^ gp[b][3];
+  };
+  // GHASH step b of the previous group after AES round 3 + 2b (all NB steps
+  // fall inside rounds 3 .. ROUNDS-1)
+  static_assert(3 + 2 * (NB - 1) < ROUNDS, "GHASH steps must fit between the AES rounds");
+  auto hook = [&](int r) {
+#pragma unroll
+    for (int b = 0; b < NB; b++)
+      if (r == 3 + 2 * b) ghash_step(b);
+  };
+  bool first = true;
   for (; t + NB <= nfull_steps; t += NB, start += NB * kWave) {
     const uint32_t i = start + lane;
     uint32_t nx[NB][4];
@@ -830,21 +856,25 @@ __device__ __forceinline__ void gcm_blocks_xN(const RecCtx& rc, const DevSession
     uint32_t ctr[NB], k[NB][4];
 #pragma unroll
     for (int b = 0; b < NB; b++) ctr[b] = ctr0 + i + kWave * b;
-    aes_ctr16xN<NB, ROUNDS>(k, ctr, rcc, rk03, rk, rkr, laneoff);
+    if (first)
+      aes_ctr16xN<NB, ROUNDS>(k, ctr, rcc, rk03, rk, rkr, laneoff);
+    else
+      aes_ctr16xN<NB, ROUNDS>(k, ctr, rcc, rk03, rk, rkr, laneoff, hook);
+    first = false;
 #pragma unroll
     for (int b = 0; b < NB; b++) {
       uint32_t o[4] = {c[b][0] ^ k[b][0], c[b][1] ^ k[b][1], c[b][2] ^ k[b][2], c[b][3] ^ k[b][3]};
       *reinterpret_cast<uint4*>(rc.dst + 16u * (i + kWave * b)) = make_uint4(o[0], o[1], o[2], o[3]);
-      const uint32_t* g = SEAL ? o : c[b];
-      uint32_t xk[4];
-      mul_k(x, xk, gl);
-      x[0] = xk[0] ^ g[0]; x[1] = xk[1] ^ g[1]; x[2] = xk[2] ^ g[2]; x[3] = xk[3] ^ g[3];
+#pragma unroll
+      for (int w = 0; w < 4; w++) gp[b][w] = SEAL ? o[w] : c[b][w];
     }
 #pragma unroll
     for (int b = 0; b < NB; b++)
 #pragma unroll
       for (int w = 0; w < 4; w++) c[b][w] = nx[b][w];
   }
+#pragma unroll
+  for (int b = 0; b < NB; b++) ghash_step(b);  // the last group's GHASH
 }
 
 // gcm_record<SEAL, ROUNDS, true> with the NB-wide full-block loop first.

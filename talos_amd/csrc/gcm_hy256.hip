@@ -7,9 +7,12 @@ namespace tg {
 int launch_gcm_hy14(const BatchArgs& a, const RecPre* pre, bool seal, int bs_waves, int groups,
                      hipStream_t s) {
   if (a.n == 0) return 0;
+#ifdef TG_DEV_QUEUE_ONLY
+  return launch_gcm_queue(a, pre, seal, 14, groups, s);
+#else
   const dim3 g(groups), b(kHyThreads);
 #ifdef TG_DEV_OPEN128
-  if (seal || 14 != 10 || bs_waves != kHyBsWaves) return -1;
+  if (seal || 14 != 10 || bs_waves != kHyBsWaves) return launch_gcm_queue(a, pre, seal, 14, groups, s);
   hipLaunchKernelGGL((gcm_hy_kernel<false, 14, kHyThreads, kHyBsWaves, 4>), g, b, 0, s, a, pre);
 #else
   if (bs_waves == kHyBsWaves) {
@@ -21,6 +24,7 @@ int launch_gcm_hy14(const BatchArgs& a, const RecPre* pre, bool seal, int bs_wav
   }
 #endif
   return hipGetLastError() == hipSuccess ? 0 : -1;
+#endif
 }
 
 }  // namespace tg

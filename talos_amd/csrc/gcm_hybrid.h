@@ -133,9 +133,10 @@ __device__ __forceinline__ void bs_xtime(const uint32_t (&p)[8], uint32_t (&o)[8
 
 // Keystream planes of pass p (blocks 1024p .. 1024p + 1023 of records A and B,
 // u = 2 + lane + 1024p) without the final AddRoundKey.
+// Rounds 1 and 2 (through round 2's AddRoundKey).
 template <int ROUNDS>
-__device__ __forceinline__ void bs_encrypt_ctr(uint32_t (&st)[128], const RecPre* pa,
-                                               const RecPre* pb, uint32_t u, cu32* rk) {
+__device__ __forceinline__ void bs_encrypt_r2(uint32_t (&st)[128], const RecPre* pa,
+                                              const RecPre* pb, uint32_t u, cu32* rk) {
   const SgprMasks km{rk};
   // counter bytes 14 (c14) and 15 (c15) of slot j: u + 64 (j mod 16)
   uint32_t c14[8], c15[8];
@@ -195,6 +196,13 @@ __device__ __forceinline__ void bs_encrypt_ctr(uint32_t (&st)[128], const RecPre
   bs_mixcolumn<1>(st, km, 2);
   bs_mixcolumn<2>(st, km, 2);
   bs_mixcolumn<3>(st, km, 2);
+}
+
+template <int ROUNDS>
+__device__ __forceinline__ void bs_encrypt_ctr(uint32_t (&st)[128], const RecPre* pa,
+                                               const RecPre* pb, uint32_t u, cu32* rk) {
+  const SgprMasks km{rk};
+  bs_encrypt_r2<ROUNDS>(st, pa, pb, u, rk);
 #pragma unroll 1
   for (int r = 3; r < ROUNDS; r++) {
     bs_subbytes(st);

@@ -5,6 +5,10 @@
 
 namespace tg {
 
+#ifndef TG_QUEUE_NB
+#define TG_QUEUE_NB 2
+#endif
+
 int launch_gcm_prep(const BatchArgs& a, RecPre* pre, bool seal, int rounds, hipStream_t s) {
   if (a.n == 0) return 0;
   const dim3 g((a.n + 255) / 256), b(256);
@@ -23,11 +27,11 @@ int launch_gcm_queue(const BatchArgs& a, const RecPre* pre, bool seal, int round
   if (a.n == 0) return 0;
   const dim3 g(groups), b(1024);
   if (rounds == 10) {
-    if (seal) hipLaunchKernelGGL((gcm_hy_kernel<true, 10, 1024, 0, 2>), g, b, 0, s, a, pre);
-    else hipLaunchKernelGGL((gcm_hy_kernel<false, 10, 1024, 0, 2>), g, b, 0, s, a, pre);
+    if (seal) hipLaunchKernelGGL((gcm_hy_kernel<true, 10, 1024, 0, TG_QUEUE_NB>), g, b, 0, s, a, pre);
+    else hipLaunchKernelGGL((gcm_hy_kernel<false, 10, 1024, 0, TG_QUEUE_NB>), g, b, 0, s, a, pre);
   } else {
-    if (seal) hipLaunchKernelGGL((gcm_hy_kernel<true, 14, 1024, 0, 2>), g, b, 0, s, a, pre);
-    else hipLaunchKernelGGL((gcm_hy_kernel<false, 14, 1024, 0, 2>), g, b, 0, s, a, pre);
+    if (seal) hipLaunchKernelGGL((gcm_hy_kernel<true, 14, 1024, 0, TG_QUEUE_NB>), g, b, 0, s, a, pre);
+    else hipLaunchKernelGGL((gcm_hy_kernel<false, 14, 1024, 0, TG_QUEUE_NB>), g, b, 0, s, a, pre);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -101,6 +101,8 @@ int launch_gcm_queue(const BatchArgs& a, const RecPre* pre, bool seal, int round
                      hipStream_t s);
 int launch_gcm_hy10(const BatchArgs& a, const RecPre* pre, bool seal, int bs_waves, int groups,
                     hipStream_t s);
+int launch_gcm_fused10(const BatchArgs& a, const RecPre* pre, bool seal, int groups, hipStream_t s);
+int launch_gcm_fused14(const BatchArgs& a, const RecPre* pre, bool seal, int groups, hipStream_t s);
 int launch_gcm_hy14(const BatchArgs& a, const RecPre* pre, bool seal, int bs_waves, int groups,
                     hipStream_t s);
 int launch_bs_ecb(const DevSession* sessions, uint32_t session, int rounds, const void* d_in,

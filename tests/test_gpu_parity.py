@@ -189,7 +189,7 @@ def gcm_impl(ta):
     ta.set_gcm_impl(prev)
 
 
-@pytest.mark.parametrize("impl", ["queue", "ttable", "hybrid", "bitslice"])
+@pytest.mark.parametrize("impl", ["queue", "ttable", "hybrid", "bitslice", "fused"])
 @pytest.mark.parametrize("name", ["aes-128-gcm", "aes-256-gcm"])
 def test_batch_gcm_impls_all_lengths(ta, engine, oracle, gcm_impl, impl, name):
     gcm_impl(impl)
@@ -202,7 +202,7 @@ BS_LENGTHS = [16384, 16384, 32768, 40000, 16384, 16400, 50000, 16384, 16384, 100
               16384, 65536 + 17, 16384, 16384]
 
 
-@pytest.mark.parametrize("impl", ["hybrid", "bitslice", "queue"])
+@pytest.mark.parametrize("impl", ["hybrid", "bitslice", "queue", "fused"])
 @pytest.mark.parametrize("shift", [0, 3])
 @pytest.mark.parametrize("name", ["aes-128-gcm", "aes-256-gcm"])
 def test_batch_bitsliced_long_records(ta, engine, oracle, gcm_impl, name, shift, impl):
