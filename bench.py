@@ -52,6 +52,21 @@ def algo_bytes_per_record(kind_name: str, length: int, op: str) -> int:
     return rd + wr
 
 
+def main_kernel(kind_name: str, op: str) -> str:
+    """Name of the step's dominant kernel as rocprofv3 lists it."""
+    import talos_amd as ta
+    if "gcm" not in kind_name:
+        return f"tg::chacha_batch_kernel<{'true' if op != 'open' else 'false'}, false>"
+    rounds = 10 if "128" in kind_name else 14
+    seal = "true" if op != "open" else "false"
+    impl = ta.get_gcm_impl()
+    return {"queue": f"tg::gcm_hy_kernel<{seal}, {rounds}, 1024, 0, 2>",
+            "hybrid": f"tg::gcm_hy_kernel<{seal}, {rounds}, 512, 4, 4>",
+            "bitslice": f"tg::gcm_hy_kernel<{seal}, {rounds}, 512, 8, 4>",
+            "fused": f"tg::gcm_fused_kernel<{seal}, {rounds}>",
+            "ttable": f"tg::gcm_batch_kernel<{seal}, false, {rounds}>"}[impl]
+
+
 def cpu_baseline(kind_name: str, rec_len: int, op: str) -> dict | None:
     try:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -72,13 +87,15 @@ def cpu_baseline(kind_name: str, rec_len: int, op: str) -> dict | None:
         return {"value": None, "error": str(exc)[:200]}
 
 
-def load_traffic(config: str):
-    """PMC-measured HBM bytes per launch for this kernel, if a profile was committed."""
+def load_traffic(config: str, kernel: str):
+    """PMC-measured HBM bytes per launch of `kernel` (FETCH_SIZE x2 + WRITE_SIZE,
+    scripts/pmc_summary.py), if a profile of that same kernel was committed."""
     p = os.path.join(ROOT, "profiles", f"pmc_config{config}.json")
     if os.path.exists(p):
         try:
             d = json.load(open(p))
-            return d.get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
+            if kernel in d.get("kernel", ""):
+                return d.get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
         except Exception:
             return None, None
     return None, None
@@ -175,7 +192,7 @@ def main():
     algo = sum(algo_bytes_per_record(kind_name, int(l), op) for l in
                ([rec_len] * wl.n if lengths is None else lengths.tolist()))
     achieved = algo / per_launch_s / 1e9
-    traffic, traffic_src = load_traffic(args.config)
+    traffic, traffic_src = load_traffic(args.config, main_kernel(kind_name, op))
 
     line = {
         "metric": METRIC if args.config == "B" else
@@ -197,12 +214,14 @@ def main():
                                f"{'16 KiB' if rec_len == 16384 else (str(rec_len) + ' B' if rec_len else 'Zipf 64 B-16 KiB')}"
                                f" records, {per_gpu} records/GPU, device-resident",
                    "records_per_gpu": per_gpu, "sessions_per_gpu": sessions,
+                   "gcm_impl": ta.get_gcm_impl() if "gcm" in kind_name else None,
                    "payload_bytes_per_gpu": total_len, "parallelism": f"batch split x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "algorithmic_bytes_per_launch": algo,
-                     "kernel": "gcm_batch_kernel<open>" if "gcm" in kind_name
-                     else "chacha_batch_kernel", "traffic_source": traffic_src},
+                     "kernel": main_kernel(kind_name, op), "traffic_source": traffic_src,
+                     "timing": "HIP events around each whole step on the engine stream "
+                               "(prep pass + status memset + main kernel)"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(kind_name, rec_len or 1400, op)
