@@ -274,11 +274,255 @@ __device__ void cc_record(const CcRec& rc, uint32_t tag_len, int32_t* status_slo
   }
 }
 
+// ---------------------------------------------------------------------------
+// LDS-staged data path (TLS batches).  With one record per lane a wave's
+// 16-B accesses touch 64 records (64 cache lines per instruction).  Here the
+// data moves in 128-B steps through a per-wave LDS tile of 64 rows: lane l
+// serves pieces of records 8k + l/8 (k = 0..7), so each load/store instruction
+// covers 8 records x 128 contiguous bytes; each lane then en/decrypts and MACs
+// its own record's row.  Rows are padded to 144 B so the row-wise ds_read_b128
+// of the 64 lanes (same column, different rows) is bank-conflict-free.
+constexpr uint32_t kCcStep = 128;
+constexpr uint32_t kCcRow = kCcStep + 16;
+constexpr int kCcThreads = 256;
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
+  const uint32_t lo = __shfl((uint32_t)v, (int)src), hi = __shfl((uint32_t)(v >> 32), (int)src);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ void lds_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <bool SEAL>
+__device__ void cc_record_staged(const CcRec& rc, bool active, uint32_t tag_len,
+                                 int32_t* status_slot, uint32_t lane, uint8_t* tile) {
+  uint32_t st[16], ks[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) st[i] = rc.st[i];
+  Poly p;
+  PolyStream ps = {{0, 0, 0, 0}, 0};
+  const uint32_t n = active ? rc.n : 0u;
+  if (active) {
+    chacha_block(st, ks);  // counter 0 block -> one-time Poly1305 key
+    poly_init(p, ks);
+    if (!rc.old) {
+      poly_block(p, rc.ad[0], rc.ad[1], rc.ad[2], rc.ad[3], 1u << 24);  // 13-B AD, pad16
+    } else {
+      for (uint32_t o = 0; o < rc.ad_len; o++) ps_byte(p, ps, (rc.ad[o >> 2] >> (8 * (o & 3))) & 0xFF);
+      ps_u64(p, ps, rc.ad_len);
+    }
+  }
+  // pieces this lane moves: records 8k + lane/8, bytes 16 (lane % 8) of each
+  // step; the records' pointers and lengths are fetched with ds_bpermute per
+  // step (keeping 8 x 5 of them in VGPRs would cost a wave per SIMD)
+  const uint32_t piece = 16u * (lane & 7);
+  uint32_t steps = (n + kCcStep - 1) / kCcStep;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) steps = max(steps, (uint32_t)__shfl_xor((int)steps, m));
+  uint8_t* myrow = tile + lane * kCcRow;
+  uint64_t ctr = ((uint64_t)st[13] << 32) | st[12];
+  // gather of step s: 8 records x 128 B per load instruction, into registers
+  // (issued one step ahead, so the loads fly during the previous step's math)
+  auto gather = [&](uint32_t base, uint4 (&v)[8]) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t off = base + piece;
+      const uint32_t rr = 8u * k + (lane >> 3);
+      const uint32_t snk = __shfl(n, (int)rr);
+      // ds_bpermute outside the branch: an inactive source lane reads as 0
+      const uint64_t srck = shfl64((uint64_t)(uintptr_t)rc.src, rr);
+      v[k] = make_uint4(0, 0, 0, 0);
+      if (off < snk) {
+        const uint8_t* src = (const uint8_t*)(uintptr_t)srck + off;
+        if (off + 16 <= snk && ((uintptr_t)src & 15) == 0) {
+          v[k] = *reinterpret_cast<const uint4*>(src);
+        } else {
+          uint32_t w[4] = {0, 0, 0, 0};
+          const uint32_t nb = min(16u, snk - off);
+          for (uint32_t b = 0; b < nb; b++) w[b >> 2] |= (uint32_t)src[b] << (8 * (b & 3));
+          v[k] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+      }
+    }
+  };
+  uint4 pf[8];
+  gather(0, pf);
+  for (uint32_t s = 0; s < steps; s++) {
+    const uint32_t base = s * kCcStep;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      *reinterpret_cast<uint4*>(tile + (8u * k + (lane >> 3)) * kCcRow + piece) = pf[k];
+    if (s + 1 < steps) gather(base + kCcStep, pf);
+    lds_wave_sync();
+    // en/decrypt + MAC this lane's row: 2 ChaCha blocks
+    if (base < n) {
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const uint32_t o64 = base + 64u * h;
+        if (o64 >= n) break;
+        ctr += 1;
+        st[12] = (uint32_t)ctr;
+        st[13] = (uint32_t)(ctr >> 32);
+        chacha_block(st, ks);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint32_t o = o64 + 16 * q;
+          if (o >= n) break;
+          const uint32_t nb = min(16u, n - o);
+          const uint4 t = *reinterpret_cast<const uint4*>(myrow + 64 * h + 16 * q);
+          uint32_t in[4] = {t.x, t.y, t.z, t.w};
+          uint32_t ob[4] = {in[0] ^ ks[4 * q], in[1] ^ ks[4 * q + 1], in[2] ^ ks[4 * q + 2],
+                            in[3] ^ ks[4 * q + 3]};
+          if (nb < 16) {  // zero the bytes past the record (MAC pad16 / staged garbage)
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+              int32_t b = (int32_t)nb - 4 * w;
+              uint32_t keep = b >= 4 ? 0xFFFFFFFFu : (b <= 0 ? 0u : ((1u << (8 * b)) - 1u));
+              ob[w] &= keep;
+              in[w] &= keep;
+            }
+          }
+          *reinterpret_cast<uint4*>(myrow + 64 * h + 16 * q) = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+          const uint32_t* c = SEAL ? ob : in;
+          if (!rc.old) {
+            poly_block(p, c[0], c[1], c[2], c[3], 1u << 24);
+          } else {
+            for (uint32_t k = 0; k < nb; k++) ps_byte(p, ps, (c[k >> 2] >> (8 * (k & 3))) & 0xFF);
+          }
+        }
+      }
+    }
+    lds_wave_sync();
+    // scatter
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t off = base + piece;
+      const uint32_t rr = 8u * k + (lane >> 3);
+      const uint32_t snk = __shfl(n, (int)rr);
+      const uint64_t dstk = shfl64((uint64_t)(uintptr_t)rc.dst, rr);
+      if (off < snk) {
+        uint8_t* dst = (uint8_t*)(uintptr_t)dstk + off;
+        const uint4 v = *reinterpret_cast<const uint4*>(tile + rr * kCcRow + piece);
+        if (off + 16 <= snk && ((uintptr_t)dst & 15) == 0) {
+          *reinterpret_cast<uint4*>(dst) = v;
+        } else {
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+          const uint32_t nb = min(16u, snk - off);
+          for (uint32_t b = 0; b < nb; b++) dst[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+        }
+      }
+    }
+    lds_wave_sync();
+  }
+  if (!active) return;
+  if (!rc.old) {
+    poly_block(p, rc.ad_len, 0, n, 0, 1u << 24);  // le64(ad_len) || le64(ct_len)
+  } else {
+    ps_u64(p, ps, n);
+    ps_final(p, ps);
+  }
+  uint32_t mac[4];
+  poly_finish(p, mac);
+  if (SEAL) {
+    for (uint32_t k = 0; k < tag_len; k++) rc.tag_out[k] = (uint8_t)(mac[k >> 2] >> (8 * (k & 3)));
+    *status_slot = rc.ok_status;
+  } else {
+    uint32_t diff = 0;
+    for (uint32_t k = 0; k < tag_len; k++)
+      diff |= rc.tag_in[k] ^ ((mac[k >> 2] >> (8 * (k & 3))) & 0xFF);
+    if (diff) {
+      for (uint64_t o = 0; o < rc.zero_len; o++) rc.dst[o] = 0;
+      *status_slot = TLSGPU_REC_BAD_MAC;
+    } else {
+      *status_slot = rc.ok_status;
+    }
+  }
+}
+
 __device__ __forceinline__ void cc_state(uint32_t st[16], const DevSession* S) {
   st[0] = 0x61707865u; st[1] = 0x3320646eu; st[2] = 0x79622d32u; st[3] = 0x6b206574u;
   const uint32_t* kw = reinterpret_cast<const uint32_t*>(S->chacha_key);
 #pragma unroll
   for (int i = 0; i < 8; i++) st[4 + i] = kw[i];
+}
+
+// TLS descriptor -> CcRec (t1_enc.c:832-975 for the ChaCha suites).  Returns
+// false when the record is not this kernel's (other kind / bad session: status
+// untouched) or publicly invalid (status written).
+template <bool SEAL>
+__device__ __forceinline__ bool cc_parse_tls(const BatchArgs& a, uint32_t r, CcRec& rc,
+                                             uint32_t& tag_len) {
+  int32_t* slot = a.status + r;
+  const DevSession* S;
+  const tlsgpu_record d = reinterpret_cast<const tlsgpu_record*>(a.descs)[r];
+  if (d.session >= a.n_sessions) return false;  // status stays PUBLIC_INVALID
+  S = a.sessions + d.session;
+  uint32_t kind = S->kind;
+  if (kind != TLSGPU_CHACHA20_POLY1305 && kind != TLSGPU_CHACHA20_POLY1305_OLD) return false;
+  tag_len = S->tag_len;
+  rc.old = kind == TLSGPU_CHACHA20_POLY1305_OLD;
+  uint32_t len = d.len_type & 0xFFFFFFu, type = d.len_type >> 24;
+  const uint8_t* ip = a.in + d.in_off;
+  uint8_t* op = a.out + d.out_off;
+  if (SEAL) {
+    rc.n = len;
+    rc.src = ip;
+    rc.dst = op;
+    rc.tag_out = op + len;
+    rc.ok_status = (int32_t)(len + tag_len);
+    rc.zero_len = 0;
+  } else {
+    if (len < tag_len) {  // t1_enc.c:958-959 (no explicit nonce for ChaCha)
+      *slot = TLSGPU_REC_PUBLIC_INVALID;
+      return false;
+    }
+    rc.n = len - tag_len;
+    rc.src = ip;
+    rc.dst = op;
+    rc.tag_in = ip + rc.n;
+    rc.ok_status = (int32_t)rc.n;
+    rc.zero_len = rc.n;
+  }
+  // nonce: RFC 7905 fixed(12) XOR (0^4 || seq) ; old: fixed(0) || seq
+  uint32_t sq_hi = bswap32((uint32_t)(d.seq >> 32)), sq_lo = bswap32((uint32_t)d.seq);
+  cc_state(rc.st, S);
+  const uint32_t* fx = reinterpret_cast<const uint32_t*>(S->fixed_nonce);
+  rc.st[12] = 0;
+  if (!rc.old) {
+    rc.st[13] = fx[0];
+    rc.st[14] = fx[1] ^ sq_hi;
+    rc.st[15] = fx[2] ^ sq_lo;
+  } else {
+    rc.st[13] = 0;
+    rc.st[14] = sq_hi;
+    rc.st[15] = sq_lo;
+  }
+  uint32_t v = S->version;
+  rc.aad_ptr = nullptr;
+  rc.ad_len = 13;
+  rc.ad[0] = sq_hi;
+  rc.ad[1] = sq_lo;
+  rc.ad[2] = type | (((v >> 8) & 0xFF) << 8) | ((v & 0xFF) << 16) | (((rc.n >> 8) & 0xFF) << 24);
+  rc.ad[3] = rc.n & 0xFF;
+  return true;
+}
+
+// TLS batches: LDS-staged coalesced data path (cc_record_staged).
+template <bool SEAL>
+__global__ __launch_bounds__(kCcThreads) void chacha_tls_kernel(BatchArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t tiles[kCcThreads / kWave][kWave * kCcRow];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  CcRec rc;
+  rc.src = nullptr;
+  rc.dst = nullptr;
+  rc.n = 0;
+  rc.old = false;
+  uint32_t tag_len = 16;
+  const bool active = r < a.n && cc_parse_tls<SEAL>(a, r, rc, tag_len);
+  cc_record_staged<SEAL>(rc, active, tag_len, a.status + (active ? r : 0), lane, tiles[wave]);
 }
 
 template <bool SEAL, bool RAW>
@@ -324,69 +568,33 @@ __global__ __launch_bounds__(256) void chacha_batch_kernel(BatchArgs a) {
     }
     rc.zero_len = j.max_out;
   } else {
-    const tlsgpu_record d = reinterpret_cast<const tlsgpu_record*>(a.descs)[r];
-    if (d.session >= a.n_sessions) return;  // status stays PUBLIC_INVALID
-    S = a.sessions + d.session;
-    uint32_t kind = S->kind;
-    if (kind != TLSGPU_CHACHA20_POLY1305 && kind != TLSGPU_CHACHA20_POLY1305_OLD) return;
-    tag_len = S->tag_len;
-    rc.old = kind == TLSGPU_CHACHA20_POLY1305_OLD;
-    uint32_t len = d.len_type & 0xFFFFFFu, type = d.len_type >> 24;
-    const uint8_t* ip = a.in + d.in_off;
-    uint8_t* op = a.out + d.out_off;
-    if (SEAL) {
-      rc.n = len;
-      rc.src = ip;
-      rc.dst = op;
-      rc.tag_out = op + len;
-      rc.ok_status = (int32_t)(len + tag_len);
-      rc.zero_len = 0;
-    } else {
-      if (len < tag_len) {  // t1_enc.c:958-959 (no explicit nonce for ChaCha)
-        *slot = TLSGPU_REC_PUBLIC_INVALID;
-        return;
-      }
-      rc.n = len - tag_len;
-      rc.src = ip;
-      rc.dst = op;
-      rc.tag_in = ip + rc.n;
-      rc.ok_status = (int32_t)rc.n;
-      rc.zero_len = rc.n;
-    }
-    // nonce: RFC 7905 fixed(12) XOR (0^4 || seq) ; old: fixed(0) || seq
-    uint32_t sq_hi = bswap32((uint32_t)(d.seq >> 32)), sq_lo = bswap32((uint32_t)d.seq);
-    cc_state(rc.st, S);
-    const uint32_t* fx = reinterpret_cast<const uint32_t*>(S->fixed_nonce);
-    rc.st[12] = 0;
-    if (!rc.old) {
-      rc.st[13] = fx[0];
-      rc.st[14] = fx[1] ^ sq_hi;
-      rc.st[15] = fx[2] ^ sq_lo;
-    } else {
-      rc.st[13] = 0;
-      rc.st[14] = sq_hi;
-      rc.st[15] = sq_lo;
-    }
-    uint32_t v = S->version;
-    rc.aad_ptr = nullptr;
-    rc.ad_len = 13;
-    rc.ad[0] = sq_hi;
-    rc.ad[1] = sq_lo;
-    rc.ad[2] = type | (((v >> 8) & 0xFF) << 8) | ((v & 0xFF) << 16) | (((rc.n >> 8) & 0xFF) << 24);
-    rc.ad[3] = rc.n & 0xFF;
+    if (!cc_parse_tls<SEAL>(a, r, rc, tag_len)) return;
   }
   cc_record<SEAL>(rc, tag_len, slot);
+}
+
+// TLSGPU_CHACHA_LEGACY=1 selects the per-lane data path for TLS batches too
+// (A/B measurement of the staged kernel).
+static bool getenv_legacy_chacha() {
+  static const bool v = [] {
+    const char* e = getenv("TLSGPU_CHACHA_LEGACY");
+    return e && *e && *e != '0';
+  }();
+  return v;
 }
 
 int launch_chacha(const BatchArgs& a, bool seal, bool raw, int groups, hipStream_t s) {
   (void)groups;
   if (a.n == 0) return 0;
   dim3 grid((a.n + 255) / 256), block(256);
+  const bool staged = !raw && !getenv_legacy_chacha();
   if (seal) {
     if (raw) hipLaunchKernelGGL((chacha_batch_kernel<true, true>), grid, block, 0, s, a);
+    else if (staged) hipLaunchKernelGGL((chacha_tls_kernel<true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((chacha_batch_kernel<true, false>), grid, block, 0, s, a);
   } else {
     if (raw) hipLaunchKernelGGL((chacha_batch_kernel<false, true>), grid, block, 0, s, a);
+    else if (staged) hipLaunchKernelGGL((chacha_tls_kernel<false>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((chacha_batch_kernel<false, false>), grid, block, 0, s, a);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
