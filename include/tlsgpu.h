@@ -54,6 +54,12 @@ enum tlsgpu_aead {
  */
 #define TLSGPU_REC_BAD_MAC (-1)
 #define TLSGPU_REC_PUBLIC_INVALID (-2)
+/* tlsgpu_open_wire only: an earlier record of the same stream failed, so
+ * ssl3_get_record would never have returned this one (not delivered). */
+#define TLSGPU_REC_SKIPPED (-3)
+/* tlsgpu_open_wire only: plaintext longer than SSL3_RT_MAX_PLAIN_LENGTH
+ * (s3_pkt.c:465-469) -> record_overflow alert, not delivered. */
+#define TLSGPU_REC_OVERFLOW (-4)
 
 /* Largest plaintext per record the batch kernels accept: 65534 AES blocks, so
  * GCM counters 2..nb+1 stay below 2^16 (TLS records are <= 16 KiB + 2 KiB,
@@ -123,6 +129,58 @@ int tlsgpu_open_batch(tlsgpu_sessions *t, const tlsgpu_record *d_recs, uint32_t 
     const uint8_t *d_in, uint8_t *d_out, int32_t *d_status, void *stream);
 int tlsgpu_seal_batch(tlsgpu_sessions *t, const tlsgpu_record *d_recs, uint32_t n,
     const uint8_t *d_in, uint8_t *d_out, int32_t *d_status, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Wire-record framing: ssl3_get_record (ssl/s3_pkt.c:279-495)
+ * for the AEAD suites over raw read-ahead bytes, many connections at once.
+ *
+ * Each stream is one connection's read direction: wire_len bytes of TLS
+ * records (5-byte header + fragment) at d_wire + wire_off, as ssl3_read_n
+ * leaves them in rbuf with read_ahead (s3_pkt.c:134-267).  Per stream, records
+ * are framed in order with the header checks of s3_pkt.c:304-341,376:
+ *   version != stream version (unless TLSGPU_WIRE_FIRST_PACKET) -> alert
+ *   protocol_version (70); major != 3 -> error without alert (alert = -1);
+ *   length > rbuf_len - 5 (rbuf_len 0 = the reference's 16712) or
+ *   length > SSL3_RT_MAX_ENCRYPTED_LENGTH (16704) -> record_overflow (22);
+ *   a record whose fragment is not complete ends the stream's batch (the
+ *   caller keeps the bytes from `consumed` on for the next call).
+ * Framed records get descriptors (written to d_recs, grouped by stream, seq =
+ * stream seq + index) and are opened IN PLACE like tls1_enc(s, 0)
+ * (t1_enc.c:951-955: plaintext at fragment + explicit nonce length).  Then,
+ * in order, the first record with an AEAD failure or a plaintext longer than
+ * 16384 B ends the stream: bad_record_mac (20) for TLSGPU_REC_BAD_MAC,
+ * decryption_failed (21) for TLSGPU_REC_PUBLIC_INVALID, record_overflow (22)
+ * for TLSGPU_REC_OVERFLOW; later records of that stream get
+ * TLSGPU_REC_SKIPPED.  Zero-length plaintexts are delivered with status 0 (the
+ * reference reads on, s3_pkt.c:486-488).
+ *
+ * max_records bounds d_recs / d_status; streams whose records do not fit are
+ * truncated at a record boundary (their `records`/`consumed` say how far).
+ * d_total receives the number of descriptors written.  Asynchronous. */
+#define TLSGPU_WIRE_FIRST_PACKET 1u	/* s->first_packet: accept any version */
+typedef struct tlsgpu_wire_stream {
+	uint64_t wire_off;	/* first byte of the stream in d_wire */
+	uint32_t wire_len;	/* bytes available */
+	uint32_t session;	/* read-direction session id */
+	uint64_t seq;		/* read sequence number of the first record */
+	uint16_t version;	/* s->version, e.g. 0x0303 */
+	uint16_t flags;		/* TLSGPU_WIRE_* */
+	uint32_t rbuf_len;	/* read buffer size for the overflow check; 0 = 16712 */
+} tlsgpu_wire_stream;
+
+typedef struct tlsgpu_wire_result {
+	uint32_t first;		/* index of the stream's first record in d_recs / d_status */
+	uint32_t records;	/* records framed (descriptors written) */
+	uint32_t delivered;	/* records before the first failure */
+	uint32_t consumed;	/* bytes of the framed records (header + fragment) */
+	int32_t alert;		/* 0, a fatal TLS AlertDescription, or -1 (error, no alert) */
+	uint32_t alert_record;	/* index within the stream of the record that failed */
+	uint32_t reserved[2];
+} tlsgpu_wire_result;
+
+int tlsgpu_open_wire(tlsgpu_sessions *t, const tlsgpu_wire_stream *d_streams,
+    uint32_t n_streams, uint8_t *d_wire, uint32_t max_records, tlsgpu_record *d_recs,
+    int32_t *d_status, tlsgpu_wire_result *d_results, uint32_t *d_total, void *stream);
 
 /* GCM TLS batch kernel selection (process-wide; results are identical).
  * TLSGPU_GCM_QUEUE (default): a prep pass computes every record's E_K(J0) and

@@ -44,6 +44,17 @@ REC_PUBLIC_INVALID = -2   # tls1_enc returns 0
 MAX_RECORD = 65534 * 16
 
 # tlsgpu_record (include/tlsgpu.h), 32 bytes
+# tlsgpu_wire_stream / tlsgpu_wire_result (include/tlsgpu.h)
+WIRE_STREAM_DTYPE = np.dtype([("wire_off", "<u8"), ("wire_len", "<u4"), ("session", "<u4"),
+                              ("seq", "<u8"), ("version", "<u2"), ("flags", "<u2"),
+                              ("rbuf_len", "<u4")])
+WIRE_RESULT_DTYPE = np.dtype([("first", "<u4"), ("records", "<u4"), ("delivered", "<u4"),
+                              ("consumed", "<u4"), ("alert", "<i4"), ("alert_record", "<u4"),
+                              ("reserved", "<u4", (2,))])
+assert WIRE_STREAM_DTYPE.itemsize == 32 and WIRE_RESULT_DTYPE.itemsize == 32
+WIRE_FIRST_PACKET = 1
+REC_BAD_MAC, REC_PUBLIC_INVALID, REC_SKIPPED, REC_OVERFLOW = -1, -2, -3, -4
+
 RECORD_DTYPE = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("seq", "<u8"),
                          ("session", "<u4"), ("len_type", "<u4")])
 assert RECORD_DTYPE.itemsize == 32
@@ -116,6 +127,7 @@ def load_library(path: str = LIBPATH) -> C.CDLL:
         "tlsgpu_get_gcm_impl": (i32, []),
         "tlsgpu_aes_ecb_bitsliced": (i32, [vp, u32, vp, vp, u32, vp]),
         "tlsgpu_debug_phase_stats": (i32, [vp, C.POINTER(C.c_ulonglong), i32]),
+        "tlsgpu_open_wire": (i32, [vp, vp, u32, vp, u32, vp, vp, vp, vp, vp]),
         "tlsgpu_malloc": (i32, [vp, C.c_size_t, C.POINTER(vp)]),
         "tlsgpu_free": (i32, [vp, vp]),
         "tlsgpu_host_alloc": (i32, [vp, C.c_size_t, C.POINTER(vp)]),
@@ -333,6 +345,15 @@ def aes_ecb_bitsliced(table: "SessionTable", session: int, d_in: int, d_out: int
 
 def len_type(length: int, rtype: int) -> int:
     return ((rtype & 0xFF) << 24) | (length & 0xFFFFFF)
+
+
+def open_wire(table: "SessionTable", d_streams: int, n_streams: int, d_wire: int,
+              max_records: int, d_recs: int, d_status: int, d_results: int, d_total: int,
+              stream: int | None = None) -> None:
+    """Frame and open raw TLS wire records in place (tlsgpu_open_wire, ssl3_get_record)."""
+    _check(table.lib.tlsgpu_open_wire(table.handle, d_streams, n_streams, d_wire, max_records,
+                                      d_recs, d_status, d_results, d_total, stream),
+           "tlsgpu_open_wire")
 
 
 def open_batch(table: SessionTable, d_recs: int, n: int, d_in: int, d_out: int,

@@ -325,6 +325,31 @@ extern "C" int tlsgpu_seal_batch(tlsgpu_sessions* t, const tlsgpu_record* d_recs
                    stream ? (hipStream_t)stream : t->eng->stream, true, false);
 }
 
+extern "C" int tlsgpu_open_wire(tlsgpu_sessions* t, const tlsgpu_wire_stream* d_streams,
+                                uint32_t n_streams, uint8_t* d_wire, uint32_t max_records,
+                                tlsgpu_record* d_recs, int32_t* d_status,
+                                tlsgpu_wire_result* d_results, uint32_t* d_total, void* stream) {
+  if (!t || !d_total || (n_streams && (!d_streams || !d_wire || !d_results)) ||
+      (max_records && (!d_recs || !d_status)))
+    return fail(TLSGPU_EINVAL, "bad arguments");
+  HIPCHK(hipSetDevice(t->eng->device));
+  hipStream_t s = stream ? (hipStream_t)stream : t->eng->stream;
+  HIPCHK(hipMemsetAsync(d_total, 0, sizeof(uint32_t), s));
+  if (n_streams == 0) return TLSGPU_OK;
+  // unused record slots name no session (0xFFFFFFFF): the open kernels skip them
+  if (max_records) HIPCHK(hipMemsetAsync(d_recs, 0xFF, sizeof(tlsgpu_record) * (size_t)max_records, s));
+  if (launch_wire_frame(d_streams, n_streams, d_wire, t->d_sess, t->capacity, max_records, d_recs,
+                        d_results, d_total, s))
+    return fail(TLSGPU_EHIP, "wire frame launch: %s", hipGetErrorString(hipGetLastError()));
+  if (max_records) {
+    int rc = run_batch(t, d_recs, max_records, d_wire, d_wire, d_status, s, false, false);
+    if (rc != TLSGPU_OK) return rc;
+  }
+  if (launch_wire_finish(n_streams, d_results, d_status, s))
+    return fail(TLSGPU_EHIP, "wire finish launch: %s", hipGetErrorString(hipGetLastError()));
+  return TLSGPU_OK;
+}
+
 extern "C" int tlsgpu_fill_synthetic(tlsgpu_engine* e, uint8_t* d_out, uint64_t stride,
                                      uint32_t span_len, uint32_t n, uint64_t seed,
                                      uint64_t index0, void* stream) {

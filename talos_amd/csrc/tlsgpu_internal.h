@@ -111,6 +111,12 @@ int launch_chacha(const BatchArgs& a, bool seal, bool raw, int groups, hipStream
 int launch_session_install(DevSession* sessions, DevGcmTables* tables,
                            const tlsgpu_session_params* d_params, uint32_t first,
                            uint32_t n, hipStream_t s);
+int launch_wire_frame(const tlsgpu_wire_stream* streams, uint32_t n_streams, const uint8_t* wire,
+                      const DevSession* sessions, uint32_t n_sessions, uint32_t max_records,
+                      tlsgpu_record* recs, tlsgpu_wire_result* results, uint32_t* total,
+                      hipStream_t s);
+int launch_wire_finish(uint32_t n_streams, tlsgpu_wire_result* results, int32_t* status,
+                       hipStream_t s);
 int launch_fill_synthetic(uint8_t* d_out, uint64_t stride, uint32_t span_len,
                           uint32_t n, uint64_t seed, uint64_t index0, hipStream_t s);
 }  // namespace tg
