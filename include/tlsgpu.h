@@ -201,6 +201,19 @@ enum tlsgpu_gcm_impl {
 int tlsgpu_set_gcm_impl(int impl);
 int tlsgpu_get_gcm_impl(void);
 
+/* EVP coalescing queue.  Turns on batching for the per-call
+ * EVP_AEAD_* drop-in: contexts initialised afterwards take a slot of one shared
+ * device session pool (pool_sessions, default 1024; contexts beyond it keep a
+ * private table and the per-call path), and their seal/open calls are queued;
+ * a dispatcher thread runs everything that arrives within window_us (or
+ * max_jobs, default 4096) as one raw batch per direction and wakes the callers.
+ * Outputs, return values and zero-fill are those of the per-call path.  Calling
+ * it again adjusts window_us / max_jobs.  The environment variables
+ * TLSGPU_EVP_BATCH_US / TLSGPU_EVP_POOL do the same at library load.
+ * tlsgpu_evp_batch_stats: batches run and jobs served so far. */
+int tlsgpu_evp_set_batching(unsigned window_us, unsigned max_jobs, unsigned pool_sessions);
+int tlsgpu_evp_batch_stats(uint64_t *batches, uint64_t *jobs);
+
 /* Diagnostic: hybrid-kernel phase timing.  With TLSGPU_PHASE_STATS=1 in the
  * environment, the first call allocates 32 device counters (shader cycles and
  * event counts per phase, summed over waves) that later hybrid launches fill;

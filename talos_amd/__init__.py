@@ -128,6 +128,8 @@ def load_library(path: str = LIBPATH) -> C.CDLL:
         "tlsgpu_aes_ecb_bitsliced": (i32, [vp, u32, vp, vp, u32, vp]),
         "tlsgpu_debug_phase_stats": (i32, [vp, C.POINTER(C.c_ulonglong), i32]),
         "tlsgpu_open_wire": (i32, [vp, vp, u32, vp, u32, vp, vp, vp, vp, vp]),
+        "tlsgpu_evp_set_batching": (i32, [C.c_uint, C.c_uint, C.c_uint]),
+        "tlsgpu_evp_batch_stats": (i32, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "tlsgpu_malloc": (i32, [vp, C.c_size_t, C.POINTER(vp)]),
         "tlsgpu_free": (i32, [vp, vp]),
         "tlsgpu_host_alloc": (i32, [vp, C.c_size_t, C.POINTER(vp)]),
@@ -410,6 +412,19 @@ class EvpAead:
 
     def cleanup(self) -> None:
         self.lib.EVP_AEAD_CTX_cleanup(C.byref(self.ctx))
+
+
+def evp_set_batching(window_us: int, max_jobs: int = 0, pool_sessions: int = 0) -> None:
+    """Turn on / retune the EVP coalescing queue (tlsgpu_evp_set_batching)."""
+    _check(load_library().tlsgpu_evp_set_batching(window_us, max_jobs, pool_sessions),
+           "tlsgpu_evp_set_batching")
+
+
+def evp_batch_stats() -> tuple[int, int]:
+    """(batches run, jobs served) by the EVP coalescing queue."""
+    b, j = C.c_uint64(0), C.c_uint64(0)
+    _check(load_library().tlsgpu_evp_batch_stats(C.byref(b), C.byref(j)), "tlsgpu_evp_batch_stats")
+    return b.value, j.value
 
 
 def header_symbols() -> list[str]:

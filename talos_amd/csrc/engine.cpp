@@ -10,13 +10,17 @@
 // no CPU cipher path.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/tlsgpu.h"
@@ -502,10 +506,56 @@ static tlsgpu_engine* default_engine() {
 }
 
 struct AeadState {
-  tlsgpu_sessions* sess;
+  tlsgpu_sessions* sess;  // the shared EVP pool table (slot >= 0) or a private one
+  int slot;               // session id in sess
   int kind;
   unsigned tag_len;
 };
+
+// ---------------------------------------------------------------------------
+// EVP coalescing queue (TaLoS make_asynchronous_ecall,
+// src/talos/enclaveshim/enclaveshim_ecalls.c:457-610, in GPU form).
+//
+// With batching on (tlsgpu_evp_set_batching or TLSGPU_EVP_BATCH_US > 0),
+// EVP_AEAD_CTX_init installs the key into a slot of one shared device session
+// pool, and every EVP_AEAD_CTX_seal/open posts a job and blocks on it.  A
+// dispatcher thread collects the jobs that arrive within the window (or
+// max_jobs), packs their inputs into one pinned staging buffer, runs ONE raw
+// batch per direction over all of them (jobs sorted by session so the GCM
+// kernel reloads its tables once per context), copies the outputs back and
+// wakes the callers.  Results are the same as the per-call path, bit for bit;
+// calls stay synchronous for the caller, throughput comes from concurrency.
+struct EvpJob {
+  const AeadState* st;
+  bool seal;
+  unsigned char* out;
+  size_t max_out;
+  const unsigned char *nonce, *in, *ad;
+  size_t nonce_len, in_len, ad_len;
+  int32_t status;
+  bool done;
+  bool failed;
+};
+
+struct EvpBatcher {
+  std::mutex mu;
+  std::condition_variable cv_work, cv_done;
+  std::vector<EvpJob*> q;
+  std::thread th;
+  bool stop = false;
+  unsigned window_us = 0, max_jobs = 4096;
+  tlsgpu_sessions* pool = nullptr;
+  std::vector<int> free_slots;
+  hipStream_t stream = nullptr;
+  uint8_t* h_stage = nullptr;
+  uint8_t* d_stage = nullptr;
+  size_t cap = 0;
+  uint64_t batches = 0, jobs_done = 0;
+  void run(std::vector<EvpJob*>& jobs);
+  void loop();
+};
+static EvpBatcher* g_batcher = nullptr;
+static std::mutex g_batcher_mu;
 
 // Per-thread staging for one call: device buffer + stream (calls on one ctx may
 // run concurrently from several threads, evp.h:1273-1274).
@@ -557,9 +607,20 @@ extern "C" int EVP_AEAD_CTX_init(EVP_AEAD_CTX* ctx, const EVP_AEAD* aead, const 
   if (!st) return 0;
   st->kind = aead->kind;
   st->tag_len = (unsigned)tag_len;
-  if (tlsgpu_sessions_create(e, 1, &st->sess) != TLSGPU_OK) {
-    delete st;
-    return 0;
+  st->slot = -1;
+  {
+    std::lock_guard<std::mutex> lk(g_batcher_mu);
+    if (g_batcher && !g_batcher->free_slots.empty()) {
+      st->slot = g_batcher->free_slots.back();
+      g_batcher->free_slots.pop_back();
+      st->sess = g_batcher->pool;
+    }
+  }
+  if (st->slot < 0) {
+    if (tlsgpu_sessions_create(e, 1, &st->sess) != TLSGPU_OK) {
+      delete st;
+      return 0;
+    }
   }
   tlsgpu_session_params p;
   memset(&p, 0, sizeof(p));
@@ -568,13 +629,20 @@ extern "C" int EVP_AEAD_CTX_init(EVP_AEAD_CTX* ctx, const EVP_AEAD* aead, const 
   memcpy(p.key, key, key_len);
   p.tag_len = (uint32_t)tag_len;
   p.version = 0x0303;
-  int rc = tlsgpu_sessions_install(st->sess, 0, 1, &p);
+  int rc = tlsgpu_sessions_install(st->sess, st->slot < 0 ? 0 : (uint32_t)st->slot, 1, &p);
   memset(&p, 0, sizeof(p));
   if (rc != TLSGPU_OK) {
-    tlsgpu_sessions_destroy(st->sess);
+    if (st->slot < 0) {
+      tlsgpu_sessions_destroy(st->sess);
+    } else {
+      std::lock_guard<std::mutex> lk(g_batcher_mu);
+      g_batcher->free_slots.push_back(st->slot);
+    }
     delete st;
     return 0;
   }
+  if (st->slot < 0) st->slot = 0;
+  else st->slot |= 0x40000000;  // marks a pool slot (see pool_slot)
   ctx->aead_state = st;
   return 1;
 }
@@ -584,10 +652,17 @@ extern "C" void EVP_AEAD_CTX_cleanup(EVP_AEAD_CTX* ctx) {
   auto* st = (AeadState*)ctx->aead_state;
   if (st) {
     // scrub the device key material before freeing (explicit_bzero analogue)
+    const bool pooled = (st->slot & 0x40000000) != 0;
+    const uint32_t slot = (uint32_t)(st->slot & 0x3FFFFFFF);
     hipSetDevice(st->sess->eng->device);
-    hipMemset(st->sess->d_sess, 0, sizeof(DevSession));
-    hipMemset(st->sess->d_gcm, 0, sizeof(DevGcmTables));
-    tlsgpu_sessions_destroy(st->sess);
+    hipMemset(st->sess->d_sess + slot, 0, sizeof(DevSession));
+    hipMemset(st->sess->d_gcm + slot, 0, sizeof(DevGcmTables));
+    if (pooled) {
+      std::lock_guard<std::mutex> lk(g_batcher_mu);
+      g_batcher->free_slots.push_back((int)slot);
+    } else {
+      tlsgpu_sessions_destroy(st->sess);
+    }
     delete st;
   }
   ctx->aead_state = nullptr;
@@ -606,6 +681,20 @@ static int gpu_call(const AeadState* st, bool seal, unsigned char* out, size_t* 
                     size_t max_out_len, const unsigned char* nonce, size_t nonce_len,
                     const unsigned char* in, size_t in_len, const unsigned char* ad,
                     size_t ad_len) {
+  if (st->slot & 0x40000000) {  // pooled context: post to the coalescing queue
+    EvpJob j = {st, seal, out, max_out_len, nonce, in, ad, nonce_len, in_len, ad_len,
+                TLSGPU_REC_BAD_MAC, false, false};
+    EvpBatcher* b = g_batcher;
+    std::unique_lock<std::mutex> lk(b->mu);
+    b->q.push_back(&j);
+    b->cv_work.notify_one();
+    b->cv_done.wait(lk, [&] { return j.done; });
+    lk.unlock();
+    if (j.failed) return -1;
+    if (j.status < 0) return 0;
+    *out_len = (size_t)j.status;
+    return 1;
+  }
   auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
   size_t out_bytes = seal ? in_len + st->tag_len : (max_out_len > in_len ? max_out_len : in_len);
   size_t o_job = 0, o_status = al(sizeof(RawJob)), o_nonce = o_status + 256;
@@ -750,4 +839,170 @@ error:
   memset(out, 0, max_out_len);  // evp_aead.c:137-143
   *out_len = 0;
   return 0;
+}
+
+// ---------------------------------------------------------------------------
+// EVP coalescing queue: dispatcher
+
+void EvpBatcher::loop() {
+  std::unique_lock<std::mutex> lk(mu);
+  for (;;) {
+    cv_work.wait(lk, [&] { return stop || !q.empty(); });
+    if (q.empty() && stop) return;
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(window_us);
+    while (!stop && q.size() < max_jobs &&
+           cv_work.wait_until(lk, deadline) != std::cv_status::timeout) {
+    }
+    std::vector<EvpJob*> jobs;
+    const size_t take = std::min<size_t>(q.size(), max_jobs);
+    jobs.assign(q.begin(), q.begin() + take);
+    q.erase(q.begin(), q.begin() + take);
+    lk.unlock();
+    run(jobs);
+    lk.lock();
+    for (EvpJob* j : jobs) j->done = true;
+    batches++;
+    jobs_done += jobs.size();
+    cv_done.notify_all();
+  }
+}
+
+void EvpBatcher::run(std::vector<EvpJob*>& jobs) {
+  // one raw batch per direction; sessions grouped inside each
+  std::stable_sort(jobs.begin(), jobs.end(), [](const EvpJob* a, const EvpJob* b) {
+    if (a->seal != b->seal) return a->seal > b->seal;
+    return (a->st->slot & 0x3FFFFFFF) < (b->st->slot & 0x3FFFFFFF);
+  });
+  const size_t n = jobs.size();
+  auto al = [](size_t v) { return (v + 15) & ~(size_t)15; };
+  // layout: [RawJob x n][status x n][inputs ...][outputs ...]
+  const size_t o_status = al(sizeof(RawJob) * n);
+  size_t o = al(o_status + 4 * n);
+  std::vector<size_t> o_nonce(n), o_ad(n), o_in(n), o_out(n), out_bytes(n);
+  for (size_t i = 0; i < n; i++) {
+    const EvpJob* j = jobs[i];
+    o_nonce[i] = o; o = al(o + j->nonce_len);
+    o_ad[i] = o;    o = al(o + j->ad_len);
+    o_in[i] = o;    o = al(o + j->in_len);
+  }
+  const size_t o_outputs = o;
+  for (size_t i = 0; i < n; i++) {
+    const EvpJob* j = jobs[i];
+    out_bytes[i] = j->seal ? j->in_len + j->st->tag_len : std::max(j->max_out, j->in_len);
+    o_out[i] = o;
+    o = al(o + out_bytes[i] + 1);
+  }
+  const size_t total = o;
+  auto fail_all = [&] {
+    for (EvpJob* j : jobs) j->failed = true;
+  };
+  if (hipSetDevice(pool->eng->device) != hipSuccess) return fail_all();
+  if (cap < total) {
+    if (h_stage) (void)hipHostFree(h_stage);
+    if (d_stage) (void)hipFree(d_stage);
+    h_stage = nullptr;
+    d_stage = nullptr;
+    cap = 0;
+    size_t want = std::max(total, (size_t)(4u << 20));
+    if (hipHostMalloc((void**)&h_stage, want, hipHostMallocDefault) != hipSuccess ||
+        hipMalloc((void**)&d_stage, want) != hipSuccess)
+      return fail_all();
+    cap = want;
+  }
+  RawJob* rj = reinterpret_cast<RawJob*>(h_stage);
+  for (size_t i = 0; i < n; i++) {
+    const EvpJob* j = jobs[i];
+    if (j->nonce_len) memcpy(h_stage + o_nonce[i], j->nonce, j->nonce_len);
+    if (j->ad_len) memcpy(h_stage + o_ad[i], j->ad, j->ad_len);
+    if (j->in_len) memcpy(h_stage + o_in[i], j->in, j->in_len);
+    rj[i].in = (uint64_t)(d_stage + o_in[i]);
+    rj[i].out = (uint64_t)(d_stage + o_out[i]);
+    rj[i].nonce = (uint64_t)(d_stage + o_nonce[i]);
+    rj[i].aad = (uint64_t)(d_stage + o_ad[i]);
+    rj[i].in_len = (uint32_t)j->in_len;
+    rj[i].nonce_len = (uint32_t)j->nonce_len;
+    rj[i].aad_len = (uint32_t)j->ad_len;
+    rj[i].session = (uint32_t)(j->st->slot & 0x3FFFFFFF);
+    rj[i].max_out = j->max_out;
+  }
+  if (hipMemcpyAsync(d_stage, h_stage, o_outputs, hipMemcpyHostToDevice, stream) != hipSuccess)
+    return fail_all();
+  size_t nseal = 0;
+  while (nseal < n && jobs[nseal]->seal) nseal++;
+  int32_t* d_status = reinterpret_cast<int32_t*>(d_stage + o_status);
+  if (nseal && run_batch(pool, d_stage, (uint32_t)nseal, nullptr, nullptr, d_status, stream, true,
+                         true) != TLSGPU_OK)
+    return fail_all();
+  if (n > nseal && run_batch(pool, d_stage + sizeof(RawJob) * nseal, (uint32_t)(n - nseal), nullptr,
+                             nullptr, d_status + nseal, stream, false, true) != TLSGPU_OK)
+    return fail_all();
+  if (hipMemcpyAsync(h_stage + o_status, d_stage + o_status, 4 * n, hipMemcpyDeviceToHost,
+                     stream) != hipSuccess ||
+      hipMemcpyAsync(h_stage + o_outputs, d_stage + o_outputs, total - o_outputs,
+                     hipMemcpyDeviceToHost, stream) != hipSuccess ||
+      hipStreamSynchronize(stream) != hipSuccess)
+    return fail_all();
+  const int32_t* hs = reinterpret_cast<const int32_t*>(h_stage + o_status);
+  for (size_t i = 0; i < n; i++) {
+    EvpJob* j = jobs[i];
+    j->status = hs[i];
+    if (hs[i] >= 0) {
+      if (hs[i]) memcpy(j->out, h_stage + o_out[i], (size_t)hs[i]);
+    } else if (j->max_out) {
+      memcpy(j->out, h_stage + o_out[i], j->max_out);  // the kernel's zero-fill
+    }
+  }
+}
+
+extern "C" int tlsgpu_evp_set_batching(unsigned window_us, unsigned max_jobs,
+                                       unsigned pool_sessions) {
+  std::lock_guard<std::mutex> lk(g_batcher_mu);
+  if (g_batcher) {  // already running: adjust the window / batch size only
+    std::lock_guard<std::mutex> lk2(g_batcher->mu);
+    g_batcher->window_us = window_us;
+    if (max_jobs) g_batcher->max_jobs = max_jobs;
+    return TLSGPU_OK;
+  }
+  if (window_us == 0 && max_jobs == 0) return TLSGPU_OK;  // stays off
+  tlsgpu_engine* e = default_engine();
+  if (!e) return fail(TLSGPU_EHIP, "no GPU engine for the EVP path");
+  auto* b = new (std::nothrow) EvpBatcher();
+  if (!b) return fail(TLSGPU_ENOMEM, "batcher");
+  b->window_us = window_us;
+  b->max_jobs = max_jobs ? max_jobs : 4096;
+  const uint32_t cap = pool_sessions ? pool_sessions : 1024;
+  int rc = tlsgpu_sessions_create(e, cap, &b->pool);
+  if (rc != TLSGPU_OK) {
+    delete b;
+    return rc;
+  }
+  HIPCHK(hipSetDevice(e->device));
+  HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+  for (int i = (int)cap - 1; i >= 0; i--) b->free_slots.push_back(i);
+  b->th = std::thread([b] { b->loop(); });
+  g_batcher = b;
+  return TLSGPU_OK;
+}
+
+extern "C" int tlsgpu_evp_batch_stats(uint64_t* batches, uint64_t* jobs) {
+  std::lock_guard<std::mutex> lk(g_batcher_mu);
+  uint64_t nb = 0, nj = 0;
+  if (g_batcher) {
+    std::lock_guard<std::mutex> lk2(g_batcher->mu);
+    nb = g_batcher->batches;
+    nj = g_batcher->jobs_done;
+  }
+  if (batches) *batches = nb;
+  if (jobs) *jobs = nj;
+  return TLSGPU_OK;
+}
+
+// TLSGPU_EVP_BATCH_US=<window> turns the queue on at load time for unchanged
+// applications (LD_PRELOAD); TLSGPU_EVP_POOL sets the pooled context count.
+__attribute__((constructor)) static void evp_batching_from_env() {
+  const char* w = getenv("TLSGPU_EVP_BATCH_US");
+  if (!w || !*w) return;
+  const char* p = getenv("TLSGPU_EVP_POOL");
+  tlsgpu_evp_set_batching((unsigned)strtoul(w, nullptr, 10), 0,
+                          p ? (unsigned)strtoul(p, nullptr, 10) : 0);
 }
