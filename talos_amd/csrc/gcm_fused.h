@@ -3,15 +3,15 @@
 // Every wave runs two pipelines in one instruction stream:
 //   * a bitsliced record pair (gcm_hybrid.h: AES-CTR keystream of 2 x 1024
 //     blocks as 128 bit planes, VALU only), and
-//   * a T-table record ("TT record"), 2 blocks per lane per group, whose
+//   * a T-table record ("TT record"), 1 block per lane per group, whose
 //     AES rounds and GHASH steps are cut into phases: phase K runs after
 //     S-box K of a bitsliced round, issues its LDS lookups there and combines
 //     them one S-box (~85 VALU ops) later, so the LDS latency hides behind the
 //     bitsliced work and the LDS pipe (idle in a pure bitsliced wave) and the
 //     VALU (two thirds idle in a pure T-table wave) are both used.
-// One TT group (128 blocks) per bitsliced round: for AES-128 the 8 fused rounds
-// of a pass (rounds 3..9 and the final round) carry exactly one 16 KiB TT
-// record per record pair.  TT record boundaries are handled after a pass's
+// One TT group (64 blocks, one per lane) per bitsliced round: for AES-128 the
+// 8 fused rounds of a pass (rounds 3..9 and the final round) carry half of a
+// 16 KiB TT record per record pair.  TT record boundaries are handled after a pass's
 // consume step, where the bitsliced state is dead.
 #pragma once
 #include "gcm_hybrid.h"
@@ -26,18 +26,20 @@ struct TtRec {
   uint32_t ctr0;       // inc32(J0)
   uint32_t g, ng;      // next 2-step group, number of full groups (uniform)
   uint32_t x[4];       // this lane's GHASH chain (LE words)
-  uint32_t c[2][4];    // ciphertext (open) / plaintext (seal) of group g
+  uint32_t c[4];       // ciphertext (open) / plaintext (seal) of group g (one block per lane)
   bool on;             // uniform: a TT record is in flight
 };
 
-// Per-round temporaries of the TT group (live between phases).
+// Per-round temporaries of the TT group (live between phases).  One block per
+// lane and quarter-width GHASH steps keep this at ~40 VGPRs beside the 128
+// bit planes (two blocks and half-width steps spilled in the round loop).
 struct TtTmp {
-  uint32_t A[2][4];    // AES state of the two blocks
-  uint32_t t[2][16];   // lookups in flight
-  uint32_t cn[2][4];   // next group's input, loaded at phase 0
-  uint32_t gin[2][4];  // GHASH inputs of this group
+  uint32_t A[4];       // AES state of the lane's block
+  uint32_t t[16];      // lookups in flight
+  uint32_t cn[4];      // next group's input, loaded at phase 0
+  uint32_t gin[4];     // GHASH input of this group
   uint32_t y[4];       // rotated chain value for the GHASH lookups
-  uint4 h[8];          // GHASH lookups in flight (half a mul_k)
+  uint4 h[4];          // GHASH lookups in flight (a quarter of mul_k)
   uint32_t acc[4];
 };
 
@@ -51,17 +53,13 @@ __device__ __forceinline__ void gh_rot(const uint32_t x[4], uint32_t y[4], const
   y[3] = __builtin_amdgcn_alignbyte(b0, b3, g.r);
 }
 
-// half H (0: positions of y[0], y[1]; 1: y[2], y[3]) of x * H^64 (mul_k)
-template <int H>
+// quarter Q (positions of y[Q]) of x * H^64 (mul_k)
+template <int Q>
 __device__ __forceinline__ void gh_issue(TtTmp& w, const GhLane& g) {
-#pragma unroll
-  for (int qq = 0; qq < 2; qq++) {
-    const int q = 2 * H + qq;
-    w.h[4 * qq + 0] = lds_u128(KT_OFF + kaddr<0>(w.y[q], g.cq[q]));
-    w.h[4 * qq + 1] = lds_u128(KT_OFF + kaddr<1>(w.y[q], g.cq[q]));
-    w.h[4 * qq + 2] = lds_u128(KT_OFF + kaddr<2>(w.y[q], g.cq[q]));
-    w.h[4 * qq + 3] = lds_u128(KT_OFF + kaddr<3>(w.y[q], g.cq[q]));
-  }
+  w.h[0] = lds_u128(KT_OFF + kaddr<0>(w.y[Q], g.cq[Q]));
+  w.h[1] = lds_u128(KT_OFF + kaddr<1>(w.y[Q], g.cq[Q]));
+  w.h[2] = lds_u128(KT_OFF + kaddr<2>(w.y[Q], g.cq[Q]));
+  w.h[3] = lds_u128(KT_OFF + kaddr<3>(w.y[Q], g.cq[Q]));
 }
 template <bool FIRST>
 __device__ __forceinline__ void gh_combine(TtTmp& w) {
@@ -70,43 +68,31 @@ __device__ __forceinline__ void gh_combine(TtTmp& w) {
   a[1] = xor3(w.h[0].y, w.h[1].y, w.h[2].y);
   a[2] = xor3(w.h[0].z, w.h[1].z, w.h[2].z);
   a[3] = xor3(w.h[0].w, w.h[1].w, w.h[2].w);
-  a[0] = xor3(a[0], w.h[3].x, w.h[4].x);
-  a[1] = xor3(a[1], w.h[3].y, w.h[4].y);
-  a[2] = xor3(a[2], w.h[3].z, w.h[4].z);
-  a[3] = xor3(a[3], w.h[3].w, w.h[4].w);
-  a[0] = xor3(a[0], w.h[5].x, w.h[6].x);
-  a[1] = xor3(a[1], w.h[5].y, w.h[6].y);
-  a[2] = xor3(a[2], w.h[5].z, w.h[6].z);
-  a[3] = xor3(a[3], w.h[5].w, w.h[6].w);
   if (FIRST) {
-    w.acc[0] = a[0] ^ w.h[7].x; w.acc[1] = a[1] ^ w.h[7].y;
-    w.acc[2] = a[2] ^ w.h[7].z; w.acc[3] = a[3] ^ w.h[7].w;
+    w.acc[0] = a[0] ^ w.h[3].x; w.acc[1] = a[1] ^ w.h[3].y;
+    w.acc[2] = a[2] ^ w.h[3].z; w.acc[3] = a[3] ^ w.h[3].w;
   } else {
-    w.acc[0] = xor3(w.acc[0], a[0], w.h[7].x); w.acc[1] = xor3(w.acc[1], a[1], w.h[7].y);
-    w.acc[2] = xor3(w.acc[2], a[2], w.h[7].z); w.acc[3] = xor3(w.acc[3], a[3], w.h[7].w);
+    w.acc[0] = xor3(w.acc[0], a[0], w.h[3].x); w.acc[1] = xor3(w.acc[1], a[1], w.h[3].y);
+    w.acc[2] = xor3(w.acc[2], a[2], w.h[3].z); w.acc[3] = xor3(w.acc[3], a[3], w.h[3].w);
   }
 }
 
-// T-table round lookups of the two blocks (LAST: final-round pattern)
+// T-table round lookups of the lane's block (LAST: final-round pattern)
 template <bool LAST>
 __device__ __forceinline__ void tt_issue_round(TtTmp& w, uint32_t laneoff) {
 #pragma unroll
-  for (int b = 0; b < 2; b++)
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      w.t[b][4 * c + 0] = TE0(w.A[b][c], 0);
-      w.t[b][4 * c + 1] = LAST ? TE0(w.A[b][(c + 1) & 3], 1) : TE1(w.A[b][(c + 1) & 3], 1);
-      w.t[b][4 * c + 2] = TE0(w.A[b][(c + 2) & 3], 2);
-      w.t[b][4 * c + 3] = TE1(w.A[b][(c + 3) & 3], 3);
-    }
+  for (int c = 0; c < 4; c++) {
+    w.t[4 * c + 0] = TE0(w.A[c], 0);
+    w.t[4 * c + 1] = LAST ? TE0(w.A[(c + 1) & 3], 1) : TE1(w.A[(c + 1) & 3], 1);
+    w.t[4 * c + 2] = TE0(w.A[(c + 2) & 3], 2);
+    w.t[4 * c + 3] = TE1(w.A[(c + 3) & 3], 3);
+  }
 }
 __device__ __forceinline__ void tt_combine_round(TtTmp& w, cu32* rkr, int r) {
 #pragma unroll
-  for (int b = 0; b < 2; b++)
-#pragma unroll
-    for (int c = 0; c < 4; c++)
-      w.A[b][c] = xor3(w.t[b][4 * c], w.t[b][4 * c + 1],
-                       rotl16(xor3(w.t[b][4 * c + 2], w.t[b][4 * c + 3], rkr[4 * r + c])));
+  for (int c = 0; c < 4; c++)
+    w.A[c] = xor3(w.t[4 * c], w.t[4 * c + 1],
+                  rotl16(xor3(w.t[4 * c + 2], w.t[4 * c + 3], rkr[4 * r + c])));
 }
 
 // Phase K of a TT group (see the file comment).  Phases: 0 round-1 lookups
@@ -118,77 +104,58 @@ __device__ __forceinline__ void tt_phase(TtRec& tt, TtTmp& w, const DevSession* 
                                          uint32_t lane, uint32_t laneoff, const GhLane& gl) {
   cu32* rk = as_const(S->rk);
   cu32* rkr = as_const(S->rk_rot);
-  const uint32_t base = tt.g * 128u;
+  const uint32_t base = tt.g * 64u;
   if constexpr (K == 0) {
-    const uint32_t rk03 = rk[3];
-#pragma unroll
-    for (int b = 0; b < 2; b++) {
-      const uint32_t v = bswap32(tt.ctr0 + base + 64u * b + lane) ^ rk03;
-      w.t[b][0] = TE1(v, 3);
-      w.t[b][1] = TE0(v, 2);
-    }
+    const uint32_t v = bswap32(tt.ctr0 + base + lane) ^ rk[3];
+    w.t[0] = TE1(v, 3);
+    w.t[1] = TE0(v, 2);
     if (tt.g + 1 < tt.ng) {
-#pragma unroll
-      for (int b = 0; b < 2; b++) {
-        const uint4 v = *reinterpret_cast<const uint4*>(tt.rc.src + 16u * (base + 128u + 64u * b + lane));
-        w.cn[b][0] = v.x; w.cn[b][1] = v.y; w.cn[b][2] = v.z; w.cn[b][3] = v.w;
-      }
+      const uint4 c = *reinterpret_cast<const uint4*>(tt.rc.src + 16u * (base + 64u + lane));
+      w.cn[0] = c.x; w.cn[1] = c.y; w.cn[2] = c.z; w.cn[3] = c.w;
     }
   } else if constexpr (K == 1) {
-#pragma unroll
-    for (int b = 0; b < 2; b++) {
-      const uint32_t s0 = tt.rcc.k1a ^ rotl16(w.t[b][0]), s1 = tt.rcc.k1b ^ rotl16(w.t[b][1]);
-      w.t[b][0] = TE0(s0, 0); w.t[b][1] = TE1(s1, 1);
-      w.t[b][2] = TE0(s1, 0); w.t[b][3] = TE1(s0, 3);
-      w.t[b][4] = TE0(s0, 2); w.t[b][5] = TE1(s1, 3);
-      w.t[b][6] = TE1(s0, 1); w.t[b][7] = TE0(s1, 2);
-    }
+    const uint32_t s0 = tt.rcc.k1a ^ rotl16(w.t[0]), s1 = tt.rcc.k1b ^ rotl16(w.t[1]);
+    w.t[0] = TE0(s0, 0); w.t[1] = TE1(s1, 1);
+    w.t[2] = TE0(s1, 0); w.t[3] = TE1(s0, 3);
+    w.t[4] = TE0(s0, 2); w.t[5] = TE1(s1, 3);
+    w.t[6] = TE1(s0, 1); w.t[7] = TE0(s1, 2);
   } else if constexpr (K == 2) {
-#pragma unroll
-    for (int b = 0; b < 2; b++) {
-      w.A[b][0] = xor3(tt.rcc.k2[0], w.t[b][0], w.t[b][1]);
-      w.A[b][1] = xor3(tt.rcc.k2[1], w.t[b][2], rotl16(w.t[b][3]));
-      w.A[b][2] = tt.rcc.k2[2] ^ rotl16(w.t[b][4] ^ w.t[b][5]);
-      w.A[b][3] = xor3(tt.rcc.k2[3], w.t[b][6], rotl16(w.t[b][7]));
-    }
+    w.A[0] = xor3(tt.rcc.k2[0], w.t[0], w.t[1]);
+    w.A[1] = xor3(tt.rcc.k2[1], w.t[2], rotl16(w.t[3]));
+    w.A[2] = tt.rcc.k2[2] ^ rotl16(w.t[4] ^ w.t[5]);
+    w.A[3] = xor3(tt.rcc.k2[3], w.t[6], rotl16(w.t[7]));
     tt_issue_round<ROUNDS == 3>(w, laneoff);
   } else if constexpr (K < ROUNDS) {
     tt_combine_round(w, rkr, K);              // round K (3 .. ROUNDS-1)
     tt_issue_round<K + 1 == ROUNDS>(w, laneoff);
   } else if constexpr (K == ROUNDS) {
-    uint32_t o[2][4];
+    uint32_t o[4];
 #pragma unroll
-    for (int b = 0; b < 2; b++) {
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        const uint32_t lo = __builtin_amdgcn_perm(w.t[b][4 * c + 1], w.t[b][4 * c + 0], 0x0C0C0501u);
-        const uint32_t hi = __builtin_amdgcn_perm(w.t[b][4 * c + 3], w.t[b][4 * c + 2], 0x07020C0Cu);
-        o[b][c] = tt.c[b][c] ^ xor3(lo, hi, rk[4 * ROUNDS + c]);
-        w.gin[b][c] = SEAL ? o[b][c] : tt.c[b][c];
-      }
-      *reinterpret_cast<uint4*>(tt.rc.dst + 16u * (base + 64u * b + lane)) =
-          make_uint4(o[b][0], o[b][1], o[b][2], o[b][3]);
+    for (int c = 0; c < 4; c++) {
+      const uint32_t lo = __builtin_amdgcn_perm(w.t[4 * c + 1], w.t[4 * c + 0], 0x0C0C0501u);
+      const uint32_t hi = __builtin_amdgcn_perm(w.t[4 * c + 3], w.t[4 * c + 2], 0x07020C0Cu);
+      o[c] = tt.c[c] ^ xor3(lo, hi, rk[4 * ROUNDS + c]);
+      w.gin[c] = SEAL ? o[c] : tt.c[c];
     }
+    *reinterpret_cast<uint4*>(tt.rc.dst + 16u * (base + lane)) = make_uint4(o[0], o[1], o[2], o[3]);
     gh_rot(tt.x, w.y, gl);
     gh_issue<0>(w, gl);
-  } else if constexpr (K == ROUNDS + 1 || K == ROUNDS + 3) {
+  } else if constexpr (K == ROUNDS + 1) {
     gh_combine<true>(w);
     gh_issue<1>(w, gl);
   } else if constexpr (K == ROUNDS + 2) {
     gh_combine<false>(w);
-    uint32_t xn[4];
-#pragma unroll
-    for (int c = 0; c < 4; c++) xn[c] = w.acc[c] ^ w.gin[0][c];
-    gh_rot(xn, w.y, gl);
-    gh_issue<0>(w, gl);
+    gh_issue<2>(w, gl);
+  } else if constexpr (K == ROUNDS + 3) {
+    gh_combine<false>(w);
+    gh_issue<3>(w, gl);
   } else if constexpr (K == ROUNDS + 4) {
     gh_combine<false>(w);
 #pragma unroll
-    for (int c = 0; c < 4; c++) tt.x[c] = w.acc[c] ^ w.gin[1][c];
-#pragma unroll
-    for (int b = 0; b < 2; b++)
-#pragma unroll
-      for (int c = 0; c < 4; c++) tt.c[b][c] = w.cn[b][c];
+    for (int c = 0; c < 4; c++) {
+      tt.x[c] = w.acc[c] ^ w.gin[c];
+      tt.c[c] = w.cn[c];
+    }
     tt.g++;
   }
 }
@@ -247,16 +214,13 @@ __device__ __forceinline__ void tt_begin(TtRec& tt, const BatchArgs& a, const Re
     tt.slot = a.status + r;
     tt.ctr0 = bswap32(tt.rc.j0[3]) + 1u;
     const bool aligned = ((((uintptr_t)tt.rc.src) | ((uintptr_t)tt.rc.dst)) & 15) == 0;
-    tt.ng = aligned ? (tt.rc.n >> 4) / 128u : 0u;
+    tt.ng = aligned ? (tt.rc.n >> 4) / 64u : 0u;
     tt.g = 0;
 #pragma unroll
     for (int c = 0; c < 4; c++) tt.x[c] = (lane == 63) ? bswap32(tt.rc.aad_be[c]) : 0u;
     if (tt.ng) {
-#pragma unroll
-      for (int b = 0; b < 2; b++) {
-        const uint4 v = *reinterpret_cast<const uint4*>(tt.rc.src + 16u * (64u * b + lane));
-        tt.c[b][0] = v.x; tt.c[b][1] = v.y; tt.c[b][2] = v.z; tt.c[b][3] = v.w;
-      }
+      const uint4 v = *reinterpret_cast<const uint4*>(tt.rc.src + 16u * lane);
+      tt.c[0] = v.x; tt.c[1] = v.y; tt.c[2] = v.z; tt.c[3] = v.w;
     }
     tt.on = true;
     return;
@@ -270,7 +234,7 @@ __device__ __forceinline__ bool tt_end_if_done(TtRec& tt, const DevSession* __re
                                                uint32_t laneoff, const GhLane& gl, bool force) {
   if (!tt.on || (!force && tt.g < tt.ng)) return false;
   const CtrConst none = {};
-  gcm_blocks<SEAL, ROUNDS, true>(tt.rc, S, tt.rcc, none, tt.x, tt.g * 128u, lane, laneoff, gl);
+  gcm_blocks<SEAL, ROUNDS, true>(tt.rc, S, tt.rcc, none, tt.x, tt.g * 64u, lane, laneoff, gl);
   gcm_finish<SEAL>(tt.rc, tt.x, tt.rcc.ek0, S, tt.slot, lane, gl);
   tt.on = false;
   return true;
