@@ -93,9 +93,9 @@ extern "C" int tlsgpu_engine_create(int device, tlsgpu_engine** out) {
 
 extern "C" void tlsgpu_engine_destroy(tlsgpu_engine* e) {
   if (!e) return;
-  hipSetDevice(e->device);
-  hipStreamSynchronize(e->stream);
-  hipStreamDestroy(e->stream);
+  (void)hipSetDevice(e->device);
+  (void)hipStreamSynchronize(e->stream);
+  (void)hipStreamDestroy(e->stream);
   delete e;
 }
 
@@ -122,7 +122,7 @@ extern "C" int tlsgpu_sessions_create(tlsgpu_engine* e, uint32_t capacity, tlsgp
   memset(t->have, 0, sizeof(t->have));
   if (hipMalloc(&t->d_sess, sizeof(DevSession) * (size_t)capacity) != hipSuccess ||
       hipMalloc(&t->d_gcm, sizeof(DevGcmTables) * (size_t)capacity) != hipSuccess) {
-    hipFree(t->d_sess);
+    (void)hipFree(t->d_sess);
     delete t;
     return fail(TLSGPU_ENOMEM, "device session table (%u sessions)", capacity);
   }
@@ -134,10 +134,10 @@ extern "C" int tlsgpu_sessions_create(tlsgpu_engine* e, uint32_t capacity, tlsgp
 
 extern "C" void tlsgpu_sessions_destroy(tlsgpu_sessions* t) {
   if (!t) return;
-  hipSetDevice(t->eng->device);
-  hipStreamSynchronize(t->eng->stream);
-  hipFree(t->d_sess);
-  hipFree(t->d_gcm);
+  (void)hipSetDevice(t->eng->device);
+  (void)hipStreamSynchronize(t->eng->stream);
+  (void)hipFree(t->d_sess);
+  (void)hipFree(t->d_gcm);
   delete t;
 }
 
@@ -171,7 +171,7 @@ extern "C" int tlsgpu_sessions_install(tlsgpu_sessions* t, uint32_t first, uint3
                ? launch_session_install(t->d_sess, t->d_gcm, d_params, first, n, t->eng->stream)
                : -1;
   hipError_t serr = hipStreamSynchronize(t->eng->stream);
-  hipFree(d_params);
+  (void)hipFree(d_params);
   if (err != hipSuccess || rc != 0 || serr != hipSuccess)
     return fail(TLSGPU_EHIP, "session install failed: %s",
                 hipGetErrorString(err != hipSuccess ? err : serr));
@@ -565,8 +565,8 @@ struct Staging {
   uint8_t* d_buf = nullptr;
   size_t cap = 0;
   ~Staging() {
-    if (d_buf) hipFree(d_buf);
-    if (stream) hipStreamDestroy(stream);
+    if (d_buf) (void)hipFree(d_buf);
+    if (stream) (void)hipStreamDestroy(stream);
   }
   bool ensure(int dev, size_t bytes) {
     if (hipSetDevice(dev) != hipSuccess) return false;
@@ -574,7 +574,7 @@ struct Staging {
       return false;
     device = dev;
     if (cap >= bytes) return true;
-    if (d_buf) hipFree(d_buf);
+    if (d_buf) (void)hipFree(d_buf);
     d_buf = nullptr;
     cap = 0;
     size_t want = bytes < (1u << 20) ? (1u << 20) : bytes;
@@ -654,9 +654,9 @@ extern "C" void EVP_AEAD_CTX_cleanup(EVP_AEAD_CTX* ctx) {
     // scrub the device key material before freeing (explicit_bzero analogue)
     const bool pooled = (st->slot & 0x40000000) != 0;
     const uint32_t slot = (uint32_t)(st->slot & 0x3FFFFFFF);
-    hipSetDevice(st->sess->eng->device);
-    hipMemset(st->sess->d_sess + slot, 0, sizeof(DevSession));
-    hipMemset(st->sess->d_gcm + slot, 0, sizeof(DevGcmTables));
+    (void)hipSetDevice(st->sess->eng->device);
+    (void)hipMemset(st->sess->d_sess + slot, 0, sizeof(DevSession));
+    (void)hipMemset(st->sess->d_gcm + slot, 0, sizeof(DevGcmTables));
     if (pooled) {
       std::lock_guard<std::mutex> lk(g_batcher_mu);
       g_batcher->free_slots.push_back((int)slot);
