@@ -636,6 +636,38 @@ __device__ __forceinline__ void gcm_blocks(const RecCtx& rc, const DevSession* _
       for (int w = 0; w < 4; w++) { c0[w] = n0[w]; c1[w] = n1[w]; }
     }
   }
+  // Two remaining steps at a time when the first is full (short records have
+  // no full step pairs; this halves their serial AES latency), masked second.
+  if (FAST) {
+    for (; base + kWave < nb; base += 2 * kWave) {
+      const uint32_t i0 = base + lane, i1 = i0 + kWave;  // i0 < nb always
+      const bool a1 = i1 < nb;
+      const uint32_t nb0 = min(16u, n - 16u * i0), nb1 = a1 ? min(16u, n - 16u * i1) : 0u;
+      uint32_t in0[4], in1[4], k0[4], k1[4];
+      load_block(rc.src + 16u * i0, nb0, aligned, in0);
+      load_block(rc.src + 16u * i1, nb1, aligned, in1);
+      aes_ctr16x2<ROUNDS>(k0, k1, ctr0 + i0, ctr0 + i1, rcc, rk[3], rk, as_const(S->rk_rot), laneoff);
+#pragma unroll
+      for (int w = 0; w < 4; w++) {
+        const int32_t b0 = (int32_t)nb0 - 4 * w, b1 = (int32_t)nb1 - 4 * w;
+        k0[w] &= b0 >= 4 ? 0xFFFFFFFFu : (b0 <= 0 ? 0u : ((1u << (8 * b0)) - 1u));
+        k1[w] &= b1 >= 4 ? 0xFFFFFFFFu : (b1 <= 0 ? 0u : ((1u << (8 * b1)) - 1u));
+      }
+      uint32_t o0[4] = {in0[0] ^ k0[0], in0[1] ^ k0[1], in0[2] ^ k0[2], in0[3] ^ k0[3]};
+      uint32_t o1[4] = {in1[0] ^ k1[0], in1[1] ^ k1[1], in1[2] ^ k1[2], in1[3] ^ k1[3]};
+      store_block(rc.dst + 16u * i0, nb0, aligned, o0);
+      if (a1) store_block(rc.dst + 16u * i1, nb1, aligned, o1);
+      uint32_t xk[4];
+      mul_k(x, xk, gl);
+      const uint32_t* g0 = SEAL ? o0 : in0;
+      x[0] = xk[0] ^ g0[0]; x[1] = xk[1] ^ g0[1]; x[2] = xk[2] ^ g0[2]; x[3] = xk[3] ^ g0[3];
+      mul_k(x, xk, gl);
+      if (a1) {
+        const uint32_t* g1 = SEAL ? o1 : in1;
+        x[0] = xk[0] ^ g1[0]; x[1] = xk[1] ^ g1[1]; x[2] = xk[2] ^ g1[2]; x[3] = xk[3] ^ g1[3];
+      }
+    }
+  }
   // Remaining steps (odd full step, partial wave, partial last block).
   for (; base < nb; base += kWave) {
     const uint32_t i = base + lane;
