@@ -36,10 +36,12 @@ namespace tg {
 
 namespace tg {
 
-// 16 S-boxes in place.
-__device__ __forceinline__ void bs_subbytes(uint32_t (&st)[128]) {
+// N / 8 S-boxes in place (N = 128: 32 blocks per lane; N = 64: the packed
+// 16-block layout of gcm_bs16.h, two bytes per plane).
+template <int N>
+__device__ __forceinline__ void bs_subbytes(uint32_t (&st)[N]) {
 #pragma unroll
-  for (int b = 0; b < 16; b++) {
+  for (int b = 0; b < N / 8; b++) {
     uint32_t* p = st + 8 * b;
     uint32_t o7, o6, o5, o4, o3, o2, o1, o0;
     TG_BS_SBOX(p[7], p[6], p[5], p[4], p[3], p[2], p[1], p[0], o7, o6, o5, o4, o3, o2, o1, o0);
@@ -90,8 +92,8 @@ __device__ __forceinline__ uint32_t bs_mc_bit(const uint32_t (&t)[4][8], uint32_
 // MixColumns on column C (bytes a_i = st[32C + 8i + k]) + AddRoundKey of
 // round r.  Outputs are produced in the order 3, 0, 1, 2 so that each input
 // byte dies as soon as its last reader (out_{i-1} reads a_i) is done.
-template <int C, class KM>
-__device__ __forceinline__ void bs_mixcolumn(uint32_t (&st)[128], const KM& km, int r) {
+template <int C, class KM, int N>
+__device__ __forceinline__ void bs_mixcolumn(uint32_t (&st)[N], const KM& km, int r) {
   uint32_t t[4][8];
 #pragma unroll
   for (int i = 0; i < 4; i++)
@@ -110,6 +112,42 @@ __device__ __forceinline__ void bs_mixcolumn(uint32_t (&st)[128], const KM& km, 
   }
 #pragma unroll
   for (int k = 0; k < 8; k++) st[32 * C + 24 + k] = o3[k];
+}
+
+// Same result, bit-serial from bit 7 down: only the column's t planes of
+// bits k and k - 1 (plus bit 7) are live, 16 temporaries instead of 40 — the
+// register peak of the packed 64-plane path (gcm_bs16.h).
+template <int C, class KM, int N>
+__device__ __forceinline__ void bs_mixcolumn_lean(uint32_t (&st)[N], const KM& km, int r) {
+  uint32_t t7[4], tk[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    t7[i] = st[32 * C + 8 * i + 7] ^ st[32 * C + 8 * ((i + 1) & 3) + 7];
+    tk[i] = t7[i];
+  }
+#pragma unroll
+  for (int k = 7; k >= 0; k--) {
+    uint32_t tm[4] = {0, 0, 0, 0}, o[4];
+    if (k >= 1) {
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        tm[i] = st[32 * C + 8 * i + k - 1] ^ st[32 * C + 8 * ((i + 1) & 3) + k - 1];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint32_t n = st[32 * C + 8 * ((i + 1) & 3) + k], t2 = tk[(i + 2) & 3];
+      const uint32_t m = km.mask(r, 32 * C + 8 * i + k);
+      if (k == 1 || k == 3 || k == 4)
+        o[i] = bop3s(bop3(tm[i], t7[i], n, 0x96), t2, m, 0x96);
+      else
+        o[i] = bop3(k == 0 ? t7[i] : tm[i], n, t2, 0x96) ^ m;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      st[32 * C + 8 * i + k] = o[i];
+      tk[i] = tm[i];
+    }
+  }
 }
 
 template <class KM>
@@ -145,8 +183,8 @@ __device__ __forceinline__ void bs_encrypt(uint32_t (&st)[128], const KM& km) {
 
 // 32x32 bit transpose of st[O..O+31] in place (x[i] bit j <-> x[j] bit i).
 // Stages 16 and 8 are byte moves (v_perm_b32), stages 4/2/1 swap-moves.
-template <int S, int O>
-__device__ __forceinline__ void transpose_stage(uint32_t (&x)[128]) {
+template <int S, int O, int N>
+__device__ __forceinline__ void transpose_stage(uint32_t (&x)[N]) {
 #pragma unroll
   for (int g = 0; g < 32; g += 2 * S)
 #pragma unroll
@@ -167,8 +205,8 @@ __device__ __forceinline__ void transpose_stage(uint32_t (&x)[128]) {
     }
 }
 
-template <int O>
-__device__ __forceinline__ void transpose32(uint32_t (&x)[128]) {
+template <int O, int N>
+__device__ __forceinline__ void transpose32(uint32_t (&x)[N]) {
   transpose_stage<16, O>(x);
   transpose_stage<8, O>(x);
   transpose_stage<4, O>(x);

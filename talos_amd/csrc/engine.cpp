@@ -52,11 +52,49 @@ extern "C" const char* tlsgpu_last_error(void) { return g_err; }
 
 // ---------------------------------------------------------------------------
 // engine / sessions
+// Per-stream scratch for the per-record constants (RecPre) of the queue
+// kernels: grow-only hipMalloc buffers, reused in stream order.  (The stream-
+// ordered pool — hipMallocAsync — was measured to hand the queue kernel stale
+// bytes on MI355X: ~20 % of seal batches in a loop of fresh batches read
+// constants the prep kernel had not made visible; plain hipMalloc memory: 0 of
+// 240.  See DESIGN.md §4.1.)
+struct PreScratch {
+  void* ptr = nullptr;
+  size_t cap = 0;
+};
+
 struct tlsgpu_engine {
   int device;
   hipStream_t stream;
   int num_cus;
+  std::mutex pre_mu;
+  std::vector<std::pair<hipStream_t, PreScratch>> pre;  // few streams per engine
 };
+
+// Scratch of at least `bytes` for stream s (enlarging waits for the stream's
+// earlier work, which may still read the old buffer).
+static void* pre_scratch(tlsgpu_engine* e, hipStream_t s, size_t bytes) {
+  std::lock_guard<std::mutex> g(e->pre_mu);
+  PreScratch* ps = nullptr;
+  for (auto& kv : e->pre)
+    if (kv.first == s) ps = &kv.second;
+  if (!ps) {
+    e->pre.emplace_back(s, PreScratch{});
+    ps = &e->pre.back().second;
+  }
+  if (ps->cap < bytes) {
+    if (ps->ptr) {
+      if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
+      (void)hipFree(ps->ptr);
+      ps->ptr = nullptr;
+      ps->cap = 0;
+    }
+    const size_t cap = std::max(bytes, (size_t)1 << 20);
+    if (hipMalloc(&ps->ptr, cap) != hipSuccess) return nullptr;
+    ps->cap = cap;
+  }
+  return ps->ptr;
+}
 
 struct tlsgpu_sessions {
   tlsgpu_engine* eng;
@@ -95,6 +133,8 @@ extern "C" void tlsgpu_engine_destroy(tlsgpu_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
   (void)hipStreamSynchronize(e->stream);
+  (void)hipDeviceSynchronize();  // batches on user streams may still use the scratch
+  for (auto& kv : e->pre) (void)hipFree(kv.second.ptr);
   (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -256,9 +296,16 @@ static uint32_t g_hy_flags = []() {
   return v ? (uint32_t)strtoul(v, nullptr, 0) & 7u : 0u;
 }();
 
+// Queue kernel: records with n >= this take the packed bitsliced path
+// (gcm_bs16.h); 0 = T-table only.  Env TLSGPU_BS16_MIN.
+static uint32_t g_bs16_min = []() {
+  const char* v = getenv("TLSGPU_BS16_MIN");
+  return v ? (uint32_t)strtoul(v, nullptr, 0) : 0u;
+}();
+
 static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const uint8_t* d_in,
                      uint8_t* d_out, int32_t* d_status, hipStream_t s, bool seal, bool raw) {
-  BatchArgs a;
+  BatchArgs a = {};
   a.sessions = t->d_sess;
   a.gcm_tables = t->d_gcm;
   a.descs = d_descs;
@@ -270,13 +317,16 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   a.bs_reserve = g_bs_reserve;
   a.hy_flags = g_hy_flags;
   a.dbg = g_phase_stats;
+  a.bs16_min = g_bs16_min;
   int groups = groups_for(t->eng, n, &a.records_per_group);
   // records whose session is empty/invalid keep this status
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)d_status, (int)TLSGPU_REC_PUBLIC_INVALID, n, s));
   const int impl = raw ? TLSGPU_GCM_TTABLE : g_gcm_impl.load();
-  RecPre* pre = nullptr;  // per-record constants of the queue kernels, stream-ordered
-  if (impl != TLSGPU_GCM_TTABLE && (t->have[TLSGPU_AES_128_GCM] || t->have[TLSGPU_AES_256_GCM]))
-    HIPCHK(hipMallocAsync((void**)&pre, sizeof(RecPre) * (size_t)n, s));
+  RecPre* pre = nullptr;  // per-record constants of the queue kernels (per-stream scratch)
+  if (impl != TLSGPU_GCM_TTABLE && (t->have[TLSGPU_AES_128_GCM] || t->have[TLSGPU_AES_256_GCM])) {
+    pre = (RecPre*)pre_scratch(t->eng, s, sizeof(RecPre) * (size_t)n);
+    if (!pre) return fail(TLSGPU_ENOMEM, "RecPre scratch (%u records)", n);
+  }
   for (int rounds : {10, 14}) {
     if (!t->have[rounds == 10 ? TLSGPU_AES_128_GCM : TLSGPU_AES_256_GCM]) continue;
     int rc;
@@ -295,12 +345,10 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
       }
     }
     if (rc) {
-      if (pre) (void)hipFreeAsync(pre, s);
       return fail(TLSGPU_EHIP, "gcm-%d launch: %s", rounds == 10 ? 128 : 256,
                   hipGetErrorString(hipGetLastError()));
     }
   }
-  if (pre) HIPCHK(hipFreeAsync(pre, s));
   if ((t->have[TLSGPU_CHACHA20_POLY1305] || t->have[TLSGPU_CHACHA20_POLY1305_OLD]) &&
       launch_chacha(a, seal, raw, groups, s))
     return fail(TLSGPU_EHIP, "chacha launch: %s", hipGetErrorString(hipGetLastError()));
@@ -718,7 +766,7 @@ static int gpu_call(const AeadState* st, bool seal, unsigned char* out, size_t* 
   if (nonce_len && hipMemcpyAsync(b + o_nonce, nonce, nonce_len, hipMemcpyHostToDevice, s)) return -1;
   if (ad_len && hipMemcpyAsync(b + o_ad, ad, ad_len, hipMemcpyHostToDevice, s)) return -1;
   if (in_len && hipMemcpyAsync(b + o_in, in, in_len, hipMemcpyHostToDevice, s)) return -1;
-  BatchArgs a;
+  BatchArgs a = {};
   a.sessions = st->sess->d_sess;
   a.gcm_tables = st->sess->d_gcm;
   a.descs = b + o_job;

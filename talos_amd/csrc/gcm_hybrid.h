@@ -131,15 +131,9 @@ __device__ __forceinline__ void bs_xtime(const uint32_t (&p)[8], uint32_t (&o)[8
   TG_BS_SBOX(in[7], in[6], in[5], in[4], in[3], in[2], in[1], in[0], out[7], out[6], out[5], \
              out[4], out[3], out[2], out[1], out[0])
 
-// Keystream planes of pass p (blocks 1024p .. 1024p + 1023 of records A and B,
-// u = 2 + lane + 1024p) without the final AddRoundKey.
-// Rounds 1 and 2 (through round 2's AddRoundKey).
-template <int ROUNDS>
-__device__ __forceinline__ void bs_encrypt_r2(uint32_t (&st)[128], const RecPre* pa,
-                                              const RecPre* pb, uint32_t u, cu32* rk) {
-  const SgprMasks km{rk};
-  // counter bytes 14 (c14) and 15 (c15) of slot j: u + 64 (j mod 16)
-  uint32_t c14[8], c15[8];
+// Planes of counter bytes 14 (c14) and 15 (c15) of slot j (bit j, both
+// half-words alike): the big-endian counter u + 64 (j mod 16) < 2^16.
+__device__ __forceinline__ void bs_ctr_c14c15(uint32_t u, uint32_t (&c14)[8], uint32_t (&c15)[8]) {
 #pragma unroll
   for (int k = 0; k < 6; k++) c15[k] = 0u - ((u >> k) & 1u);
   const uint32_t U = u >> 6, ulo = U & 15u, uhi = U >> 4;
@@ -152,6 +146,17 @@ __device__ __forceinline__ void bs_encrypt_r2(uint32_t (&st)[128], const RecPre*
 #pragma unroll
   for (int q = 0; q < 6; q++)
     c14[2 + q] = (cm & (0u - ((h1 >> q) & 1u))) | (~cm & (0u - ((uhi >> q) & 1u)));
+}
+
+// Keystream planes of pass p (blocks 1024p .. 1024p + 1023 of records A and B,
+// u = 2 + lane + 1024p) without the final AddRoundKey.
+// Rounds 1 and 2 (through round 2's AddRoundKey).
+template <int ROUNDS>
+__device__ __forceinline__ void bs_encrypt_r2(uint32_t (&st)[128], const RecPre* pa,
+                                              const RecPre* pb, uint32_t u, cu32* rk) {
+  const SgprMasks km{rk};
+  uint32_t c14[8], c15[8];
+  bs_ctr_c14c15(u, c14, c15);
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     c14[k] ^= km.mask(0, 8 * 14 + k);
@@ -288,6 +293,12 @@ __device__ void gcm_pair_hy(const RecCtx (&rc)[2], const RecPre* pa, const RecPr
   pc.lap(3, lane);
 }
 
+}  // namespace tg
+
+#include "gcm_bs16.h"
+
+namespace tg {
+
 template <bool SEAL, int ROUNDS, int NB = 4>
 __device__ __forceinline__ void hy_tt_record(const BatchArgs& a, const RecPre* __restrict__ pre,
                                              uint32_t r, const DevSession* __restrict__ S,
@@ -295,6 +306,13 @@ __device__ __forceinline__ void hy_tt_record(const BatchArgs& a, const RecPre* _
   const tlsgpu_record* D = reinterpret_cast<const tlsgpu_record*>(a.descs);
   RecCtx rc;
   if (!parse_tls<SEAL>(load_desc(D + r), S, a.in, a.out, a.status + r, lane, rc)) return;
+#ifdef TG_BS16  // packed bitsliced path (experimental build)
+  if (a.bs16_min != 0 && rc.n >= a.bs16_min && rc.n <= 16384u &&
+      ((((uintptr_t)rc.src) | ((uintptr_t)rc.dst)) & 15) == 0) {
+    gcm_record_bs16<SEAL, ROUNDS>(rc, pre + r, S, a.status + r, lane, gl, a.dbg);
+    return;
+  }
+#endif
   const RecConsts rcc = rec_consts_of(pre + r);
   gcm_record_x4<SEAL, ROUNDS, NB>(rc, S, rcc, a.status + r, lane, laneoff, gl, a.dbg);
 }

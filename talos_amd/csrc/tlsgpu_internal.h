@@ -77,6 +77,8 @@ struct BatchArgs {
                                     // 1 = no bitsliced pairs, 2 = T-table waves idle,
                                     // 4 = bitsliced waves idle
   unsigned long long* dbg;          // phase timing (PhaseClock), normally null
+  uint32_t bs16_min;                // queue kernel: records of n >= this (<= 16384, 16-B
+                                    // aligned) take the packed bitsliced path; 0 = never
 };
 
 // Per-record constants of the hybrid kernel (gcm_prep_kernel, one per record,

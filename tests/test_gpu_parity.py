@@ -275,3 +275,14 @@ def test_batch_publicly_invalid(ta, engine, oracle):
     ob.run(table)
     assert [s for s, _ in ob.results()] == [-2] * len(recs)
     table.close()
+
+
+def test_batch_repeated_fresh_batches(ta, engine, oracle, gcm_impl):
+    """Back-to-back fresh batches on one stream (new tables and buffers each
+    time): the queue kernels' per-record constants must never come from an
+    earlier batch.  A stream-ordered-pool scratch failed this on MI355X in about
+    one iteration of five; the per-stream scratch passes."""
+    gcm_impl("queue")
+    for it in range(24):
+        name = ["aes-128-gcm", "aes-256-gcm"][it % 2]
+        _run_seal_open(ta, engine, oracle, [KINDS[name]] * 2, LENGTHS[::3], seed=300 + it)
