@@ -67,7 +67,11 @@ def main_kernel(kind_name: str, op: str) -> str:
             "ttable": f"tg::gcm_batch_kernel<{seal}, false, {rounds}>"}[impl]
 
 
-def cpu_baseline(kind_name: str, rec_len: int, op: str) -> dict | None:
+def cpu_baseline(kind_name: str, rec_len: int, op: str, note: str = "") -> dict | None:
+    # the reference build links LibreSSL's x86-64 AES-NI and PCLMUL GHASH
+    # assembly (oracle/Makefile); its ChaCha20 and Poly1305 are the portable C
+    impl = ("AES-NI + PCLMUL GHASH asm" if "gcm" in kind_name
+            else "portable C chacha.c + poly1305-donna")
     try:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import pyoracle
@@ -80,8 +84,8 @@ def cpu_baseline(kind_name: str, rec_len: int, op: str) -> dict | None:
                                   threads, secs)
         return {"value": round(r["gib_per_s"], 3), "unit": "GiB/s", "cores": threads,
                 "kind": "reference",
-                "sample": f"LibreSSL 2.4.1 EVP_AEAD_CTX_{op} (AES-NI+PCLMUL) over {nrec} x "
-                          f"{rec_len}-B records, {threads} pthreads x {secs:.1f}s "
+                "sample": f"LibreSSL 2.4.1 EVP_AEAD_CTX_{op} ({impl}) over {nrec} x "
+                          f"{rec_len}-B records{note}, {threads} pthreads x {secs:.1f}s "
                           f"({r['records']} records timed), oracle/_ref/libref.so"}
     except Exception as exc:  # baseline is reported, never fatal
         return {"value": None, "error": str(exc)[:200]}
@@ -224,7 +228,12 @@ def main():
                                "(prep pass + status memset + main kernel)"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(kind_name, rec_len or 1400, op)
+        if rec_len:
+            line["cpu_baseline"] = cpu_baseline(kind_name, rec_len, op)
+        else:  # mixed lengths: the mix's mean record length
+            mean = max(1, int(round(total_len / per_gpu)))
+            line["cpu_baseline"] = cpu_baseline(kind_name, mean, op,
+                                                " (the Zipf mix's mean length)")
     if rank == 0:
         print(json.dumps(line), flush=True)
     ev0.close()

@@ -282,8 +282,12 @@ __device__ void cc_record(const CcRec& rc, uint32_t tag_len, int32_t* status_slo
 // covers 8 records x 128 contiguous bytes; each lane then en/decrypts and MACs
 // its own record's row.  Rows are padded to 144 B so the row-wise ds_read_b128
 // of the 64 lanes (same column, different rows) is bank-conflict-free.
+// 128 B per record per step (64-B steps fit 4 waves/SIMD at 124 VGPRs but
+// measured 535 vs 570 GiB/s on config C: twice the LDS syncs per byte)
 constexpr uint32_t kCcStep = 128;
 constexpr uint32_t kCcRow = kCcStep + 16;
+constexpr int kCcP = kCcStep / 16;           // 16-B pieces of a record per step = loads per lane
+constexpr int kCcR = kWave / kCcP;           // records covered by one load instruction
 constexpr int kCcThreads = 256;
 
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
@@ -317,7 +321,7 @@ __device__ void cc_record_staged(const CcRec& rc, bool active, uint32_t tag_len,
   // pieces this lane moves: records 8k + lane/8, bytes 16 (lane % 8) of each
   // step; the records' pointers and lengths are fetched with ds_bpermute per
   // step (keeping 8 x 5 of them in VGPRs would cost a wave per SIMD)
-  const uint32_t piece = 16u * (lane & 7);
+  const uint32_t piece = 16u * (lane % kCcP);
   uint32_t steps = (n + kCcStep - 1) / kCcStep;
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) steps = max(steps, (uint32_t)__shfl_xor((int)steps, m));
@@ -325,11 +329,11 @@ __device__ void cc_record_staged(const CcRec& rc, bool active, uint32_t tag_len,
   uint64_t ctr = ((uint64_t)st[13] << 32) | st[12];
   // gather of step s: 8 records x 128 B per load instruction, into registers
   // (issued one step ahead, so the loads fly during the previous step's math)
-  auto gather = [&](uint32_t base, uint4 (&v)[8]) {
+  auto gather = [&](uint32_t base, uint4 (&v)[kCcP]) {
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
+    for (int k = 0; k < kCcP; k++) {
       const uint32_t off = base + piece;
-      const uint32_t rr = 8u * k + (lane >> 3);
+      const uint32_t rr = kCcR * k + lane / kCcP;
       const uint32_t snk = __shfl(n, (int)rr);
       // ds_bpermute outside the branch: an inactive source lane reads as 0
       const uint64_t srck = shfl64((uint64_t)(uintptr_t)rc.src, rr);
@@ -347,19 +351,19 @@ __device__ void cc_record_staged(const CcRec& rc, bool active, uint32_t tag_len,
       }
     }
   };
-  uint4 pf[8];
+  uint4 pf[kCcP];
   gather(0, pf);
   for (uint32_t s = 0; s < steps; s++) {
     const uint32_t base = s * kCcStep;
 #pragma unroll
-    for (int k = 0; k < 8; k++)
-      *reinterpret_cast<uint4*>(tile + (8u * k + (lane >> 3)) * kCcRow + piece) = pf[k];
+    for (int k = 0; k < kCcP; k++)
+      *reinterpret_cast<uint4*>(tile + (kCcR * k + lane / kCcP) * kCcRow + piece) = pf[k];
     if (s + 1 < steps) gather(base + kCcStep, pf);
     lds_wave_sync();
     // en/decrypt + MAC this lane's row: 2 ChaCha blocks
     if (base < n) {
 #pragma unroll
-      for (int h = 0; h < 2; h++) {
+      for (int h = 0; h < (int)(kCcStep / 64); h++) {
         const uint32_t o64 = base + 64u * h;
         if (o64 >= n) break;
         ctr += 1;
@@ -397,9 +401,9 @@ __device__ void cc_record_staged(const CcRec& rc, bool active, uint32_t tag_len,
     lds_wave_sync();
     // scatter
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
+    for (int k = 0; k < kCcP; k++) {
       const uint32_t off = base + piece;
-      const uint32_t rr = 8u * k + (lane >> 3);
+      const uint32_t rr = kCcR * k + lane / kCcP;
       const uint32_t snk = __shfl(n, (int)rr);
       const uint64_t dstk = shfl64((uint64_t)(uintptr_t)rc.dst, rr);
       if (off < snk) {
