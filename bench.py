@@ -113,8 +113,10 @@ def main():
     ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
     ap.add_argument("--records", type=int, default=0, help="override records per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", default="device", choices=["device", "host"],
-                    help="host: pinned host buffers + H2D/D2H overlap (PCIe-inclusive rate)")
+    ap.add_argument("--mode", default="device", choices=["device", "host", "wire"],
+                    help="host: pinned host buffers + H2D/D2H overlap (PCIe-inclusive rate); "
+                         "wire: raw TLS wire streams through tlsgpu_open_wire (framing + "
+                         "in-place open, SURVEY.md §8f-1)")
     args = ap.parse_args()
 
     import talos_amd as ta
@@ -139,10 +141,12 @@ def main():
     lengths = None if rec_len else glob[lo:hi]
     wl = Workload(eng, kind, hi - lo, max(1, sessions * (hi - lo) // per_gpu),
                   seed ^ (rank * 0x100000001), lengths=lengths, record_len=rec_len or 0,
-                  index0=lo, tamper_every=1024 if op == "open" else 0)
+                  index0=lo, tamper_every=1024 if op == "open" and args.mode != "wire" else 0)
     total_len = int(wl.lengths.sum())
     if args.mode == "host":
         return host_mode(args, eng, wl, kind_name, total_len)
+    if args.mode == "wire":
+        return wire_mode(args, eng, wl, kind_name, total_len)
 
     def step(stream=None):
         if op == "open":
@@ -265,6 +269,90 @@ def host_mode(args, eng, wl, kind_name, total_len):
                       "steps": args.steps, "records": wl.n,
                       "ms_per_step": round(dt * 1e3 / args.steps, 3)}), flush=True)
     pipe.close()
+    wl.free()
+    eng.close()
+
+
+def wire_mode(args, eng, wl, kind_name, total_len):
+    """Raw wire streams (one per session = connection direction, its records back
+    to back as 5-B header + fragment) through tlsgpu_open_wire: device framing
+    (ssl3_get_record's header walk) + in-place open + alert mapping.  Fragments
+    sit at wire offsets, i.e. mostly not 16-B aligned, as on a real socket
+    buffer.  The wire is restored from a pristine copy before every step (in-place
+    open overwrites it); only the open_wire calls are timed (HIP events)."""
+    import talos_amd as ta
+    eiv = ta.EXPLICIT_NONCE_LEN[wl.kind]
+    body = wl.d_body.download()
+    frag = (wl.lengths + eiv + ta.TAG_LEN).astype(np.int64)
+    parts, descs, frag_pos = [], [], np.zeros(wl.n, dtype=np.int64)
+    pos = 0
+    for s in range(wl.S):
+        idx = np.nonzero(wl.session == s)[0]
+        if len(idx) == 0:
+            continue
+        start = pos
+        for i in idx:
+            fl = int(frag[i])
+            parts.append(np.frombuffer(bytes([23, 3, 3, fl >> 8, fl & 0xFF]), dtype=np.uint8))
+            o = int(wl.body_off[i])
+            parts.append(body[o:o + fl])
+            frag_pos[i] = pos + 5
+            pos += 5 + fl
+        descs.append((start, pos - start, s, int(wl.seq[idx[0]]), 0x0303, 0, 0))
+    wire = np.concatenate(parts)
+    del parts, body
+    ns = len(descs)
+    d_streams = ta.DeviceBuffer(eng, ns * ta.WIRE_STREAM_DTYPE.itemsize)
+    d_streams.upload(np.array(descs, dtype=ta.WIRE_STREAM_DTYPE).view(np.uint8))
+    d_wire0 = ta.DeviceBuffer(eng, len(wire) + 64)
+    d_wire0.upload(np.concatenate([wire, np.zeros(64, np.uint8)]))
+    d_wire = ta.DeviceBuffer(eng, len(wire) + 64)
+    d_recs = ta.DeviceBuffer(eng, 32 * wl.n)
+    d_status = ta.DeviceBuffer(eng, 4 * wl.n)
+    d_results = ta.DeviceBuffer(eng, ta.WIRE_RESULT_DTYPE.itemsize * ns)
+    d_total = ta.DeviceBuffer(eng, 4)
+    evs = [ta.Event(eng) for _ in range(2)]
+
+    def step():
+        d_wire.copy_from(d_wire0)
+        evs[0].record()
+        ta.open_wire(wl.table, d_streams.ptr, ns, d_wire.ptr, wl.n, d_recs.ptr, d_status.ptr,
+                     d_results.ptr, d_total.ptr)
+        evs[1].record()
+        eng.sync()
+        return evs[0].elapsed_ms(evs[1])
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    ms = [step() for _ in range(args.steps)]
+    # verify: every stream fully framed and delivered, statuses exact, sampled plaintexts
+    res = d_results.download().view(ta.WIRE_RESULT_DTYPE)
+    assert int(d_total.download().view(np.uint32)[0]) == wl.n
+    assert (res["alert"] == 0).all() and int(res["delivered"].sum()) == wl.n
+    assert (res["consumed"].astype(np.int64) == np.array([d[1] for d in descs])).all()
+    recs = d_recs.download().view(ta.RECORD_DTYPE)
+    st = d_status.download().view(np.int32)
+    by_off = {int(r["in_off"]): k for k, r in enumerate(recs)}
+    rng = np.random.default_rng(wl.seed)
+    for i in rng.choice(wl.n, size=min(32, wl.n), replace=False):
+        k = by_off[int(frag_pos[i])]
+        assert st[k] == wl.lengths[i], (i, st[k])
+        ln, o = int(wl.lengths[i]), int(frag_pos[i]) + eiv
+        got = d_wire.download(ln, o)
+        assert np.array_equal(got, wl.d_pt.download(ln, int(wl.pt_off[i]))), i
+    avg = sum(ms) / len(ms)
+    mis = int(((frag_pos + eiv) % 16 != 0).sum())
+    print(json.dumps({
+        "metric": f"GiB/s device-resident {kind_name} TLS wire-stream open (tlsgpu_open_wire: "
+                  "framing + in-place open + alerts)",
+        "value": round(total_len / (avg / 1e3) / GIB, 3), "unit": "GiB/s", "steps": args.steps,
+        "ms_per_step": round(avg, 4), "records": wl.n, "streams": ns,
+        "payload_bytes": total_len, "wire_bytes": int(len(wire)),
+        "records_not_16B_aligned": mis, "gcm_impl": ta.get_gcm_impl(),
+        "timing": "HIP events around each tlsgpu_open_wire call; wire restored between steps"}),
+        flush=True)
+    for b in (d_streams, d_wire0, d_wire, d_recs, d_status, d_results, d_total):
+        b.free()
     wl.free()
     eng.close()
 

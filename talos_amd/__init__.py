@@ -248,6 +248,13 @@ class DeviceBuffer:
         self.engine.sync_stream(stream)
         return out
 
+    def copy_from(self, src: "DeviceBuffer", nbytes: int | None = None,
+                  stream: int | None = None) -> None:
+        """Device-to-device copy, stream-ordered (no host sync)."""
+        n = min(self.nbytes, src.nbytes) if nbytes is None else nbytes
+        _check(self.lib.tlsgpu_memcpy(self.engine.handle, self.ptr, src.ptr, n, stream),
+               "tlsgpu_memcpy")
+
     def fill(self, value: int, stream: int | None = None, sync: bool = True) -> None:
         _check(self.lib.tlsgpu_memset(self.engine.handle, self.ptr, value, self.nbytes, stream),
                "tlsgpu_memset")

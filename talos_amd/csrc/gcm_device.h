@@ -439,11 +439,57 @@ __device__ __forceinline__ uint32_t load_u32_bytes(const uint8_t* p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
+// A full 16-B block at any byte address with dword loads: the dwords that hold
+// its bytes (each contains at least one byte of the block, so none crosses the
+// buffer's last page) funnel-shifted into place.  TLS wire fragments sit 5 B
+// past their headers, so in-place opens of wire buffers take this path.
+__device__ __forceinline__ void load16_any(const uint8_t* p, uint32_t v[4]) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t sh = (uint32_t)a & 3u;
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+  const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
+  const uint32_t w4 = sh ? q[4] : 0u;
+  v[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+  v[1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+  v[2] = __builtin_amdgcn_alignbyte(w3, w2, sh);
+  v[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
+}
+
+// The matching store: whole dwords inside the block, 1-2 byte/short stores at
+// its two ends (never a read-modify-write of a neighbour's bytes).
+__device__ __forceinline__ void store16_any(uint8_t* p, const uint32_t o[4]) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t sh = (uint32_t)a & 3u;
+  if (sh == 0) {
+    uint32_t* q = reinterpret_cast<uint32_t*>(p);
+    q[0] = o[0]; q[1] = o[1]; q[2] = o[2]; q[3] = o[3];
+    return;
+  }
+  uint32_t* q = reinterpret_cast<uint32_t*>(a - sh);  // q[1..3] lie inside the block
+  q[1] = __builtin_amdgcn_alignbyte(o[1], o[0], 4 - sh);
+  q[2] = __builtin_amdgcn_alignbyte(o[2], o[1], 4 - sh);
+  q[3] = __builtin_amdgcn_alignbyte(o[3], o[2], 4 - sh);
+  if (sh == 1) {
+    p[0] = (uint8_t)o[0];
+    *reinterpret_cast<uint16_t*>(p + 1) = (uint16_t)(o[0] >> 8);
+    p[15] = (uint8_t)(o[3] >> 24);
+  } else if (sh == 2) {
+    *reinterpret_cast<uint16_t*>(p) = (uint16_t)o[0];
+    *reinterpret_cast<uint16_t*>(p + 14) = (uint16_t)(o[3] >> 16);
+  } else {
+    p[0] = (uint8_t)o[0];
+    *reinterpret_cast<uint16_t*>(p + 13) = (uint16_t)(o[3] >> 8);
+    p[15] = (uint8_t)(o[3] >> 24);
+  }
+}
+
 __device__ __forceinline__ void load_block(const uint8_t* p, uint32_t nbytes, bool aligned,
                                            uint32_t v[4]) {
   if (aligned && nbytes == 16) {
     uint4 t = *reinterpret_cast<const uint4*>(p);
     v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else if (nbytes == 16) {
+    load16_any(p, v);
   } else {
     v[0] = v[1] = v[2] = v[3] = 0;
 #pragma unroll
@@ -456,6 +502,8 @@ __device__ __forceinline__ void store_block(uint8_t* p, uint32_t nbytes, bool al
                                             const uint32_t v[4]) {
   if (nbytes == 16 && aligned) {
     *reinterpret_cast<uint4*>(p) = make_uint4(v[0], v[1], v[2], v[3]);
+  } else if (nbytes == 16) {
+    store16_any(p, v);
   } else {
 #pragma unroll
     for (uint32_t k = 0; k < 16; k++)
@@ -836,7 +884,7 @@ __device__ __forceinline__ void aes_ctr16xN(uint32_t (&ks)[NB][4], const uint32_
   aes_ctr16xN<NB, ROUNDS>(ks, ctr, c, rk03, rk, rkr, laneoff, [](int) {});
 }
 
-// Full NB-step groups of a 16-B-aligned record from block `start` on (FAST
+// Full NB-step groups of a record (any alignment) from block `start` on (FAST
 // constants only): NB keystream blocks per lane in flight, the next group's
 // input loads issued first, and the GHASH of each group's NB blocks folded
 // into the AES rounds of the following group (the chain's LDS round trips then
@@ -847,7 +895,10 @@ __device__ __forceinline__ void gcm_blocks_xN(const RecCtx& rc, const DevSession
                                               const RecConsts& rcc, uint32_t (&x)[4],
                                               uint32_t& start, uint32_t lane, uint32_t laneoff,
                                               const GhLane& gl) {
-  if (((((uintptr_t)rc.src) | ((uintptr_t)rc.dst)) & 15) != 0) return;
+  const bool aligned = ((((uintptr_t)rc.src) | ((uintptr_t)rc.dst)) & 15) == 0;
+#ifndef TG_XN_UNALIGNED
+  if (!aligned) return;
+#endif
   cu32* rk = as_const(S->rk);
   cu32* rkr = as_const(S->rk_rot);
   const uint32_t rk03 = rk[3];
@@ -857,10 +908,7 @@ __device__ __forceinline__ void gcm_blocks_xN(const RecCtx& rc, const DevSession
   if (t + NB > nfull_steps) return;
   uint32_t c[NB][4], gp[NB][4];
 #pragma unroll
-  for (int b = 0; b < NB; b++) {
-    const uint4 v = *reinterpret_cast<const uint4*>(rc.src + 16u * (start + kWave * b + lane));
-    c[b][0] = v.x; c[b][1] = v.y; c[b][2] = v.z; c[b][3] = v.w;
-  }
+  for (int b = 0; b < NB; b++) load_block(rc.src + 16u * (start + kWave * b + lane), 16, aligned, c[b]);
   auto ghash_step = [&](int b) {
     uint32_t xk[4];
     mul_k(x, xk, gl);
@@ -880,10 +928,7 @@ __device__ __forceinline__ void gcm_blocks_xN(const RecCtx& rc, const DevSession
     uint32_t nx[NB][4];
     if (t + 2 * NB <= nfull_steps) {
 #pragma unroll
-      for (int b = 0; b < NB; b++) {
-        const uint4 v = *reinterpret_cast<const uint4*>(rc.src + 16u * (i + kWave * (NB + b)));
-        nx[b][0] = v.x; nx[b][1] = v.y; nx[b][2] = v.z; nx[b][3] = v.w;
-      }
+      for (int b = 0; b < NB; b++) load_block(rc.src + 16u * (i + kWave * (NB + b)), 16, aligned, nx[b]);
     }
     uint32_t ctr[NB], k[NB][4];
 #pragma unroll
@@ -896,7 +941,7 @@ __device__ __forceinline__ void gcm_blocks_xN(const RecCtx& rc, const DevSession
 #pragma unroll
     for (int b = 0; b < NB; b++) {
       uint32_t o[4] = {c[b][0] ^ k[b][0], c[b][1] ^ k[b][1], c[b][2] ^ k[b][2], c[b][3] ^ k[b][3]};
-      *reinterpret_cast<uint4*>(rc.dst + 16u * (i + kWave * b)) = make_uint4(o[0], o[1], o[2], o[3]);
+      store_block(rc.dst + 16u * (i + kWave * b), 16, aligned, o);
 #pragma unroll
       for (int w = 0; w < 4; w++) gp[b][w] = SEAL ? o[w] : c[b][w];
     }

@@ -31,35 +31,85 @@ struct WireWalk {
   int32_t alert;      // header-level failure after them (0: none / incomplete)
 };
 
+struct Hdr {
+  uint32_t type, ver, len;
+};
+// The 5 header bytes from the two dwords that hold them (each holds a header
+// byte, so neither reaches past the buffer's last page): 2 loads, not 5.
+__device__ __forceinline__ Hdr read_hdr(const uint8_t* h) {
+  const uintptr_t a = (uintptr_t)h;
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)a & 3u;
+  const uint32_t q0 = q[0], q1 = q[1];
+  const uint32_t lo = __builtin_amdgcn_alignbyte(q1, q0, sh);  // header bytes 0..3
+  const uint32_t b4 = (q1 >> (8 * sh)) & 0xFFu;                // header byte 4
+  return {lo & 0xFFu, (((lo >> 8) & 0xFFu) << 8) | ((lo >> 16) & 0xFFu), ((lo >> 24) << 8) | b4};
+}
+
+// The header walk is a chain of dependent reads (each header gives the next
+// one's offset): one memory round trip per record.  It covers up to kSpec
+// headers per round trip by speculating that the next records have the last
+// record's length (a bulk sender's stream is runs of equal-size records): the
+// speculative headers are loaded together, and header k is used only if the
+// real walk lands exactly on it; a misprediction restarts from the real offset.
+constexpr int kSpec = 8;
+
+// Visits the complete records of stream `st` that pass the header checks, in
+// order, at most `limit`, calling visit(index, offset, header) for each.
+template <class Visit>
 __device__ __forceinline__ WireWalk wire_walk(const tlsgpu_wire_stream& st, const uint8_t* w,
-                                              uint32_t limit) {
+                                              uint32_t limit, Visit&& visit) {
   WireWalk r = {0, 0, 0};
   const uint32_t rbuf = st.rbuf_len ? st.rbuf_len : kDefaultRbuf;
-  uint32_t pos = 0;
-  while (r.records < limit && pos + kHdr <= st.wire_len) {
-    const uint8_t* h = w + pos;
-    const uint32_t ver = ((uint32_t)h[1] << 8) | h[2];
-    const uint32_t len = ((uint32_t)h[3] << 8) | h[4];
-    if (!(st.flags & TLSGPU_WIRE_FIRST_PACKET) && ver != st.version) {
-      r.alert = kAlertProtocolVersion;  // s3_pkt.c:319-329
-      break;
+  uint32_t pos = 0, stride = 0;
+  bool stop = false;
+  while (!stop && r.records < limit && pos + kHdr <= st.wire_len) {
+    const uint32_t base = pos, sb = stride;
+    Hdr hs[kSpec];
+#pragma unroll
+    for (int k = 0; k < kSpec; k++) {  // unconditional loads (clamped into the stream):
+      // a header past the stream end is never used (the walk stops first)
+      const uint32_t p = min(base + (uint32_t)k * sb, st.wire_len - kHdr);
+      hs[k] = read_hdr(w + p);
     }
-    if ((ver >> 8) != 3) {  // SSL3_VERSION_MAJOR, :331-335 (goto err: no alert)
-      r.alert = -1;
-      break;
+#pragma unroll
+    for (int k = 0; k < kSpec; k++) {
+      if (k > 0 && (sb == 0 || pos != base + (uint32_t)k * sb)) break;  // mispredicted
+      if (r.records >= limit || pos + kHdr > st.wire_len) {
+        stop = true;
+        break;
+      }
+      const Hdr h = hs[k];
+      if (!(st.flags & TLSGPU_WIRE_FIRST_PACKET) && h.ver != st.version) {
+        r.alert = kAlertProtocolVersion;  // s3_pkt.c:319-329
+        stop = true;
+        break;
+      }
+      if ((h.ver >> 8) != 3) {  // SSL3_VERSION_MAJOR, :331-335 (goto err: no alert)
+        r.alert = -1;
+        stop = true;
+        break;
+      }
+      if (h.len > rbuf - kHdr) {  // :337-341
+        r.alert = kAlertRecordOverflow;
+        stop = true;
+        break;
+      }
+      if (pos + kHdr + h.len > st.wire_len) {  // fragment not complete yet
+        stop = true;
+        break;
+      }
+      if (h.len > kMaxEncrypted) {  // :376-380
+        r.alert = kAlertRecordOverflow;
+        stop = true;
+        break;
+      }
+      visit(r.records, pos, h);
+      r.records++;
+      pos += kHdr + h.len;
+      r.consumed = pos;
+      stride = kHdr + h.len;
     }
-    if (len > rbuf - kHdr) {  // :337-341
-      r.alert = kAlertRecordOverflow;
-      break;
-    }
-    if (pos + kHdr + len > st.wire_len) break;  // fragment not complete yet
-    if (len > kMaxEncrypted) {  // :376-380
-      r.alert = kAlertRecordOverflow;
-      break;
-    }
-    r.records++;
-    pos += kHdr + len;
-    r.consumed = pos;
   }
   return r;
 }
@@ -75,17 +125,13 @@ __global__ __launch_bounds__(256) void wire_frame_kernel(const tlsgpu_wire_strea
   if (s >= n_streams) return;
   const tlsgpu_wire_stream st = streams[s];
   const uint8_t* w = wire + st.wire_off;
-  WireWalk walk = wire_walk(st, w, 0xFFFFFFFFu);
+  WireWalk walk = wire_walk(st, w, 0xFFFFFFFFu, [](uint32_t, uint32_t, const Hdr&) {});
   uint32_t first = walk.records ? atomicAdd(total, walk.records) : 0u;
   uint32_t n = walk.records;
   if (first >= max_records) {
     n = 0;
   } else if (first + n > max_records) {
     n = max_records - first;
-  }
-  if (n != walk.records) {  // truncated at a record boundary: no alert reached
-    walk = wire_walk(st, w, n);
-    walk.alert = 0;
   }
   // explicit nonce length of the session's AEAD (GCM 8, ChaCha 0); an unknown
   // session still gets descriptors, which the open kernels leave PUBLIC_INVALID
@@ -94,18 +140,19 @@ __global__ __launch_bounds__(256) void wire_frame_kernel(const tlsgpu_wire_strea
     const uint32_t kind = sessions[st.session].kind;
     eiv = (kind == TLSGPU_AES_128_GCM || kind == TLSGPU_AES_256_GCM) ? 8u : 0u;
   }
-  uint32_t pos = 0;
-  for (uint32_t i = 0; i < n; i++) {
-    const uint8_t* h = w + pos;
-    const uint32_t len = ((uint32_t)h[3] << 8) | h[4];
+  // second walk (headers now cache-resident) writes the in-place descriptors
+  const WireWalk w2 = wire_walk(st, w, n, [&](uint32_t i, uint32_t pos, const Hdr& h) {
     tlsgpu_record d;
     d.in_off = st.wire_off + pos + kHdr;
     d.out_off = d.in_off + eiv;
     d.seq = st.seq + i;
     d.session = st.session;
-    d.len_type = ((uint32_t)h[0] << 24) | len;
+    d.len_type = (h.type << 24) | h.len;
     recs[first + i] = d;
-    pos += kHdr + len;
+  });
+  if (n != walk.records) {  // truncated at a record boundary: no alert reached
+    walk = w2;
+    walk.alert = 0;
   }
   tlsgpu_wire_result r;
   r.first = n ? first : 0u;
@@ -125,27 +172,36 @@ __global__ __launch_bounds__(256) void wire_finish_kernel(uint32_t n_streams,
   if (s >= n_streams) return;
   tlsgpu_wire_result r = results[s];
   bool dead = false;
-  for (uint32_t i = 0; i < r.records; i++) {
-    int32_t* sp = status + r.first + i;
-    if (dead) {
-      *sp = TLSGPU_REC_SKIPPED;
-      continue;
-    }
-    const int32_t st = *sp;
-    int32_t alert = 0;
-    if (st == TLSGPU_REC_BAD_MAC) {
-      alert = kAlertBadRecordMac;
-    } else if (st == TLSGPU_REC_PUBLIC_INVALID) {
-      alert = kAlertDecryptionFailed;
-    } else if (st > (int32_t)kMaxPlain) {
-      alert = kAlertRecordOverflow;
-      *sp = TLSGPU_REC_OVERFLOW;
-    }
-    if (alert) {
-      dead = true;
-      r.alert = alert;
-      r.alert_record = i;
-      r.delivered = i;
+  // statuses in groups of 8 loaded together (independent loads, one round trip)
+  for (uint32_t i0 = 0; i0 < r.records; i0 += 8) {
+    int32_t sv[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) sv[k] = i0 + k < r.records ? status[r.first + i0 + k] : 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t i = i0 + k;
+      if (i >= r.records) break;
+      int32_t* sp = status + r.first + i;
+      if (dead) {
+        *sp = TLSGPU_REC_SKIPPED;
+        continue;
+      }
+      const int32_t st = sv[k];
+      int32_t alert = 0;
+      if (st == TLSGPU_REC_BAD_MAC) {
+        alert = kAlertBadRecordMac;
+      } else if (st == TLSGPU_REC_PUBLIC_INVALID) {
+        alert = kAlertDecryptionFailed;
+      } else if (st > (int32_t)kMaxPlain) {
+        alert = kAlertRecordOverflow;
+        *sp = TLSGPU_REC_OVERFLOW;
+      }
+      if (alert) {
+        dead = true;
+        r.alert = alert;
+        r.alert_record = i;
+        r.delivered = i;
+      }
     }
   }
   results[s] = r;
@@ -156,7 +212,8 @@ int launch_wire_frame(const tlsgpu_wire_stream* streams, uint32_t n_streams, con
                       tlsgpu_record* recs, tlsgpu_wire_result* results, uint32_t* total,
                       hipStream_t s) {
   if (n_streams == 0) return 0;
-  hipLaunchKernelGGL(wire_frame_kernel, dim3((n_streams + 255) / 256), dim3(256), 0, s, streams,
+  // 64-lane groups: the scattered header loads of one wave per CU, not four
+  hipLaunchKernelGGL(wire_frame_kernel, dim3((n_streams + 63) / 64), dim3(64), 0, s, streams,
                      n_streams, wire, sessions, n_sessions, max_records, recs, results, total);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -164,7 +221,7 @@ int launch_wire_frame(const tlsgpu_wire_stream* streams, uint32_t n_streams, con
 int launch_wire_finish(uint32_t n_streams, tlsgpu_wire_result* results, int32_t* status,
                        hipStream_t s) {
   if (n_streams == 0) return 0;
-  hipLaunchKernelGGL(wire_finish_kernel, dim3((n_streams + 255) / 256), dim3(256), 0, s, n_streams,
+  hipLaunchKernelGGL(wire_finish_kernel, dim3((n_streams + 63) / 64), dim3(64), 0, s, n_streams,
                      results, status);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
