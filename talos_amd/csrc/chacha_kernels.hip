@@ -342,6 +342,10 @@ __device__ void cc_record_staged(const CcRec& rc, bool active, uint32_t tag_len,
         const uint8_t* src = (const uint8_t*)(uintptr_t)srck + off;
         if (off + 16 <= snk && ((uintptr_t)src & 15) == 0) {
           v[k] = *reinterpret_cast<const uint4*>(src);
+        } else if (off + 16 <= snk) {  // wire fragments: misaligned full piece
+          uint32_t w[4];
+          load16_any(src, w);
+          v[k] = make_uint4(w[0], w[1], w[2], w[3]);
         } else {
           uint32_t w[4] = {0, 0, 0, 0};
           const uint32_t nb = min(16u, snk - off);
@@ -411,6 +415,9 @@ __device__ void cc_record_staged(const CcRec& rc, bool active, uint32_t tag_len,
         const uint4 v = *reinterpret_cast<const uint4*>(tile + rr * kCcRow + piece);
         if (off + 16 <= snk && ((uintptr_t)dst & 15) == 0) {
           *reinterpret_cast<uint4*>(dst) = v;
+        } else if (off + 16 <= snk) {
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+          store16_any(dst, w);
         } else {
           const uint32_t w[4] = {v.x, v.y, v.z, v.w};
           const uint32_t nb = min(16u, snk - off);

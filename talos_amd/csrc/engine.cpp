@@ -775,6 +775,10 @@ static int gpu_call(const AeadState* st, bool seal, unsigned char* out, size_t* 
   a.in = nullptr;
   a.out = nullptr;
   a.status = (int32_t*)(b + o_status);
+  a.n_sessions = st->sess->capacity;
+  // a job the kernel rejects keeps this status (never a stale one)
+  if (hipMemsetD32Async((hipDeviceptr_t)a.status, (int)TLSGPU_REC_PUBLIC_INVALID, 1, s) != hipSuccess)
+    return -1;
   bool gcm = st->kind == TLSGPU_AES_128_GCM || st->kind == TLSGPU_AES_256_GCM;
   int rc = gcm ? launch_gcm(a, seal, true, st->kind == TLSGPU_AES_128_GCM ? 10 : 14, 1, s)
                : launch_chacha(a, seal, true, 1, s);

@@ -439,50 +439,7 @@ __device__ __forceinline__ uint32_t load_u32_bytes(const uint8_t* p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
-// A full 16-B block at any byte address with dword loads: the dwords that hold
-// its bytes (each contains at least one byte of the block, so none crosses the
-// buffer's last page) funnel-shifted into place.  TLS wire fragments sit 5 B
-// past their headers, so in-place opens of wire buffers take this path.
-__device__ __forceinline__ void load16_any(const uint8_t* p, uint32_t v[4]) {
-  const uintptr_t a = (uintptr_t)p;
-  const uint32_t sh = (uint32_t)a & 3u;
-  const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
-  const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
-  const uint32_t w4 = sh ? q[4] : 0u;
-  v[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
-  v[1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
-  v[2] = __builtin_amdgcn_alignbyte(w3, w2, sh);
-  v[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
-}
-
-// The matching store: whole dwords inside the block, 1-2 byte/short stores at
-// its two ends (never a read-modify-write of a neighbour's bytes).
-__device__ __forceinline__ void store16_any(uint8_t* p, const uint32_t o[4]) {
-  const uintptr_t a = (uintptr_t)p;
-  const uint32_t sh = (uint32_t)a & 3u;
-  if (sh == 0) {
-    uint32_t* q = reinterpret_cast<uint32_t*>(p);
-    q[0] = o[0]; q[1] = o[1]; q[2] = o[2]; q[3] = o[3];
-    return;
-  }
-  uint32_t* q = reinterpret_cast<uint32_t*>(a - sh);  // q[1..3] lie inside the block
-  q[1] = __builtin_amdgcn_alignbyte(o[1], o[0], 4 - sh);
-  q[2] = __builtin_amdgcn_alignbyte(o[2], o[1], 4 - sh);
-  q[3] = __builtin_amdgcn_alignbyte(o[3], o[2], 4 - sh);
-  if (sh == 1) {
-    p[0] = (uint8_t)o[0];
-    *reinterpret_cast<uint16_t*>(p + 1) = (uint16_t)(o[0] >> 8);
-    p[15] = (uint8_t)(o[3] >> 24);
-  } else if (sh == 2) {
-    *reinterpret_cast<uint16_t*>(p) = (uint16_t)o[0];
-    *reinterpret_cast<uint16_t*>(p + 14) = (uint16_t)(o[3] >> 16);
-  } else {
-    p[0] = (uint8_t)o[0];
-    *reinterpret_cast<uint16_t*>(p + 13) = (uint16_t)(o[3] >> 8);
-    p[15] = (uint8_t)(o[3] >> 24);
-  }
-}
-
+// (load16_any / store16_any: tlsgpu_internal.h)
 __device__ __forceinline__ void load_block(const uint8_t* p, uint32_t nbytes, bool aligned,
                                            uint32_t v[4]) {
   if (aligned && nbytes == 16) {

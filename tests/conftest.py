@@ -18,6 +18,13 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: test needs an MI355X GPU")
 
 
+def pytest_collection_modifyitems(session, config, items):
+    """The EVP coalescing-queue test turns batching on for the rest of the
+    process (EVP contexts then live in the shared pool); run it last so every
+    other EVP test exercises the per-call path."""
+    items.sort(key=lambda it: "test_evp_queue" in it.nodeid)
+
+
 @pytest.fixture(scope="session")
 def oracle():
     import pyoracle
