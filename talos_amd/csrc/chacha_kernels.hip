@@ -341,7 +341,7 @@ __device__ void cc_record_staged(const CcRec& rc, bool active, uint32_t tag_len,
       if (off < snk) {
         const uint8_t* src = (const uint8_t*)(uintptr_t)srck + off;
         if (off + 16 <= snk && ((uintptr_t)src & 15) == 0) {
-          v[k] = *reinterpret_cast<const uint4*>(src);
+          v[k] = gload16(src);
         } else if (off + 16 <= snk) {  // wire fragments: misaligned full piece
           uint32_t w[4];
           load16_any(src, w);
@@ -349,7 +349,7 @@ __device__ void cc_record_staged(const CcRec& rc, bool active, uint32_t tag_len,
         } else {
           uint32_t w[4] = {0, 0, 0, 0};
           const uint32_t nb = min(16u, snk - off);
-          for (uint32_t b = 0; b < nb; b++) w[b >> 2] |= (uint32_t)src[b] << (8 * (b & 3));
+          for (uint32_t b = 0; b < nb; b++) w[b >> 2] |= (uint32_t)gld<uint8_t>(src)[b] << (8 * (b & 3));
           v[k] = make_uint4(w[0], w[1], w[2], w[3]);
         }
       }
@@ -414,14 +414,14 @@ __device__ void cc_record_staged(const CcRec& rc, bool active, uint32_t tag_len,
         uint8_t* dst = (uint8_t*)(uintptr_t)dstk + off;
         const uint4 v = *reinterpret_cast<const uint4*>(tile + rr * kCcRow + piece);
         if (off + 16 <= snk && ((uintptr_t)dst & 15) == 0) {
-          *reinterpret_cast<uint4*>(dst) = v;
+          gstore16(dst, v);
         } else if (off + 16 <= snk) {
           const uint32_t w[4] = {v.x, v.y, v.z, v.w};
           store16_any(dst, w);
         } else {
           const uint32_t w[4] = {v.x, v.y, v.z, v.w};
           const uint32_t nb = min(16u, snk - off);
-          for (uint32_t b = 0; b < nb; b++) dst[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+          for (uint32_t b = 0; b < nb; b++) gst<uint8_t>(dst)[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
         }
       }
     }

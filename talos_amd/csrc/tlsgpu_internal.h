@@ -61,6 +61,33 @@ struct RawJob {
 };
 
 // Kernel launch parameters for the GCM / ChaCha batch kernels.
+// Global-address-space views of generic pointers.  Record pointers reach the
+// kernels through descriptors, structs and lane shuffles, where the compiler
+// loses their address space and emits FLAT loads/stores; a FLAT op counts in
+// lgkmcnt as well as vmcnt, so every LDS wait (s_waitcnt lgkmcnt) would also
+// wait for the in-flight prefetch loads.  Going through an integer keeps them
+// global_load / global_store.
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* gld(const void* p) {
+  return (const __attribute__((address_space(1))) T*)(uintptr_t)p;
+}
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gst(void* p) {
+  return (__attribute__((address_space(1))) T*)(uintptr_t)p;
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// 16 B through a global-address-space pointer (p 16-B aligned)
+__device__ __forceinline__ uint4 gload16(const void* p) {
+  const u32x4 v = *gld<u32x4>(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void gstore16(void* p, uint4 v) {
+  u32x4 w;
+  w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
+  *gst<u32x4>(p) = w;
+}
+
 // A full 16-B block at any byte address with dword loads: the dwords that hold
 // its bytes (each contains at least one byte of the block, so none crosses the
 // buffer's last page) funnel-shifted into place.  TLS wire fragments sit 5 B
@@ -68,7 +95,7 @@ struct RawJob {
 __device__ __forceinline__ void load16_any(const uint8_t* p, uint32_t v[4]) {
   const uintptr_t a = (uintptr_t)p;
   const uint32_t sh = (uint32_t)a & 3u;
-  const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+  const auto q = gld<uint32_t>((const void*)(a & ~(uintptr_t)3));
   const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
   const uint32_t w4 = sh ? q[4] : 0u;
   v[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
@@ -83,25 +110,27 @@ __device__ __forceinline__ void store16_any(uint8_t* p, const uint32_t o[4]) {
   const uintptr_t a = (uintptr_t)p;
   const uint32_t sh = (uint32_t)a & 3u;
   if (sh == 0) {
-    uint32_t* q = reinterpret_cast<uint32_t*>(p);
+    const auto q = gst<uint32_t>(p);
     q[0] = o[0]; q[1] = o[1]; q[2] = o[2]; q[3] = o[3];
     return;
   }
-  uint32_t* q = reinterpret_cast<uint32_t*>(a - sh);  // q[1..3] lie inside the block
+  const auto q = gst<uint32_t>((void*)(a - sh));  // q[1..3] lie inside the block
+  const auto b = gst<uint8_t>(p);
+  const auto h = gst<uint16_t>(p);  // used at even byte offsets only
   q[1] = __builtin_amdgcn_alignbyte(o[1], o[0], 4 - sh);
   q[2] = __builtin_amdgcn_alignbyte(o[2], o[1], 4 - sh);
   q[3] = __builtin_amdgcn_alignbyte(o[3], o[2], 4 - sh);
   if (sh == 1) {
-    p[0] = (uint8_t)o[0];
-    *reinterpret_cast<uint16_t*>(p + 1) = (uint16_t)(o[0] >> 8);
-    p[15] = (uint8_t)(o[3] >> 24);
+    b[0] = (uint8_t)o[0];
+    gst<uint16_t>(p + 1)[0] = (uint16_t)(o[0] >> 8);
+    b[15] = (uint8_t)(o[3] >> 24);
   } else if (sh == 2) {
-    *reinterpret_cast<uint16_t*>(p) = (uint16_t)o[0];
-    *reinterpret_cast<uint16_t*>(p + 14) = (uint16_t)(o[3] >> 16);
+    h[0] = (uint16_t)o[0];
+    h[7] = (uint16_t)(o[3] >> 16);
   } else {
-    p[0] = (uint8_t)o[0];
-    *reinterpret_cast<uint16_t*>(p + 13) = (uint16_t)(o[3] >> 8);
-    p[15] = (uint8_t)(o[3] >> 24);
+    b[0] = (uint8_t)o[0];
+    gst<uint16_t>(p + 13)[0] = (uint16_t)(o[3] >> 8);
+    b[15] = (uint8_t)(o[3] >> 24);
   }
 }
 
