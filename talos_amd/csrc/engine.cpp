@@ -303,6 +303,12 @@ static uint32_t g_bs16_min = []() {
   return v ? (uint32_t)strtoul(v, nullptr, 0) : 0u;
 }();
 
+// Queue kernel: short-record packs (gcm_pack).  Env TLSGPU_PACK=0 turns them off.
+static uint32_t g_pack = []() {
+  const char* v = getenv("TLSGPU_PACK");
+  return v ? (uint32_t)strtoul(v, nullptr, 0) : 1u;
+}();
+
 static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const uint8_t* d_in,
                      uint8_t* d_out, int32_t* d_status, hipStream_t s, bool seal, bool raw) {
   BatchArgs a = {};
@@ -318,6 +324,7 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   a.hy_flags = g_hy_flags;
   a.dbg = g_phase_stats;
   a.bs16_min = g_bs16_min;
+  a.pack = g_pack;
   int groups = groups_for(t->eng, n, &a.records_per_group);
   // records whose session is empty/invalid keep this status
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)d_status, (int)TLSGPU_REC_PUBLIC_INVALID, n, s));

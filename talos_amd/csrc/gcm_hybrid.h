@@ -317,6 +317,167 @@ __device__ __forceinline__ void hy_tt_record(const BatchArgs& a, const RecPre* _
   gcm_record_x4<SEAL, ROUNDS, NB>(rc, S, rcc, a.status + r, lane, laneoff, gl, a.dbg);
 }
 
+// ---------------------------------------------------------------------------
+// Short-record packs.  A record's GHASH sequence is
+// [AAD, C_0..C_{nb-1}, lengths] (gcm128.c:826-881,1356-1500): nb + 2 elements.
+// When that fits in the wave, consecutive records of one session are laid side
+// by side across the lanes, record i at lanes [base_i, base_i + nb_i + 2).  Each
+// lane then holds ONE element E_j and GHASH = XOR_j E_j * H^(nb + 1 - j)
+// (j = -1 for the AAD, nb for the lengths block): one Shoup multiply per lane
+// and a segmented XOR scan, so the per-record finish (the dominant cost of a
+// record of a few blocks) is paid once per pack instead of once per record.
+constexpr uint32_t kPackMaxNeed = 64;  // lanes; nb + 2 <= 64 keeps H^e within H^1..H^65
+constexpr uint32_t kPackNone = 0xFFu;
+
+// Lanes record descriptor word len_type needs in a pack, or kPackNone when it
+// takes the single-record path (too long, or publicly invalid: parse_tls).
+template <bool SEAL>
+__device__ __forceinline__ uint32_t pack_need(uint32_t len_type, uint32_t tag_len) {
+  const uint32_t len = len_type & 0xFFFFFFu;
+  if (!SEAL && len < 8 + tag_len) return kPackNone;
+  const uint32_t n = SEAL ? len : len - 8 - tag_len;
+  const uint32_t nb = (n + 15) >> 4;
+  return nb + 2 <= kPackMaxNeed ? nb + 2 : kPackNone;
+}
+
+// Records r0..r0+k-1 (one session S, each pack_need() <= 64, sum <= 64 lanes);
+// `need` = pack_need of record r0 + lane for lane < k.  Same outputs, status and
+// zero-fill as parse_tls + gcm_record_x4 record by record (t1_enc.c:832-975).
+template <bool SEAL, int ROUNDS>
+__device__ void gcm_pack(const BatchArgs& a, const RecPre* __restrict__ pre, uint32_t r0, uint32_t k,
+                         const DevSession* __restrict__ S, uint32_t lane, uint32_t laneoff,
+                         uint32_t need) {
+  const tlsgpu_record* D = reinterpret_cast<const tlsgpu_record*>(a.descs);
+  cu32* rk = as_const(S->rk);
+  cu32* rkr = as_const(S->rk_rot);
+  const uint32_t tag_len = as_const(&S->tag_len)[0];
+  const uint32_t version = as_const(&S->version)[0];
+  // lane layout: exclusive prefix sum of the needs
+  const uint32_t own = lane < k ? need : 0u;
+  uint32_t incl = own;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint32_t t = __shfl_up(incl, d);
+    if (lane >= (uint32_t)d) incl += t;
+  }
+  const uint32_t base_of = incl - own;  // lane i < k: first lane of record r0 + i
+  uint32_t ri = 0;
+  for (uint32_t i = 1; i < k; i++) ri += __builtin_amdgcn_readlane(base_of, i) <= lane ? 1u : 0u;
+  const uint32_t total = __builtin_amdgcn_readlane(incl, k - 1);
+  const bool used = lane < total;
+  const uint32_t base = __shfl(base_of, (int)ri);
+  const uint32_t rneed = __shfl(need, (int)ri);
+  const uint32_t nb = rneed - 2;
+  const int32_t j = (int32_t)lane - (int32_t)base - 1;  // -1: AAD, nb: lengths block
+  const uint32_t r = r0 + ri;
+
+  const tlsgpu_record d = D[used ? r : r0];
+  const uint32_t len = d.len_type & 0xFFFFFFu;
+  const uint8_t* ip = a.in + d.in_off;
+  uint8_t* op = a.out + d.out_off;
+  const uint32_t n = SEAL ? len : len - 8 - tag_len;
+  const uint8_t* src = SEAL ? ip : ip + 8;
+  uint8_t* dst = SEAL ? op + 8 : op;
+  const uint4* P = reinterpret_cast<const uint4*>(pre + (used ? r : r0));
+  const uint4 p0 = P[0], p1 = P[1], p2 = P[2];
+  RecConsts rcc;
+  rcc.ek0[0] = p0.x; rcc.ek0[1] = p0.y; rcc.ek0[2] = p0.z; rcc.ek0[3] = p0.w;
+  rcc.k1a = p1.x; rcc.k1b = p1.y;
+  rcc.k2[0] = p1.z; rcc.k2[1] = p1.w; rcc.k2[2] = p2.x; rcc.k2[3] = p2.y;
+
+  // this lane's element (BE words) and, for a data block, its output block
+  const bool blk = used && j >= 0 && (uint32_t)j < nb;
+  const uint32_t jb = blk ? (uint32_t)j : 0u;
+  const uint32_t nbytes = blk ? min(16u, n - 16u * jb) : 0u;
+  const bool aligned = ((((uintptr_t)(src + 16u * jb)) | ((uintptr_t)(dst + 16u * jb))) & 15) == 0;
+  uint32_t in[4] = {0, 0, 0, 0}, ks[4];
+  if (blk) load_block(src + 16u * jb, nbytes, aligned, in);
+  uint32_t tagw[4] = {0, 0, 0, 0};  // open: received tag (lengths lane)
+  const bool last = used && j == (int32_t)nb;
+  if (!SEAL && last) {
+    const uint8_t* t = src + n;
+    if (tag_len == 16) {
+      load16_any(t, tagw);
+    } else {
+      for (uint32_t b = 0; b < tag_len; b++) tagw[b >> 2] |= (uint32_t)t[b] << (8 * (b & 3));
+    }
+  }
+  aes_ctr16<ROUNDS>(ks, 2u + jb, rcc, rk[3], rk, rkr, laneoff);  // inc32(J0) = 2 (TLS J0)
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    const int32_t b = (int32_t)nbytes - 4 * w;
+    ks[w] &= b >= 4 ? 0xFFFFFFFFu : (b <= 0 ? 0u : ((1u << (8 * b)) - 1u));
+  }
+  const uint32_t ob[4] = {in[0] ^ ks[0], in[1] ^ ks[1], in[2] ^ ks[2], in[3] ^ ks[3]};
+  uint32_t e[4];
+  if (blk) {
+    const uint32_t* c = SEAL ? ob : in;
+    e[0] = bswap32(c[0]); e[1] = bswap32(c[1]); e[2] = bswap32(c[2]); e[3] = bswap32(c[3]);
+  } else if (j == -1) {  // AAD = seq || type || version || length (t1_enc.c:841-847,961-962)
+    e[0] = (uint32_t)(d.seq >> 32);
+    e[1] = (uint32_t)d.seq;
+    e[2] = ((d.len_type >> 24) << 24) | ((version & 0xFFFF) << 8) | ((n >> 8) & 0xFF);
+    e[3] = (n & 0xFF) << 24;
+  } else {  // lengths block: BE64(13 * 8) || BE64(n * 8)
+    e[0] = 0; e[1] = 13u * 8u;
+    e[2] = (uint32_t)(((uint64_t)n * 8) >> 32); e[3] = (uint32_t)((uint64_t)n * 8);
+  }
+  if (SEAL && blk) store_block(dst + 16u * jb, nbytes, aligned, ob);
+  if (SEAL && used && j == -1) {
+    for (int b = 0; b < 8; b++) op[b] = (uint8_t)(d.seq >> (56 - 8 * b));  // explicit nonce
+  }
+  // y = E_j * H^(nb + 1 - j), then the per-record XOR: inclusive scan, minus
+  // the scan value just before the record's first lane
+  uint32_t y[4];
+  mul_shoup(e, used ? (uint32_t)((int32_t)nb + 1 - j) : 1u, y);
+#pragma unroll
+  for (int w = 0; w < 4; w++) y[w] = used ? y[w] : 0u;
+#pragma unroll
+  for (int dd = 1; dd < kWave; dd <<= 1) {
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      const uint32_t t = __shfl_up(y[w], dd);
+      if (lane >= (uint32_t)dd) y[w] ^= t;
+    }
+  }
+  uint32_t tag[4];
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    const uint32_t before = __shfl(y[w], (int)(base == 0 ? 0 : base - 1));
+    tag[w] = bswap32(y[w] ^ (base == 0 ? 0u : before)) ^ rcc.ek0[w];
+  }
+  uint32_t bad = 0;
+  if (last) {
+    int32_t* slot = a.status + r;
+    if (SEAL) {
+      uint8_t* to = dst + n;
+      if (tag_len == 16) {
+        store16_any(to, tag);
+      } else {
+        for (uint32_t b = 0; b < tag_len; b++) to[b] = (uint8_t)(tag[b >> 2] >> (8 * (b & 3)));
+      }
+      *slot = (int32_t)(len + 8 + tag_len);
+    } else {
+      uint32_t diff = 0;
+#pragma unroll
+      for (int w = 0; w < 4; w++) {
+        const int32_t b = (int32_t)tag_len - 4 * w;
+        const uint32_t keep = b >= 4 ? 0xFFFFFFFFu : (b <= 0 ? 0u : ((1u << (8 * b)) - 1u));
+        diff |= (tag[w] ^ tagw[w]) & keep;  // every byte compared (timingsafe_memcmp)
+      }
+      bad = diff != 0 ? 1u : 0u;
+      *slot = bad ? TLSGPU_REC_BAD_MAC : (int32_t)n;
+    }
+  }
+  if (!SEAL) {  // plaintext, or zeros when the record's tag failed (evp_aead.c:137-143)
+    const uint32_t rbad = __shfl(bad, (int)(base + rneed - 1));
+    if (blk) {
+      const uint32_t z[4] = {0, 0, 0, 0};
+      store_block(dst + 16u * jb, nbytes, aligned, rbad ? z : ob);
+    }
+  }
+}
+
 __device__ __forceinline__ uint32_t queue_take(uint32_t* q, uint32_t k, uint32_t lane) {
   uint32_t r = 0;
   if (lane == 0) r = atomicAdd(q, k);
@@ -399,6 +560,30 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
         } else {
           const uint32_t r = queue_take(q, 1, lane);
           if (r >= run_end) break;
+          if (a.pack) {  // short records: take the consecutive short ones too, as a pack
+            const uint32_t tag_len = as_const(&S->tag_len)[0];
+            const uint32_t need0 = pack_need<SEAL>(as_const(&D[r].len_type)[0], tag_len);
+            if (need0 <= kPackMaxNeed) {
+              const uint32_t p = r + lane;
+              uint32_t need = lane == 0 ? need0
+                            : (lane < 32 && p < run_end) ? pack_need<SEAL>(D[p].len_type, tag_len)
+                                                         : kPackNone;
+              uint32_t incl = need;
+#pragma unroll
+              for (int dd = 1; dd < kWave; dd <<= 1) {
+                const uint32_t t = __shfl_up(incl, dd);
+                if (lane >= (uint32_t)dd) incl += t;
+              }
+              uint32_t k = (uint32_t)__builtin_popcountll(__ballot(incl <= kPackMaxNeed));
+              if (k > 1) {  // claim r+1..r+k-1 unless another wave took r+1 meanwhile
+                uint32_t got = 0;
+                if (lane == 0) got = atomicCAS(q, r + 1, r + k);
+                if (__builtin_amdgcn_readfirstlane(got) != r + 1) k = 1;
+              }
+              gcm_pack<SEAL, ROUNDS>(a, pre, r, k, S, lane, laneoff, need);
+              continue;
+            }
+          }
           hy_tt_record<SEAL, ROUNDS, NB>(a, pre, r, S, lane, laneoff, gl);
         }
       }

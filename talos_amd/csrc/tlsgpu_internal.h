@@ -152,6 +152,8 @@ struct BatchArgs {
   unsigned long long* dbg;          // phase timing (PhaseClock), normally null
   uint32_t bs16_min;                // queue kernel: records of n >= this (<= 16384, 16-B
                                     // aligned) take the packed bitsliced path; 0 = never
+  uint32_t pack;                    // queue kernel: short records of one session share a
+                                    // wave (gcm_pack); 0 = off
 };
 
 // Per-record constants of the hybrid kernel (gcm_prep_kernel, one per record,

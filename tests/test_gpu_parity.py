@@ -286,3 +286,28 @@ def test_batch_repeated_fresh_batches(ta, engine, oracle, gcm_impl):
     for it in range(24):
         name = ["aes-128-gcm", "aes-256-gcm"][it % 2]
         _run_seal_open(ta, engine, oracle, [KINDS[name]] * 2, LENGTHS[::3], seed=300 + it)
+
+
+# Short-record packs (gcm_pack): runs of records with
+# nb + 2 <= 64 GHASH elements share one wave.  Lengths cross the pack limit
+# (992 B = 62 blocks is the longest packed plaintext), packs of up to 32 empty
+# records, odd tails; every 5th record tampered (zero-fill inside a pack).
+PACK_LENGTHS = [0, 0, 1, 15, 16, 17, 31, 100, 255, 991, 992, 993, 1008, 0, 3, 47, 500, 64,
+                0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                0, 0, 0, 0, 2000, 12, 13, 14, 700, 800, 900, 15, 16, 16, 16, 16]
+
+
+@pytest.mark.parametrize("shift,in_place", [(0, False), (3, False), (0, True)])
+@pytest.mark.parametrize("name", ["aes-128-gcm", "aes-256-gcm"])
+def test_batch_short_record_packs(ta, engine, oracle, gcm_impl, name, shift, in_place):
+    gcm_impl("queue")
+    _run_seal_open(ta, engine, oracle, [KINDS[name]] * 3, PACK_LENGTHS, seed=41,
+                   in_shift=shift, out_shift=shift, in_place=in_place)
+
+
+def test_batch_short_record_packs_zipf(ta, engine, oracle, gcm_impl):
+    """The config-D length mix (Zipf 64 B - 16 KiB) on a few sessions."""
+    from talos_amd.workload import zipf_lengths
+    gcm_impl("queue")
+    lengths = [int(x) for x in zipf_lengths(400, 0x5EED0003)]
+    _run_seal_open(ta, engine, oracle, [KINDS["aes-256-gcm"]] * 2, lengths, seed=42)
