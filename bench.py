@@ -52,15 +52,17 @@ def algo_bytes_per_record(kind_name: str, length: int, op: str) -> int:
     return rd + wr
 
 
-def main_kernel(kind_name: str, op: str) -> str:
-    """Name of the step's dominant kernel as rocprofv3 lists it."""
+def main_kernel(kind_name: str, op: str, short_records: bool = False) -> str:
+    """Name of the step's dominant kernel as rocprofv3 lists it (the queue kernel's
+    pack variant runs when the batch has records of <= 62 blocks)."""
     import talos_amd as ta
     if "gcm" not in kind_name:
         return f"tg::chacha_batch_kernel<{'true' if op != 'open' else 'false'}, false>"
     rounds = 10 if "128" in kind_name else 14
     seal = "true" if op != "open" else "false"
     impl = ta.get_gcm_impl()
-    return {"queue": f"tg::gcm_hy_kernel<{seal}, {rounds}, 1024, 0, 2>",
+    pack = ", true" if short_records and os.environ.get("TLSGPU_PACK", "1") != "0" else ""
+    return {"queue": f"tg::gcm_hy_kernel<{seal}, {rounds}, 1024, 0, 2{pack}>",
             "hybrid": f"tg::gcm_hy_kernel<{seal}, {rounds}, 512, 4, 4>",
             "bitslice": f"tg::gcm_hy_kernel<{seal}, {rounds}, 512, 8, 4>",
             "fused": f"tg::gcm_fused_kernel<{seal}, {rounds}>",
@@ -182,7 +184,8 @@ def main():
         st = ta.debug_phase_stats(eng, reset=True)
         names = {1: "bs-aes", 2: "bs-consume", 3: "bs-finish", 4: "bs-barrier", 5: "tables",
                  6: "tt-switch",
-                 9: "tt-x4", 10: "tt-rest", 11: "tt-finish", 12: "tt-barrier"}
+                 9: "tt-x4", 10: "tt-rest", 11: "tt-finish", 12: "tt-barrier",
+                 13: "pack", 14: "recs/pack", 15: "plan"}
         for i, nm in names.items():
             if st[2 * i + 1]:
                 print(f"phase {nm:11s} cycles/step {st[2*i]/args.steps:14.0f} events/step "
@@ -200,7 +203,7 @@ def main():
     algo = sum(algo_bytes_per_record(kind_name, int(l), op) for l in
                ([rec_len] * wl.n if lengths is None else lengths.tolist()))
     achieved = algo / per_launch_s / 1e9
-    traffic, traffic_src = load_traffic(args.config, main_kernel(kind_name, op))
+    traffic, traffic_src = load_traffic(args.config, main_kernel(kind_name, op, CONFIGS[args.config][3] is None))
 
     line = {
         "metric": METRIC if args.config == "B" else
@@ -227,7 +230,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "algorithmic_bytes_per_launch": algo,
-                     "kernel": main_kernel(kind_name, op), "traffic_source": traffic_src,
+                     "kernel": main_kernel(kind_name, op, CONFIGS[args.config][3] is None), "traffic_source": traffic_src,
                      "timing": "HIP events around each whole step on the engine stream "
                                "(prep pass + status memset + main kernel)"},
     }

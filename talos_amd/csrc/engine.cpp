@@ -331,8 +331,12 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   const int impl = raw ? TLSGPU_GCM_TTABLE : g_gcm_impl.load();
   RecPre* pre = nullptr;  // per-record constants of the queue kernels (per-stream scratch)
   if (impl != TLSGPU_GCM_TTABLE && (t->have[TLSGPU_AES_128_GCM] || t->have[TLSGPU_AES_256_GCM])) {
-    pre = (RecPre*)pre_scratch(t->eng, s, sizeof(RecPre) * (size_t)n);
+    pre = (RecPre*)pre_scratch(t->eng, s, sizeof(RecPre) * (size_t)n + 256);
     if (!pre) return fail(TLSGPU_ENOMEM, "RecPre scratch (%u records)", n);
+    if (impl == TLSGPU_GCM_QUEUE && a.pack) {  // the prep pass's "packable record" flag
+      a.short_flag = reinterpret_cast<uint32_t*>(pre + n);
+      HIPCHK(hipMemsetD32Async((hipDeviceptr_t)a.short_flag, 0, 1, s));
+    }
   }
   for (int rounds : {10, 14}) {
     if (!t->have[rounds == 10 ? TLSGPU_AES_128_GCM : TLSGPU_AES_256_GCM]) continue;

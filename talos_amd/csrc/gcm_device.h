@@ -21,7 +21,9 @@ constexpr uint32_t SH_OFF = 131072;
 constexpr uint32_t R4_OFF = SH_OFF + kPowMax * 256;
 constexpr uint32_t Q_OFF = R4_OFF + 64;      // hybrid kernel: per-run record queue
 constexpr uint32_t DBG_OFF = Q_OFF + 16;     // hybrid kernel: phase counters (diagnostic)
-constexpr uint32_t LDS_BYTES = DBG_OFF + 32 * 8;
+constexpr uint32_t PLAN_OFF = DBG_OFF + 32 * 8;  // queue kernel: per-run pack plan
+constexpr uint32_t kPlanCap = 2048;                // records planned per run (runs split)
+constexpr uint32_t LDS_BYTES = PLAN_OFF + 4 * kPlanCap;
 
 __shared__ __attribute__((aligned(16))) uint8_t s_lds[LDS_BYTES];
 

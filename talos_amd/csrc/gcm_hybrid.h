@@ -340,11 +340,11 @@ __device__ __forceinline__ uint32_t pack_need(uint32_t len_type, uint32_t tag_le
   return nb + 2 <= kPackMaxNeed ? nb + 2 : kPackNone;
 }
 
-// Records r0..r0+k-1 (one session S, each pack_need() <= 64, sum <= 64 lanes);
-// `need` = pack_need of record r0 + lane for lane < k.  Same outputs, status and
+// k records of one session S (each pack_need() <= 64, sum <= 64 lanes): lane
+// i < k holds record index `rec` and its pack_need `need`.  Same outputs, status and
 // zero-fill as parse_tls + gcm_record_x4 record by record (t1_enc.c:832-975).
 template <bool SEAL, int ROUNDS>
-__device__ void gcm_pack(const BatchArgs& a, const RecPre* __restrict__ pre, uint32_t r0, uint32_t k,
+__device__ void gcm_pack(const BatchArgs& a, const RecPre* __restrict__ pre, uint32_t rec, uint32_t k,
                          const DevSession* __restrict__ S, uint32_t lane, uint32_t laneoff,
                          uint32_t need) {
   const tlsgpu_record* D = reinterpret_cast<const tlsgpu_record*>(a.descs);
@@ -369,16 +369,16 @@ __device__ void gcm_pack(const BatchArgs& a, const RecPre* __restrict__ pre, uin
   const uint32_t rneed = __shfl(need, (int)ri);
   const uint32_t nb = rneed - 2;
   const int32_t j = (int32_t)lane - (int32_t)base - 1;  // -1: AAD, nb: lengths block
-  const uint32_t r = r0 + ri;
+  const uint32_t r = __shfl(rec, (int)ri);  // ri < k: always a record of the pack
 
-  const tlsgpu_record d = D[used ? r : r0];
+  const tlsgpu_record d = D[r];
   const uint32_t len = d.len_type & 0xFFFFFFu;
   const uint8_t* ip = a.in + d.in_off;
   uint8_t* op = a.out + d.out_off;
   const uint32_t n = SEAL ? len : len - 8 - tag_len;
   const uint8_t* src = SEAL ? ip : ip + 8;
   uint8_t* dst = SEAL ? op + 8 : op;
-  const uint4* P = reinterpret_cast<const uint4*>(pre + (used ? r : r0));
+  const uint4* P = reinterpret_cast<const uint4*>(pre + r);
   const uint4 p0 = P[0], p1 = P[1], p2 = P[2];
   RecConsts rcc;
   rcc.ek0[0] = p0.x; rcc.ek0[1] = p0.y; rcc.ek0[2] = p0.z; rcc.ek0[3] = p0.w;
@@ -486,9 +486,12 @@ __device__ __forceinline__ uint32_t queue_take(uint32_t* q, uint32_t k, uint32_t
 
 // NT threads, the first BSW waves bitsliced (0: a pure T-table queue kernel,
 // 16 waves of <= 128 VGPRs), T-table waves NB blocks wide.
-template <bool SEAL, int ROUNDS, int NT, int BSW, int NB>
+template <bool SEAL, int ROUNDS, int NT, int BSW, int NB, bool PACK = false>
 __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
                                                        const RecPre* __restrict__ pre) {
+  // pack and no-pack variants are separate kernels (the pack code costs the
+  // long-record loop SGPR spills); the prep pass's flag picks the one that runs
+  if (a.short_flag && (as_const(a.short_flag)[0] != 0) != PACK) return;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t laneoff = (lane & 31) * 4;
@@ -505,27 +508,78 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
   const uint32_t rhi = min(a.n, rlo + a.records_per_group);
   uint32_t cur = 0xFFFFFFFFu;
   uint32_t pos = rlo;
+  // short-record packs (gcm_pack): T-table waves only, planned per run in LDS
+  const bool packing = PACK && BSW == 0 && a.pack != 0;
+  // the run in claim order: long records first (run-relative index order[t]),
+  // then the short ones, packed greedily (plan_k[t] records from position t)
+  uint16_t* order = reinterpret_cast<uint16_t*>(s_lds + PLAN_OFF);
+  uint8_t* plan_need = s_lds + PLAN_OFF + 2 * kPlanCap;  // pack_need of order[t]
+  uint8_t* plan_k = plan_need + kPlanCap;
+  uint32_t* ends = q + 1;  // [0]: next long slot (from the front), [1]: short slots (from the back)
   while (pos < rhi) {
     const uint32_t sid = __builtin_amdgcn_readfirstlane(D[pos].session);
-    uint32_t run_end = pos + 1;
-    while (run_end < rhi) {
-      uint32_t p = run_end + lane;
-      uint32_t s = p < rhi ? D[p].session : sid;
-      uint64_t diff = __ballot(p < rhi && s != sid);
-      if (diff) { run_end += __builtin_amdgcn_readfirstlane((uint32_t)__builtin_ctzll(diff)); break; }
-      run_end = min(rhi, run_end + 64);
-    }
     const bool in_range = sid < a.n_sessions;
     const DevSession* __restrict__ S = a.sessions + (in_range ? sid : 0);
+    const uint32_t tag_len = as_const(&S->tag_len)[0];
+    const uint32_t run_cap = packing ? min(rhi, pos + kPlanCap) : rhi;
+    bool has_short = packing && pack_need<SEAL>(as_const(&D[pos].len_type)[0], tag_len) <= kPackMaxNeed;
+    uint32_t run_end = pos + 1;
+    while (run_end < run_cap) {
+      uint32_t p = run_end + lane;
+      uint32_t s = p < run_cap ? D[p].session : sid;
+      if (packing)  // a hint only: records past the run's end may count
+        has_short |= __ballot(p < run_cap && s == sid &&
+                              pack_need<SEAL>(D[p].len_type, tag_len) <= kPackMaxNeed) != 0;
+      uint64_t diff = __ballot(p < run_cap && s != sid);
+      if (diff) { run_end += __builtin_amdgcn_readfirstlane((uint32_t)__builtin_ctzll(diff)); break; }
+      run_end = min(run_cap, run_end + 64);
+    }
     const uint32_t kind = as_const(&S->kind)[0];
     const bool usable = in_range && is_gcm(kind) && (int)as_const(&S->rounds)[0] == ROUNDS;
     if (usable) {
       PhaseClock pc(a.dbg);
-      __syncthreads();  // every wave is done with the previous run (queue, tables)
+      __syncthreads();  // every wave is done with the previous run (queue, tables, plan)
       pc.lap(bs_role ? 4 : 12, lane);
       if (threadIdx.x == 0) *q = pos;
       if (sid != cur) load_session_tables<NT>(a.gcm_tables + sid);
       cur = sid;
+      const uint32_t run_len = run_end - pos;
+      if (has_short) {  // the plan: greedy pack from every start, <= 64 lanes, <= 32 records
+        if (threadIdx.x == 0) { ends[0] = 0; ends[1] = run_len; }
+        __syncthreads();
+        for (uint32_t c = wave * kWave; c < run_len; c += NT) {  // ballot compaction per wave
+          const uint32_t t = c + lane;
+          const uint32_t nd = t < run_len ? pack_need<SEAL>(D[pos + t].len_type, tag_len) : 0u;
+          const bool sh = t < run_len && nd <= kPackMaxNeed;
+          const uint64_t lm = __ballot(t < run_len && !sh), sm = __ballot(sh);
+          uint32_t fb = 0, bb = 0;
+          if (lane == 0) {
+            fb = atomicAdd(ends, (uint32_t)__builtin_popcountll(lm));
+            bb = atomicSub(ends + 1, (uint32_t)__builtin_popcountll(sm)) -
+                 (uint32_t)__builtin_popcountll(sm);
+          }
+          fb = __builtin_amdgcn_readfirstlane(fb);
+          bb = __builtin_amdgcn_readfirstlane(bb);
+          const uint64_t below = (1ull << lane) - 1ull;
+          if (t < run_len) {
+            const uint32_t at = sh ? bb + (uint32_t)__builtin_popcountll(sm & below)
+                                   : fb + (uint32_t)__builtin_popcountll(lm & below);
+            order[at] = (uint16_t)t;
+            plan_need[at] = (uint8_t)nd;
+          }
+        }
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < run_len; t += NT) {
+          uint32_t k = 0, sum = 0;
+          for (; k < 32 && t + k < run_len; k++) {
+            const uint32_t nd = plan_need[t + k];
+            if (sum + nd > kPackMaxNeed) break;
+            sum += nd;
+          }
+          plan_k[t] = (uint8_t)k;
+        }
+        pc.lap(15, lane);
+      }
       __syncthreads();
       pc.lap(5, lane);
       const bool idle = (a.hy_flags & (bs_role ? 4u : 2u)) != 0;
@@ -558,31 +612,37 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
             if (rb < run_end) hy_tt_record<SEAL, ROUNDS, NB>(a, pre, rb, S, lane, laneoff, gl);
           }
         } else {
-          const uint32_t r = queue_take(q, 1, lane);
-          if (r >= run_end) break;
-          if (a.pack) {  // short records: take the consecutive short ones too, as a pack
-            const uint32_t tag_len = as_const(&S->tag_len)[0];
-            const uint32_t need0 = pack_need<SEAL>(as_const(&D[r].len_type)[0], tag_len);
-            if (need0 <= kPackMaxNeed) {
-              const uint32_t p = r + lane;
-              uint32_t need = lane == 0 ? need0
-                            : (lane < 32 && p < run_end) ? pack_need<SEAL>(D[p].len_type, tag_len)
-                                                         : kPackNone;
-              uint32_t incl = need;
-#pragma unroll
-              for (int dd = 1; dd < kWave; dd <<= 1) {
-                const uint32_t t = __shfl_up(incl, dd);
-                if (lane >= (uint32_t)dd) incl += t;
+          uint32_t r;
+          if (has_short) {
+            // claim the pack the plan starts at the queue head (k = 0: a long
+            // record alone); the CAS window is two LDS operations
+            uint32_t k = 0;
+            for (;;) {
+              r = __builtin_amdgcn_readfirstlane(__atomic_load_n(q, __ATOMIC_RELAXED));
+              if (r >= run_end) break;
+              k = plan_k[r - pos];
+              uint32_t got = 0;
+              if (lane == 0) got = atomicCAS(q, r, r + (k ? k : 1u));
+              if (__builtin_amdgcn_readfirstlane(got) == r) break;
+            }
+            if (r >= run_end) break;
+            if (k != 0) {
+              PhaseClock pp(a.dbg);
+              const uint32_t li = r - pos + min(lane, k - 1);
+              const uint32_t need = lane < k ? (uint32_t)plan_need[li] : kPackNone;
+              gcm_pack<SEAL, ROUNDS>(a, pre, pos + order[li], k, S, lane, laneoff, need);
+              pp.lap(13, lane);
+              if (a.dbg && lane == 0) {  // phase slot 14: records per pack (diagnostic)
+                unsigned long long* c = reinterpret_cast<unsigned long long*>(s_lds + DBG_OFF);
+                atomicAdd(c + 28, (unsigned long long)k);
+                atomicAdd(c + 29, 1ull);
               }
-              uint32_t k = (uint32_t)__builtin_popcountll(__ballot(incl <= kPackMaxNeed));
-              if (k > 1) {  // claim r+1..r+k-1 unless another wave took r+1 meanwhile
-                uint32_t got = 0;
-                if (lane == 0) got = atomicCAS(q, r + 1, r + k);
-                if (__builtin_amdgcn_readfirstlane(got) != r + 1) k = 1;
-              }
-              gcm_pack<SEAL, ROUNDS>(a, pre, r, k, S, lane, laneoff, need);
               continue;
             }
+            r = pos + order[r - pos];
+          } else {
+            r = queue_take(q, 1, lane);
+            if (r >= run_end) break;
           }
           hy_tt_record<SEAL, ROUNDS, NB>(a, pre, r, S, lane, laneoff, gl);
         }
@@ -610,6 +670,7 @@ __global__ __launch_bounds__(256) void gcm_prep_kernel(BatchArgs a, RecPre* __re
   if (d.session >= a.n_sessions) return;
   const DevSession* S = a.sessions + d.session;
   if (!is_gcm(S->kind) || (int)S->rounds != ROUNDS) return;
+  if (a.short_flag && pack_need<SEAL>(d.len_type, S->tag_len) <= kPackMaxNeed) *a.short_flag = 1u;
   auto T0 = [&](uint32_t w, int b) { return te[(w >> (8 * b)) & 0xFF]; };
   auto T1 = [&](uint32_t w, int b) { return rotl32(te[(w >> (8 * b)) & 0xFF], 8); };
   auto SB = [&](uint32_t w, int b) { return (te[(w >> (8 * b)) & 0xFF] >> 8) & 0xFF; };

@@ -154,6 +154,9 @@ struct BatchArgs {
                                     // aligned) take the packed bitsliced path; 0 = never
   uint32_t pack;                    // queue kernel: short records of one session share a
                                     // wave (gcm_pack); 0 = off
+  uint32_t* short_flag;             // set by the prep pass when a record can be packed; the
+                                    // queue kernel's pack / no-pack variants both launch and
+                                    // the one that does not match returns (null: no flag)
 };
 
 // Per-record constants of the hybrid kernel (gcm_prep_kernel, one per record,
