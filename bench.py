@@ -61,10 +61,10 @@ def main_kernel(kind_name: str, op: str, short_records: bool = False) -> str:
     rounds = 10 if "128" in kind_name else 14
     seal = "true" if op != "open" else "false"
     impl = ta.get_gcm_impl()
-    pack = ", true" if short_records and os.environ.get("TLSGPU_PACK", "1") != "0" else ""
+    pack = ", true" if short_records and os.environ.get("TLSGPU_PACK", "1") != "0" else ", false"
     return {"queue": f"tg::gcm_hy_kernel<{seal}, {rounds}, 1024, 0, 2{pack}>",
-            "hybrid": f"tg::gcm_hy_kernel<{seal}, {rounds}, 512, 4, 4>",
-            "bitslice": f"tg::gcm_hy_kernel<{seal}, {rounds}, 512, 8, 4>",
+            "hybrid": f"tg::gcm_hy_kernel<{seal}, {rounds}, 512, 4, 4, false>",
+            "bitslice": f"tg::gcm_hy_kernel<{seal}, {rounds}, 512, 8, 4, false>",
             "fused": f"tg::gcm_fused_kernel<{seal}, {rounds}>",
             "ttable": f"tg::gcm_batch_kernel<{seal}, false, {rounds}>"}[impl]
 
