@@ -185,7 +185,8 @@ int tlsgpu_open_wire(tlsgpu_sessions *t, const tlsgpu_wire_stream *d_streams,
 /* GCM TLS batch kernel selection (process-wide; results are identical).
  * TLSGPU_GCM_QUEUE (default): a prep pass computes every record's E_K(J0) and
  * round-1/2 constants, then 16 T-table waves per CU (AES rounds as LDS
- * lookups) pull records from a per-session-run queue.
+ * lookups) pull records from a per-session-run queue.  Records of <= 62
+ * blocks share a wave in packs (environment TLSGPU_PACK=0 turns packs off).
  * TLSGPU_GCM_TTABLE: T-table waves with in-kernel constants, static split.
  * TLSGPU_GCM_HYBRID: 4 bitsliced waves (AES-CTR on the VALU, pairs of
  * 16-byte-aligned records of >= 16 KiB) beside 4 T-table waves per CU.
