@@ -311,3 +311,23 @@ def test_batch_short_record_packs_zipf(ta, engine, oracle, gcm_impl):
     gcm_impl("queue")
     lengths = [int(x) for x in zipf_lengths(400, 0x5EED0003)]
     _run_seal_open(ta, engine, oracle, [KINDS["aes-256-gcm"]] * 2, lengths, seed=42)
+
+
+def test_batch_packs_long_runs(ta, engine):
+    """One session over 600 K mostly-short records: every workgroup's range is
+    longer than the LDS pack plan (kPlanCap = 2,048 records), so runs are split.
+    Device seal -> tamper 1/97 -> device open; statuses exact, sampled
+    plaintexts equal, tampered records zero-filled (Workload.verify_open)."""
+    import numpy as np
+    from talos_amd.workload import Workload
+    n = 600_000
+    rng = np.random.default_rng(7)
+    lengths = rng.integers(0, 200, n)
+    lengths[rng.random(n) < 0.05] = 3000   # long records between the packs
+    for kind in (po.AES_128_GCM, po.AES_256_GCM):
+        wl = Workload(engine, kind, n, 1, 0x5EED0041, lengths=lengths, record_len=0,
+                      tamper_every=97)
+        wl.open()
+        engine.sync()
+        wl.verify_open(sample=512)
+        wl.free()
