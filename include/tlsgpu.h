@@ -214,6 +214,11 @@ int tlsgpu_get_gcm_impl(void);
  * tlsgpu_evp_batch_stats: batches run and jobs served so far. */
 int tlsgpu_evp_set_batching(unsigned window_us, unsigned max_jobs, unsigned pool_sessions);
 int tlsgpu_evp_batch_stats(uint64_t *batches, uint64_t *jobs);
+/* EVP_AEAD_CTX_seal / _open calls whose cipher work ran on the GPU (per-call
+ * or queued; authentication failures included, argument-check rejections
+ * not), process-wide since load.  Lets a caller that interposed the library
+ * under an unchanged libssl check that every TLS record went through it. */
+int tlsgpu_evp_call_stats(uint64_t *seal_calls, uint64_t *open_calls);
 
 /* Diagnostic: hybrid-kernel phase timing.  With TLSGPU_PHASE_STATS=1 in the
  * environment, the first call allocates 32 device counters (shader cycles and
@@ -232,6 +237,11 @@ int tlsgpu_aes_ecb_bitsliced(tlsgpu_sessions *t, uint32_t session, const uint8_t
  * (same stream as the oracle's oracle_fill_bytes; used by bench/tests). */
 int tlsgpu_fill_synthetic(tlsgpu_engine *e, uint8_t *d_out, uint64_t stride,
     uint32_t span_len, uint32_t n, uint64_t seed, uint64_t index0, void *stream);
+/* The same stream for n variable-length spans in one launch: span i covers
+ * d_lengths[i] bytes at d_out + d_offsets[i] (device arrays) and is keyed
+ * (seed, index0 + i). */
+int tlsgpu_fill_synthetic_spans(tlsgpu_engine *e, uint8_t *d_out, const uint64_t *d_offsets,
+    const uint32_t *d_lengths, uint32_t n, uint64_t seed, uint64_t index0, void *stream);
 
 /* Device / pinned-host memory, copies and events on the engine's device, so
  * callers need no other GPU runtime (the bench and tests use only these). */

@@ -122,6 +122,7 @@ def load_library(path: str = LIBPATH) -> C.CDLL:
         "tlsgpu_open_batch": (i32, [vp, vp, u32, vp, vp, vp, vp]),
         "tlsgpu_seal_batch": (i32, [vp, vp, u32, vp, vp, vp, vp]),
         "tlsgpu_fill_synthetic": (i32, [vp, vp, u64, u32, u32, u64, u64, vp]),
+        "tlsgpu_fill_synthetic_spans": (i32, [vp, vp, vp, vp, u32, u64, u64, vp]),
         "tlsgpu_last_error": (C.c_char_p, []),
         "tlsgpu_set_gcm_impl": (i32, [i32]),
         "tlsgpu_get_gcm_impl": (i32, []),
@@ -130,6 +131,7 @@ def load_library(path: str = LIBPATH) -> C.CDLL:
         "tlsgpu_open_wire": (i32, [vp, vp, u32, vp, u32, vp, vp, vp, vp, vp]),
         "tlsgpu_evp_set_batching": (i32, [C.c_uint, C.c_uint, C.c_uint]),
         "tlsgpu_evp_batch_stats": (i32, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+        "tlsgpu_evp_call_stats": (i32, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "tlsgpu_malloc": (i32, [vp, C.c_size_t, C.POINTER(vp)]),
         "tlsgpu_free": (i32, [vp, vp]),
         "tlsgpu_host_alloc": (i32, [vp, C.c_size_t, C.POINTER(vp)]),
@@ -211,6 +213,12 @@ class Engine:
                        index0: int = 0, stream: int | None = None) -> None:
         _check(self.lib.tlsgpu_fill_synthetic(self.handle, d_out, stride, span_len, n, seed,
                                               index0, stream), "tlsgpu_fill_synthetic")
+
+    def fill_synthetic_spans(self, d_out: int, d_offsets: int, d_lengths: int, n: int, seed: int,
+                             index0: int = 0, stream: int | None = None) -> None:
+        _check(self.lib.tlsgpu_fill_synthetic_spans(self.handle, d_out, d_offsets, d_lengths, n,
+                                                    seed, index0, stream),
+               "tlsgpu_fill_synthetic_spans")
 
     def close(self) -> None:
         if self.handle:

@@ -230,11 +230,25 @@ static int initial_gcm_impl() {
   if (v && strcmp(v, "fused") == 0) return TLSGPU_GCM_FUSED;
   return TLSGPU_GCM_QUEUE;
 }
-static std::atomic<int> g_gcm_impl{initial_gcm_impl()};
+// The bitsliced / hybrid / fused GCM variants measured slower than the queue
+// kernel; they are compiled only with `make EXPERIMENTAL=1`
+// (-DTG_EXPERIMENTAL).  Without it, selecting them fails and the default stays.
+#ifdef TG_EXPERIMENTAL
+static constexpr bool kExperimental = true;
+#else
+static constexpr bool kExperimental = false;
+#endif
+static bool impl_built(int impl) {
+  return impl == TLSGPU_GCM_QUEUE || impl == TLSGPU_GCM_TTABLE || kExperimental;
+}
+static std::atomic<int> g_gcm_impl{impl_built(initial_gcm_impl()) ? initial_gcm_impl()
+                                                                 : (int)TLSGPU_GCM_QUEUE};
 
 extern "C" int tlsgpu_set_gcm_impl(int impl) {
   if (impl < TLSGPU_GCM_BITSLICE || impl > TLSGPU_GCM_FUSED)
     return fail(TLSGPU_EINVAL, "unknown gcm impl %d", impl);
+  if (!impl_built(impl))
+    return fail(TLSGPU_EINVAL, "gcm impl %d not built (make EXPERIMENTAL=1)", impl);
   g_gcm_impl.store(impl);
   return TLSGPU_OK;
 }
@@ -246,12 +260,17 @@ extern "C" int tlsgpu_aes_ecb_bitsliced(tlsgpu_sessions* t, uint32_t session, co
   if (session >= t->capacity ||
       (t->kinds[session] != TLSGPU_AES_128_GCM && t->kinds[session] != TLSGPU_AES_256_GCM))
     return fail(TLSGPU_EINVAL, "session %u is not an installed AES-GCM session", session);
+#ifdef TG_EXPERIMENTAL
   HIPCHK(hipSetDevice(t->eng->device));
   int rounds = t->kinds[session] == TLSGPU_AES_128_GCM ? 10 : 14;
   if (launch_bs_ecb(t->d_sess, session, rounds, d_in, d_out, nblocks,
                     stream ? (hipStream_t)stream : t->eng->stream))
     return fail(TLSGPU_EHIP, "bs ecb launch: %s", hipGetErrorString(hipGetLastError()));
   return TLSGPU_OK;
+#else
+  (void)stream;
+  return fail(TLSGPU_EINVAL, "bitsliced AES not built (make EXPERIMENTAL=1)");
+#endif
 }
 
 static int groups_for(const tlsgpu_engine* e, uint32_t n, uint32_t* per_group) {
@@ -333,13 +352,15 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   if (impl != TLSGPU_GCM_TTABLE && (t->have[TLSGPU_AES_128_GCM] || t->have[TLSGPU_AES_256_GCM])) {
     pre = (RecPre*)pre_scratch(t->eng, s, sizeof(RecPre) * (size_t)n + 256);
     if (!pre) return fail(TLSGPU_ENOMEM, "RecPre scratch (%u records)", n);
-    if (impl == TLSGPU_GCM_QUEUE && a.pack) {  // the prep pass's "packable record" flag
-      a.short_flag = reinterpret_cast<uint32_t*>(pre + n);
-      HIPCHK(hipMemsetD32Async((hipDeviceptr_t)a.short_flag, 0, 1, s));
-    }
+    if (impl == TLSGPU_GCM_QUEUE && a.pack)  // the prep passes' "packable record" flags
+      HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(pre + n), 0, 2, s));
   }
   for (int rounds : {10, 14}) {
     if (!t->have[rounds == 10 ? TLSGPU_AES_128_GCM : TLSGPU_AES_256_GCM]) continue;
+    // one flag word per key size: a short AES-128 record must not send the
+    // AES-256 pass to the pack variant
+    if (pre && impl == TLSGPU_GCM_QUEUE && a.pack)
+      a.short_flag = reinterpret_cast<uint32_t*>(pre + n) + (rounds == 10 ? 0 : 1);
     int rc;
     if (impl == TLSGPU_GCM_TTABLE) {
       rc = launch_gcm(a, seal, raw, rounds, groups, s);
@@ -348,11 +369,16 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
       if (rc == 0) {
         if (impl == TLSGPU_GCM_QUEUE)
           rc = launch_gcm_queue(a, pre, seal, rounds, groups, s);
+#ifdef TG_EXPERIMENTAL
         else if (impl == TLSGPU_GCM_FUSED)
           rc = (rounds == 10 ? launch_gcm_fused10 : launch_gcm_fused14)(a, pre, seal, groups, s);
         else
           rc = (rounds == 10 ? launch_gcm_hy10 : launch_gcm_hy14)(
               a, pre, seal, impl == TLSGPU_GCM_HYBRID ? 4 : 8, groups, s);
+#else
+        else
+          rc = -1;
+#endif
       }
     }
     if (rc) {
@@ -420,6 +446,18 @@ extern "C" int tlsgpu_fill_synthetic(tlsgpu_engine* e, uint8_t* d_out, uint64_t 
   HIPCHK(hipSetDevice(e->device));
   if (launch_fill_synthetic(d_out, stride, span_len, n, seed, index0,
                             stream ? (hipStream_t)stream : e->stream))
+    return fail(TLSGPU_EHIP, "fill launch: %s", hipGetErrorString(hipGetLastError()));
+  return TLSGPU_OK;
+}
+
+extern "C" int tlsgpu_fill_synthetic_spans(tlsgpu_engine* e, uint8_t* d_out,
+                                           const uint64_t* d_offsets, const uint32_t* d_lengths,
+                                           uint32_t n, uint64_t seed, uint64_t index0,
+                                           void* stream) {
+  if (!e || (n && (!d_out || !d_offsets || !d_lengths))) return fail(TLSGPU_EINVAL, "bad arguments");
+  HIPCHK(hipSetDevice(e->device));
+  if (launch_fill_synthetic_spans(d_out, d_offsets, d_lengths, n, seed, index0,
+                                  stream ? (hipStream_t)stream : e->stream))
     return fail(TLSGPU_EHIP, "fill launch: %s", hipGetErrorString(hipGetLastError()));
   return TLSGPU_OK;
 }
@@ -734,12 +772,38 @@ static int check_alias(const unsigned char* in, size_t in_len, const unsigned ch
   return 0;
 }
 
-// One EVP call on the GPU.  Layout of the staging buffer:
-// [RawJob | status | nonce | ad | in | out] each 256-B aligned.
+// EVP calls whose cipher work ran on the GPU (tlsgpu_evp_call_stats).
+static std::atomic<uint64_t> g_evp_calls[2];  // [0] open, [1] seal
+
+extern "C" int tlsgpu_evp_call_stats(uint64_t* seal_calls, uint64_t* open_calls) {
+  if (seal_calls) *seal_calls = g_evp_calls[1].load();
+  if (open_calls) *open_calls = g_evp_calls[0].load();
+  return TLSGPU_OK;
+}
+
+static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, size_t* out_len,
+                         size_t max_out_len, const unsigned char* nonce, size_t nonce_len,
+                         const unsigned char* in, size_t in_len, const unsigned char* ad,
+                         size_t ad_len);
+
+// One EVP call on the GPU: 1 = success, 0 = authentication failure / rejected
+// by the kernel (output zero-filled), -1 = runtime failure.
 static int gpu_call(const AeadState* st, bool seal, unsigned char* out, size_t* out_len,
                     size_t max_out_len, const unsigned char* nonce, size_t nonce_len,
                     const unsigned char* in, size_t in_len, const unsigned char* ad,
                     size_t ad_len) {
+  int r = gpu_call_impl(st, seal, out, out_len, max_out_len, nonce, nonce_len, in, in_len, ad,
+                        ad_len);
+  if (r >= 0) g_evp_calls[seal ? 1 : 0].fetch_add(1, std::memory_order_relaxed);
+  return r;
+}
+
+// Layout of the per-call staging buffer:
+// [RawJob | status | nonce | ad | in | out] each 256-B aligned.
+static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, size_t* out_len,
+                         size_t max_out_len, const unsigned char* nonce, size_t nonce_len,
+                         const unsigned char* in, size_t in_len, const unsigned char* ad,
+                         size_t ad_len) {
   if (st->slot & 0x40000000) {  // pooled context: post to the coalescing queue
     EvpJob j = {st, seal, out, max_out_len, nonce, in, ad, nonce_len, in_len, ad_len,
                 TLSGPU_REC_BAD_MAC, false, false};

@@ -188,6 +188,40 @@ __global__ void fill_synthetic(uint8_t* __restrict__ out, uint64_t stride, uint3
   }
 }
 
+// Variable-length spans in one launch: span i (offs[i], lens[i]) keyed index0 + i.
+// One workgroup per span (grid-strided), 8 B per thread-step.
+__global__ void fill_synthetic_spans(uint8_t* __restrict__ out, const uint64_t* __restrict__ offs,
+                                     const uint32_t* __restrict__ lens, uint32_t n, uint64_t seed,
+                                     uint64_t index0) {
+  for (uint32_t span = blockIdx.x; span < n; span += gridDim.x) {
+    const uint32_t len = lens[span];
+    uint8_t* base = out + offs[span];
+    const uint64_t st = seed ^ ((index0 + span) * 0xD1B54A32D192ED03ull);
+    for (uint32_t w = threadIdx.x; w * 8 < len; w += blockDim.x) {
+      uint64_t z = st + (uint64_t)(w + 1) * 0x9E3779B97F4A7C15ull;
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+      z ^= z >> 31;
+      uint8_t* p = base + (uint64_t)w * 8;
+      const uint32_t left = len - w * 8;
+      if (left >= 8 && ((uintptr_t)p & 7) == 0) {
+        *(uint64_t*)p = z;
+      } else {
+        for (uint32_t k = 0; k < 8 && k < left; k++) p[k] = (uint8_t)(z >> (8 * k));
+      }
+    }
+  }
+}
+
+int launch_fill_synthetic_spans(uint8_t* d_out, const uint64_t* d_offs, const uint32_t* d_lens,
+                                uint32_t n, uint64_t seed, uint64_t index0, hipStream_t s) {
+  if (n == 0) return 0;
+  const uint32_t blocks = n < 65536 ? n : 65536;
+  hipLaunchKernelGGL(fill_synthetic_spans, dim3(blocks), dim3(256), 0, s, d_out, d_offs, d_lens, n,
+                     seed, index0);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_session_install(DevSession* sessions, DevGcmTables* tables,
                            const tlsgpu_session_params* d_params, uint32_t first, uint32_t n,
                            hipStream_t s) {

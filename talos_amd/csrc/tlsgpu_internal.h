@@ -199,4 +199,6 @@ int launch_wire_finish(uint32_t n_streams, tlsgpu_wire_result* results, int32_t*
                        hipStream_t s);
 int launch_fill_synthetic(uint8_t* d_out, uint64_t stride, uint32_t span_len,
                           uint32_t n, uint64_t seed, uint64_t index0, hipStream_t s);
+int launch_fill_synthetic_spans(uint8_t* d_out, const uint64_t* d_offs, const uint32_t* d_lens,
+                                uint32_t n, uint64_t seed, uint64_t index0, hipStream_t s);
 }  // namespace tg

@@ -50,6 +50,28 @@ def zipf_lengths(n: int, seed: int, lo: int = 64, hi: int = 16384, alpha: float 
     return rng.choice(ls, size=n, p=p).astype(np.int64)
 
 
+def session_plan(kind: int, n_records: int, n_sessions: int, seed: int):
+    """(session params, start seqs, per-record session, per-record seq) of a
+    workload; oracle/batch_digest.c restates the same rule in C."""
+    params, start_seq = [], []
+    for s in range(n_sessions):
+        key = fill_bytes(seed ^ KEY_TAG, s, KEY_LEN[kind])
+        fiv = fill_bytes(seed ^ IV_TAG, s, FIXED_IV_LEN[kind])
+        params.append(SessionParams(kind, key, fiv))
+        sq = int.from_bytes(fill_bytes(seed ^ SEQ_TAG, s, 8), "little")
+        # some sessions sit just below a byte / 32-bit carry
+        if s % 7 == 1:
+            sq = (sq | 0xFF) - 3
+        elif s % 7 == 2:
+            sq = (sq | 0xFFFFFFFF) - 5
+        start_seq.append(sq & M64)
+    per = max(1, n_records // n_sessions)
+    r = np.arange(n_records, dtype=np.int64)
+    session = np.minimum(r // per, n_sessions - 1).astype(np.uint32)
+    seq = np.array(start_seq, dtype=np.uint64)[session] + (r % per).astype(np.uint64)
+    return params, start_seq, session, seq
+
+
 class Workload:
     """R records over S sessions of one AEAD kind, resident in HBM.
 
@@ -65,7 +87,6 @@ class Workload:
         self.n = n_records
         self.seed = seed
         self.S = n_sessions
-        per = max(1, n_records // n_sessions)
         self.lengths = (np.full(n_records, record_len, dtype=np.int64) if lengths is None
                         else np.asarray(lengths, dtype=np.int64))
         eiv = EXPLICIT_NONCE_LEN[kind]
@@ -77,28 +98,11 @@ class Workload:
         self.pt_bytes = int(pt_slot.sum())
         self.body_bytes = int(body_slot.sum()) + 16
 
-        # sessions
-        self.params = []
-        self.start_seq = []
-        for s in range(n_sessions):
-            key = fill_bytes(seed ^ KEY_TAG, s, KEY_LEN[kind])
-            fiv = fill_bytes(seed ^ IV_TAG, s, FIXED_IV_LEN[kind])
-            self.params.append(SessionParams(kind, key, fiv))
-            sq = int.from_bytes(fill_bytes(seed ^ SEQ_TAG, s, 8), "little")
-            # some sessions sit just below a byte / 32-bit carry
-            if s % 7 == 1:
-                sq = (sq | 0xFF) - 3
-            elif s % 7 == 2:
-                sq = (sq | 0xFFFFFFFF) - 5
-            self.start_seq.append(sq & M64)
+        # sessions, record -> session map and sequence numbers
+        self.params, self.start_seq, self.session, self.seq = session_plan(
+            kind, n_records, n_sessions, seed)
         self.table = SessionTable(engine, n_sessions)
         self.table.install(0, self.params)
-
-        r = np.arange(n_records, dtype=np.int64)
-        self.session = np.minimum(r // per, n_sessions - 1).astype(np.uint32)
-        seqs = (np.array(self.start_seq, dtype=np.uint64)[self.session] +
-                (r % per).astype(np.uint64))
-        self.seq = seqs
         self.rtype = np.full(n_records, 23, dtype=np.uint32)
 
         # device buffers
@@ -106,12 +110,19 @@ class Workload:
         self.d_body = DeviceBuffer(engine, self.body_bytes)
         self.d_out = DeviceBuffer(engine, self.pt_bytes)
         self.d_status = DeviceBuffer(engine, 4 * n_records)
-        if lengths is None:
-            engine.fill_synthetic(self.d_pt.ptr, record_len, record_len, n_records, seed, index0)
-        else:
-            for i in range(n_records):  # variable spans: one launch per record is fine here
-                engine.fill_synthetic(self.d_pt.ptr + int(self.pt_off[i]), 0, int(self.lengths[i]),
-                                      1, seed, index0 + i)
+        if lengths is None:  # record i's plaintext = fill(seed, index0 + i) at pt_off[i]
+            engine.fill_synthetic(self.d_pt.ptr, (record_len + 15) // 16 * 16, record_len,
+                                  n_records, seed, index0)
+        else:  # variable spans: one launch over (offset, length) arrays
+            d_offs = DeviceBuffer(engine, 8 * n_records)
+            d_lens = DeviceBuffer(engine, 4 * n_records)
+            d_offs.upload(self.pt_off.astype(np.uint64).view(np.uint8))
+            d_lens.upload(self.lengths.astype(np.uint32).view(np.uint8))
+            engine.fill_synthetic_spans(self.d_pt.ptr, d_offs.ptr, d_lens.ptr, n_records, seed,
+                                        index0)
+            engine.sync()
+            d_offs.free()
+            d_lens.free()
         seal = np.zeros(n_records, dtype=RECORD_DTYPE)
         seal["in_off"] = self.pt_off
         seal["out_off"] = self.body_off
@@ -138,13 +149,43 @@ class Workload:
             raise RuntimeError("workload seal failed for %d records" % int((st != body_len).sum()))
         self.tampered = np.zeros(n_records, dtype=bool)
         if tamper_every:
-            idx = np.arange(tamper_every // 2, n_records, tamper_every)
-            for i in idx:   # flip one ciphertext/tag bit (SURVEY.md §8d tamper subset)
-                pos = int(self.body_off[i]) + eiv + int((i * 7919) % (self.lengths[i] + TAG_LEN))
-                b = self.d_body.download(1, pos)
-                b[0] ^= 1 << int(i % 8)
-                self.d_body.upload(b, pos)
-            self.tampered[idx] = True
+            self.apply_tamper(tamper_every)
+
+    def apply_tamper(self, every: int) -> None:
+        """Flip one ciphertext/tag bit of records every//2, every//2 + every, ...
+        (SURVEY.md §8d tamper subset): bit i%8 of body byte eiv + (i*7919) %
+        (len + 16).  oracle/batch_digest.c applies the same rule."""
+        eiv = EXPLICIT_NONCE_LEN[self.kind]
+        idx = np.arange(every // 2, self.n, every)
+        for i in idx:
+            pos = int(self.body_off[i]) + eiv + int((i * 7919) % (self.lengths[i] + TAG_LEN))
+            b = self.d_body.download(1, pos)
+            b[0] ^= 1 << int(i % 8)
+            self.d_body.upload(b, pos)
+        self.tampered[idx] = True
+
+    def sealed_digest(self) -> str:
+        """SHA-256 over the record bodies (explicit nonce || ct || tag) in record
+        order, as tests/golden/batch_digests.json pins them."""
+        import hashlib
+        eiv = EXPLICIT_NONCE_LEN[self.kind]
+        body = self.d_body.download()
+        h = hashlib.sha256()
+        mv = memoryview(body)
+        for off, ln in zip(self.body_off.tolist(), (self.lengths + eiv + TAG_LEN).tolist()):
+            h.update(mv[off:off + ln])
+        return h.hexdigest()
+
+    def opened_digest(self) -> str:
+        """SHA-256 over the opened plaintexts (tampered records zero-filled) in
+        record order."""
+        import hashlib
+        out = self.d_out.download()
+        h = hashlib.sha256()
+        mv = memoryview(out)
+        for off, ln in zip(self.pt_off.tolist(), self.lengths.tolist()):
+            h.update(mv[off:off + ln])
+        return h.hexdigest()
 
     def seal(self, stream=None):
         seal_batch(self.table, self.d_seal.ptr, self.n, self.d_pt.ptr, self.d_body.ptr,

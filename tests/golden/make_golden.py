@@ -12,8 +12,14 @@ Inputs (read-only, never copied as source):
     to give record-level vectors at sizes no reference test covers
     (nothing pins 16 KiB / 1400 B / record level).
 
+  * oracle/_ref/batch_digest (our generator over oracle/_ref/libssl_ref.so,
+    the whole reference libcrypto compiled from its own sources) — SHA-256
+    digests of the full-size seeded batches of SURVEY.md §8d (configs B, C, D,
+    plus session-count variants), sealed and opened by the reference with the
+    t1_enc framing and the workload rules of talos_amd/workload.py.
+
 Outputs: aeadtests.txt, gcm128_vectors.json, chacha_vectors.json,
-poly1305_vectors.json, records.json.
+poly1305_vectors.json, records.json, batch_digests.json.
 """
 from __future__ import annotations
 
@@ -128,6 +134,49 @@ def make_records(ref: po.Reference):
     return recs
 
 
+# name: (aead, records, sessions, seed, tamper_every, length or "zipf")
+BATCHES = {
+    # full-size BASELINE configs (checked on the GPU)
+    "B": ("aes-128-gcm", 65536, 1024, 0x5EED0001, 1024, 16384),
+    "C": ("chacha20-poly1305", 1 << 20, 4096, 0x5EED0002, 1024, 1400),
+    "D": ("aes-256-gcm", 1 << 18, 1024, 0x5EED0003, 1024, "zipf"),
+    # session-count sensitivity: one session, one record per session
+    "B_S1": ("aes-128-gcm", 65536, 1, 0x5EED0001, 1024, 16384),
+    "B_Sn": ("aes-128-gcm", 65536, 65536, 0x5EED0001, 1024, 16384),
+    # small batches the CPU restatement re-derives in seconds (tests/test_oracle_kat.py)
+    "B_small": ("aes-128-gcm", 96, 8, 0x5EED0001, 16, 16384),
+    "C_small": ("chacha20-poly1305", 512, 32, 0x5EED0002, 64, 1400),
+    "D_small": ("aes-256-gcm", 256, 16, 0x5EED0003, 32, "zipf"),
+    "old_small": ("chacha20-poly1305-old", 128, 8, 0x5EED0005, 16, 1000),
+}
+
+
+def make_batch_digests():
+    import subprocess
+    import tempfile
+
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    from talos_amd.workload import zipf_lengths
+    exe = os.path.join(ROOT, "oracle", "_ref", "batch_digest")
+    out = {}
+    for name, (aead, n, S, seed, tamper, ln) in BATCHES.items():
+        with tempfile.NamedTemporaryFile(suffix=".u32") as f:
+            if ln == "zipf":
+                f.write(zipf_lengths(n, seed).astype(np.uint32).tobytes())
+                f.flush()
+                arg = "@" + f.name
+            else:
+                arg = str(ln)
+            r = subprocess.run([exe, aead, str(n), str(S), hex(seed), str(tamper), arg],
+                               check=True, capture_output=True, text=True)
+        d = json.loads(r.stdout)
+        d["lengths"] = ln
+        out[name] = d
+        print(name, d["sealed_sha256"][:16], d["opened_sha256"][:16], flush=True)
+    return out
+
+
 def main():
     os.makedirs(HERE, exist_ok=True)
     shutil.copyfile(os.path.join(REFT, "aeadtests.txt"), os.path.join(HERE, "aeadtests.txt"))
@@ -142,6 +191,10 @@ def main():
     json.dump({"generator": "tests/golden/make_golden.py via oracle/_ref/libref.so",
                "records": make_records(ref)},
               open(os.path.join(HERE, "records.json"), "w"), indent=1)
+    json.dump({"generator": "tests/golden/make_golden.py via oracle/_ref/batch_digest "
+                            "(reference libcrypto, oracle/_ref/libssl_ref.so)",
+               "batches": make_batch_digests()},
+              open(os.path.join(HERE, "batch_digests.json"), "w"), indent=1)
     print("golden fixtures written to", HERE)
 
 

@@ -76,6 +76,18 @@ def test_evp_error_semantics(ta):
     c = ta.EvpAead(ta.CHACHA20_POLY1305, bytes(32))
     ok, out, ol = c.seal(bytes(8), b"abc", b"")                    # wrong nonce length
     assert ok == 0 and ol == 0
+    # check_alias (evp_aead.c:79-87): out may alias in only at or before it
+    import ctypes as C
+    for fn, shift, want in ((a.lib.EVP_AEAD_CTX_seal, 1, 0), (a.lib.EVP_AEAD_CTX_seal, 0, 1),
+                            (a.lib.EVP_AEAD_CTX_open, 3, 0)):
+        buf = (C.c_ubyte * 256)(*([0x5A] * 256))
+        base = C.addressof(buf)
+        ol = C.c_size_t(99)
+        ok = fn(C.byref(a.ctx), C.c_void_p(base + 16 + shift), C.byref(ol), 100,
+                a._b(bytes(12)), 12, C.c_void_p(base + 16), 64, a._b(b""), 0)
+        assert ok == want, (shift, ok)
+        if not want:  # rejected before any cipher work: zero-filled, out_len 0
+            assert bytes(buf)[16 + shift:16 + shift + 100] == bytes(100) and ol.value == 0
     a.cleanup()
     c.cleanup()
 
@@ -181,11 +193,23 @@ def test_batch_seal_open_all_lengths(ta, engine, oracle, name):
     _run_seal_open(ta, engine, oracle, [KINDS[name]] * 3, LENGTHS, seed=11)
 
 
+EXPERIMENTAL_IMPLS = ("hybrid", "bitslice", "fused")
+
+
 @pytest.fixture
 def gcm_impl(ta):
-    """Run a test under one GCM kernel and restore the default afterwards."""
+    """Run a test under one GCM kernel and restore the default afterwards.  The
+    slower variants exist only in a `make EXPERIMENTAL=1` build."""
     prev = ta.get_gcm_impl()
-    yield lambda impl: ta.set_gcm_impl(impl)
+
+    def use(impl):
+        try:
+            ta.set_gcm_impl(impl)
+        except ta.TlsGpuError:
+            if impl in EXPERIMENTAL_IMPLS:
+                pytest.skip(f"gcm impl {impl} not built (make EXPERIMENTAL=1)")
+            raise
+    yield use
     ta.set_gcm_impl(prev)
 
 
@@ -212,9 +236,10 @@ def test_batch_bitsliced_long_records(ta, engine, oracle, gcm_impl, name, shift,
 
 
 @pytest.mark.parametrize("name", ["aes-128-gcm", "aes-256-gcm"])
-def test_bitsliced_aes_core_ecb(ta, engine, oracle, name):
+def test_bitsliced_aes_core_ecb(ta, engine, oracle, gcm_impl, name):
     """The bitsliced AES core against the oracle's AES (aes_core.c) on random
-    blocks, plus the FIPS-197 C.1 / C.3 known answers."""
+    blocks, plus the FIPS-197 C.1 / C.3 known answers (EXPERIMENTAL build)."""
+    gcm_impl("bitslice")   # skips when the experimental kernels are not built
     rnd = random.Random(31)
     kind = KINDS[name]
     klen = po.KEY_LEN[kind]
@@ -313,13 +338,16 @@ def test_batch_short_record_packs_zipf(ta, engine, oracle, gcm_impl):
     _run_seal_open(ta, engine, oracle, [KINDS["aes-256-gcm"]] * 2, lengths, seed=42)
 
 
-def test_batch_packs_long_runs(ta, engine):
+def test_batch_packs_long_runs(ta, engine, oracle, gcm_impl):
     """One session over 600 K mostly-short records: every workgroup's range is
     longer than the LDS pack plan (kPlanCap = 2,048 records), so runs are split.
     Device seal -> tamper 1/97 -> device open; statuses exact, sampled
-    plaintexts equal, tampered records zero-filled (Workload.verify_open)."""
+    plaintexts equal, tampered records zero-filled (Workload.verify_open);
+    sampled sealed bodies equal the oracle's (a symmetric seal/open error in
+    the shared pack GHASH code would cancel out in the round trip alone)."""
     import numpy as np
     from talos_amd.workload import Workload
+    gcm_impl("queue")
     n = 600_000
     rng = np.random.default_rng(7)
     lengths = rng.integers(0, 200, n)
@@ -327,7 +355,65 @@ def test_batch_packs_long_runs(ta, engine):
     for kind in (po.AES_128_GCM, po.AES_256_GCM):
         wl = Workload(engine, kind, n, 1, 0x5EED0041, lengths=lengths, record_len=0,
                       tamper_every=97)
+        p = wl.params[0]
+        osess = oracle.tls_session(kind, p.key, p.fixed_iv)
+        for i in np.random.default_rng(kind).choice(n, 64, replace=False).tolist() + [0, n - 1]:
+            if wl.tampered[i]:
+                continue
+            ln = int(wl.lengths[i])
+            pt = wl.d_pt.download(ln, int(wl.pt_off[i])).tobytes()
+            body = wl.d_body.download(ln + 24, int(wl.body_off[i])).tobytes()
+            assert body == oracle.tls_seal(osess, int(wl.seq[i]), 23, pt), i
         wl.open()
         engine.sync()
         wl.verify_open(sample=512)
         wl.free()
+
+
+# Records of 63+ blocks only: the prep pass leaves the pack flag clear, so the
+# no-pack queue-kernel variant runs (the one config B uses); AES-128 and
+# AES-256 in one batch check the per-key-size flag words.
+LONG_ONLY = [ln for ln in LENGTHS + BS_LENGTHS if ln > 992]
+
+
+@pytest.mark.parametrize("name", ["aes-128-gcm", "aes-256-gcm"])
+def test_batch_queue_no_pack_variant(ta, engine, oracle, gcm_impl, name):
+    gcm_impl("queue")
+    _run_seal_open(ta, engine, oracle, [KINDS[name]] * 2, LONG_ONLY, seed=43)
+
+
+def test_batch_queue_mixed_key_sizes_pack_flags(ta, engine, oracle, gcm_impl):
+    """Short AES-128 records beside long-only AES-256 records in one batch."""
+    gcm_impl("queue")
+    kinds = [po.AES_128_GCM, po.AES_256_GCM]
+    from talos_amd.batch import RecordBatch
+    rnd = random.Random(44)
+    params = _mk_sessions(ta, rnd, kinds)
+    table = ta.SessionTable(engine, 2)
+    table.install(0, params)
+    osess = _oracle_sessions(oracle, params)
+    recs = [(0, i, 23, bytes(rnd.getrandbits(8) for _ in range(ln)), kinds[0])
+            for i, ln in enumerate([0, 5, 100, 700])]
+    recs += [(1, i, 23, bytes(rnd.getrandbits(8) for _ in range(ln)), kinds[1])
+             for i, ln in enumerate([2000, 16384, 5000])]
+    sb = RecordBatch(engine, recs, "seal")
+    sb.run(table)
+    for (st, body), (sid, seq, rtype, pt, _) in zip(sb.results(), recs):
+        assert body == oracle.tls_seal(osess[sid], seq, rtype, pt)
+    table.close()
+
+
+def test_batch_packs_disabled_env(ta):
+    """TLSGPU_PACK=0 (read at library load): the short-record mix runs through
+    the no-pack variant, in a child process with the variable set."""
+    import subprocess
+    code = ("import sys; sys.path[:0] = [%r, %r]\n"
+            "import test_gpu_parity as t, pyoracle as po, talos_amd as ta\n"
+            "ta.load_library(); e = ta.Engine(0); o = po.Oracle()\n"
+            "for k in (po.AES_128_GCM, po.AES_256_GCM):\n"
+            "    t._run_seal_open(ta, e, o, [k] * 2, t.PACK_LENGTHS, seed=45)\n"
+            "e.close(); print('ok')\n") % (os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle"))
+    env = dict(os.environ, TLSGPU_PACK="0", TLSGPU_GCM_IMPL="queue")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=100,
+                       env=env, cwd=ROOT)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]

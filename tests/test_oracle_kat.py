@@ -106,3 +106,43 @@ def test_fill_bytes_matches_c(oracle):
         buf = (C.c_ubyte * n)()
         oracle.lib.oracle_fill_bytes(seed, idx, buf, n)
         assert bytes(buf) == fill_bytes(seed, idx, n)
+
+
+def _batches():
+    return json.load(open(os.path.join(GOLD, "batch_digests.json")))["batches"]
+
+
+@pytest.mark.parametrize("name", [k for k in _batches() if k.endswith("_small")])
+def test_batch_digests_oracle(oracle, name):
+    """The CPU restatement re-derives the reference's small seeded batch digests
+    (tests/golden/batch_digests.json, made by oracle/_ref/batch_digest over the
+    reference libcrypto): same sessions / seqs / plaintexts as
+    talos_amd.workload, sealed, tampered, opened, hashed in record order."""
+    import ctypes as C
+    import numpy as np
+    from talos_amd.workload import session_plan, zipf_lengths
+    d = _batches()[name]
+    kind = po.KIND_BY_NAME[d["aead"]]
+    n, S, seed, te = d["records"], d["sessions"], d["seed"], d["tamper_every"]
+    lengths = (zipf_lengths(n, seed) if d["lengths"] == "zipf"
+               else np.full(n, d["lengths"], dtype=np.int64))
+    params, _, session, seq = session_plan(kind, n, S, seed)
+    sess = [oracle.tls_session(kind, p.key, p.fixed_iv) for p in params]
+    oracle.lib.oracle_fill_bytes.argtypes = [C.c_uint64, C.c_uint64, C.c_void_p, C.c_size_t]
+    eiv = 8 if kind in (po.AES_128_GCM, po.AES_256_GCM) else 0
+    hs, ho, bad = hashlib.sha256(), hashlib.sha256(), 0
+    for r in range(n):
+        ln = int(lengths[r])
+        buf = (C.c_ubyte * max(ln, 1))()
+        oracle.lib.oracle_fill_bytes(seed, r, buf, ln)
+        pt = bytes(buf)[:ln]
+        body = bytearray(oracle.tls_seal(sess[session[r]], int(seq[r]), 23, pt))
+        hs.update(body)
+        if te and r % te == te // 2:
+            body[eiv + (r * 7919) % (ln + 16)] ^= 1 << (r % 8)
+        st, out = oracle.tls_open(sess[session[r]], int(seq[r]), 23, bytes(body))
+        bad += st == -1
+        ho.update(out if st == 1 else bytes(ln))
+    assert hs.hexdigest() == d["sealed_sha256"]
+    assert ho.hexdigest() == d["opened_sha256"]
+    assert bad == d["bad_record_mac"]
