@@ -10,6 +10,7 @@ Inputs are synthetic (counter-SplitMix64 plaintexts, 1024 sessions x 64 records,
 sealer; every step's outputs are verified after the warmup.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config B|C|D]
+                  [--sessions S] [--interleave] [--mode device|host|wire|copy]
   N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
        (one rank per GPU, records split by rank, no collective on the data path;
         gloo only for the barrier and the max-over-ranks of the timing).
@@ -56,8 +57,9 @@ def main_kernel(kind_name: str, op: str, short_records: bool = False) -> str:
     """Name of the step's dominant kernel as rocprofv3 lists it (the queue kernel's
     pack variant runs when the batch has records of <= 62 blocks)."""
     import talos_amd as ta
-    if "gcm" not in kind_name:
-        return f"tg::chacha_batch_kernel<{'true' if op != 'open' else 'false'}, false>"
+    if "gcm" not in kind_name:   # the LDS-staged TLS kernel (DESIGN.md §4.5); C = seal + open
+        return "tg::chacha_tls_kernel<" if op == "seal+open" else \
+            f"tg::chacha_tls_kernel<{'true' if op == 'seal' else 'false'}>"
     rounds = 10 if "128" in kind_name else 14
     seal = "true" if op != "open" else "false"
     impl = ta.get_gcm_impl()
@@ -69,26 +71,67 @@ def main_kernel(kind_name: str, op: str, short_records: bool = False) -> str:
             "ttable": f"tg::gcm_batch_kernel<{seal}, false, {rounds}>"}[impl]
 
 
-def cpu_baseline(kind_name: str, rec_len: int, op: str, note: str = "") -> dict | None:
+def host_cpus() -> tuple[int, int, str, str]:
+    """(threads usable by this process, visible cores, CPU model, what limits it).
+    Usable = the affinity set, capped by the cgroup CPU quota (cpu.max) when one
+    is set: on the GPU box the process's share is a quota, not a cpuset."""
+    visible = len(os.sched_getaffinity(0))
+    usable, why = visible, "sched_getaffinity"
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+            if quota < usable:
+                usable, why = quota, f"cgroup cpu.max quota ({q}/{period})"
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return usable, visible, model, why
+
+
+def cpu_baseline(kind_name: str, rec_len, op: str, note: str = "") -> dict | None:
+    """Reference LibreSSL EVP_AEAD_CTX_open/seal (oracle/_ref/libref.so) on every
+    core this process may use; rec_len is an int or an array of record lengths
+    (the Zipf mix itself, passed to cpubench as a lengths file)."""
     # the reference build links LibreSSL's x86-64 AES-NI and PCLMUL GHASH
     # assembly (oracle/Makefile); its ChaCha20 and Poly1305 are the portable C
     impl = ("AES-NI + PCLMUL GHASH asm" if "gcm" in kind_name
             else "portable C chacha.c + poly1305-donna")
     try:
+        import tempfile
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import pyoracle
         if not (os.path.exists(pyoracle.LIBREF) and os.path.exists(pyoracle.CPUBENCH)):
             return None
-        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        threads, visible, model, why = host_cpus()
         secs = max(1.0, 20.0 / threads)   # ~20 s of CPU work in total
-        nrec = max(threads * 16, 1024)
-        r = pyoracle.run_cpubench(kind_name, "both" if op == "seal+open" else op, rec_len, nrec,
+        if np.ndim(rec_len):
+            lens = np.asarray(rec_len, dtype=np.uint32)
+            nrec = len(lens)
+            with tempfile.NamedTemporaryFile(suffix=".u32", delete=False) as f:
+                f.write(lens.tobytes())
+                arg = "@" + f.name
+            what = f"{nrec} records of the workload's own length mix (mean {lens.mean():.0f} B)"
+        else:
+            nrec = max(threads * 16, 1024)
+            arg, what = rec_len, f"{nrec} x {rec_len}-B records"
+        r = pyoracle.run_cpubench(kind_name, "both" if op == "seal+open" else op, arg, nrec,
                                   threads, secs)
+        if isinstance(arg, str):
+            os.unlink(arg[1:])
         return {"value": round(r["gib_per_s"], 3), "unit": "GiB/s", "cores": threads,
                 "kind": "reference",
-                "sample": f"LibreSSL 2.4.1 EVP_AEAD_CTX_{op} ({impl}) over {nrec} x "
-                          f"{rec_len}-B records{note}, {threads} pthreads x {secs:.1f}s "
-                          f"({r['records']} records timed), oracle/_ref/libref.so"}
+                "host": f"{model}; {threads} threads = {why}, {visible} cores visible",
+                "sample": f"LibreSSL 2.4.1 EVP_AEAD_CTX_{op} ({impl}) over {what}{note}, "
+                          f"{threads} pthreads x {secs:.1f}s ({r['records']} records timed), "
+                          f"oracle/_ref/libref.so"}
     except Exception as exc:  # baseline is reported, never fatal
         return {"value": None, "error": str(exc)[:200]}
 
@@ -114,11 +157,17 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
     ap.add_argument("--records", type=int, default=0, help="override records per GPU")
+    ap.add_argument("--sessions", type=int, default=0,
+                    help="override sessions per GPU (SURVEY.md §8d sensitivity: 1 .. #records)")
+    ap.add_argument("--interleave", action="store_true",
+                    help="deal records to sessions round-robin (a many-connection server "
+                         "batch) instead of grouping each session's records")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", default="device", choices=["device", "host", "wire"],
+    ap.add_argument("--mode", default="device", choices=["device", "host", "wire", "copy"],
                     help="host: pinned host buffers + H2D/D2H overlap (PCIe-inclusive rate); "
                          "wire: raw TLS wire streams through tlsgpu_open_wire (framing + "
-                         "in-place open, SURVEY.md §8f-1)")
+                         "in-place open, SURVEY.md §8f-1); copy: the box's achievable "
+                         "device-to-device copy bandwidth (hipMemcpy, 1 GiB)")
     args = ap.parse_args()
 
     import talos_amd as ta
@@ -128,12 +177,16 @@ def main():
     world, rank, local = env_rank()
     ta.load_library()
     eng = ta.Engine(device_for(local, ta.device_count()))  # first GPU runtime user
+    if args.mode == "copy":
+        return copy_mode(args, eng)
     cp = ControlPlane(world)   # gloo control plane: barrier + max over ranks only
 
     kind_name, per_gpu, sessions, rec_len, seed, op = CONFIGS[args.config]
     if args.records:
         per_gpu = args.records
         sessions = max(1, min(sessions, per_gpu // 16))
+    if args.sessions:
+        sessions = min(args.sessions, per_gpu)
     kind = ta.AEAD_NAMES[kind_name]
     # weak scaling: the global batch has world * per_gpu records; rank r owns a
     # contiguous equal-byte slice, no data-path collective
@@ -143,7 +196,8 @@ def main():
     lengths = None if rec_len else glob[lo:hi]
     wl = Workload(eng, kind, hi - lo, max(1, sessions * (hi - lo) // per_gpu),
                   seed ^ (rank * 0x100000001), lengths=lengths, record_len=rec_len or 0,
-                  index0=lo, tamper_every=1024 if op == "open" and args.mode != "wire" else 0)
+                  index0=lo, tamper_every=1024 if op == "open" and args.mode != "wire" else 0,
+                  interleave=args.interleave)
     total_len = int(wl.lengths.sum())
     if args.mode == "host":
         return host_mode(args, eng, wl, kind_name, total_len)
@@ -225,6 +279,7 @@ def main():
                                f"{'16 KiB' if rec_len == 16384 else (str(rec_len) + ' B' if rec_len else 'Zipf 64 B-16 KiB')}"
                                f" records, {per_gpu} records/GPU, device-resident",
                    "records_per_gpu": per_gpu, "sessions_per_gpu": sessions,
+                   "session_order": "interleaved" if args.interleave else "grouped",
                    "gcm_impl": ta.get_gcm_impl() if "gcm" in kind_name else None,
                    "payload_bytes_per_gpu": total_len, "parallelism": f"batch split x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -237,16 +292,40 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if rec_len:
             line["cpu_baseline"] = cpu_baseline(kind_name, rec_len, op)
-        else:  # mixed lengths: the mix's mean record length
-            mean = max(1, int(round(total_len / per_gpu)))
-            line["cpu_baseline"] = cpu_baseline(kind_name, mean, op,
-                                                " (the Zipf mix's mean length)")
+        else:  # mixed lengths: the first 16 Ki records of the workload's own Zipf mix
+            line["cpu_baseline"] = cpu_baseline(kind_name, lengths[:16384], op)
     if rank == 0:
         print(json.dumps(line), flush=True)
     ev0.close()
     ev1.close()
     wl.free()
     cp.close()
+    eng.close()
+
+
+def copy_mode(args, eng):
+    """Achievable HBM bandwidth on this box: hipMemcpyAsync device-to-device of
+    1 GiB (read 1 GiB + write 1 GiB per step), HIP events on the engine stream."""
+    import talos_amd as ta
+    nbytes = 1 << 30
+    a, b = ta.DeviceBuffer(eng, nbytes), ta.DeviceBuffer(eng, nbytes)
+    a.fill(0x5A)
+    ev0, ev1 = ta.Event(eng), ta.Event(eng)
+    for _ in range(max(1, args.warmup)):
+        b.copy_from(a)
+    eng.sync()
+    ev0.record()
+    for _ in range(args.steps):
+        b.copy_from(a)
+    ev1.record()
+    ms = ev0.elapsed_ms(ev1) / args.steps
+    print(json.dumps({"metric": "device-to-device copy bandwidth (hipMemcpyAsync, 1 GiB)",
+                      "value": round(2 * nbytes / (ms / 1e3) / 1e9, 1), "unit": "GB/s",
+                      "note": "read + written bytes / time", "ms_per_copy": round(ms, 4),
+                      "frac_of_8TBs": round(2 * nbytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                      "steps": args.steps}), flush=True)
+    for x in (a, b):
+        x.free()
     eng.close()
 
 

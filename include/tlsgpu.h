@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define TLSGPU_ABI_VERSION 1
+#define TLSGPU_ABI_VERSION 2	/* 2: batch calls take buffer sizes */
 
 /* AEAD kinds (crypto/evp/e_aes.c:1512-1546, e_chacha20poly1305.c:288-322). */
 enum tlsgpu_aead {
@@ -60,6 +60,10 @@ enum tlsgpu_aead {
 /* tlsgpu_open_wire only: plaintext longer than SSL3_RT_MAX_PLAIN_LENGTH
  * (s3_pkt.c:465-469) -> record_overflow alert, not delivered. */
 #define TLSGPU_REC_OVERFLOW (-4)
+/* tlsgpu_open_batch / _seal_batch: the record's input span (in_off, length) or
+ * output span (out_off, plaintext / fragment length) leaves d_in / d_out as
+ * sized by the caller; nothing of the record was read or written. */
+#define TLSGPU_REC_OUT_OF_BOUNDS (-5)
 
 /* Largest plaintext per record the batch kernels accept: 65534 AES blocks, so
  * GCM counters 2..nb+1 stay below 2^16 (TLS records are <= 16 KiB + 2 KiB,
@@ -121,14 +125,18 @@ void tlsgpu_sessions_destroy(tlsgpu_sessions *t);
 int tlsgpu_sessions_install(tlsgpu_sessions *t, uint32_t first, uint32_t n,
     const tlsgpu_session_params *params);
 
-/* Batch record decrypt / encrypt (device-resident).  Records should be grouped
- * by session for speed (a workgroup rebuilds its LDS GHASH table when the
- * session changes); any order is correct.  d_status: int32 per record.
- * Asynchronous on `stream` (NULL = engine stream). */
+/* Batch record decrypt / encrypt (device-resident).  Any record order is
+ * correct; grouping each session's records together is fastest.  in_bytes /
+ * out_bytes are the sizes of d_in / d_out: records whose spans leave them get
+ * TLSGPU_REC_OUT_OF_BOUNDS and are not touched.  d_status: int32 per record.
+ * d_in == d_out is allowed (in-place open at out_off = in_off + 8 for GCM,
+ * t1_enc.c:951-955).  Asynchronous on `stream` (NULL = engine stream). */
 int tlsgpu_open_batch(tlsgpu_sessions *t, const tlsgpu_record *d_recs, uint32_t n,
-    const uint8_t *d_in, uint8_t *d_out, int32_t *d_status, void *stream);
+    const uint8_t *d_in, size_t in_bytes, uint8_t *d_out, size_t out_bytes, int32_t *d_status,
+    void *stream);
 int tlsgpu_seal_batch(tlsgpu_sessions *t, const tlsgpu_record *d_recs, uint32_t n,
-    const uint8_t *d_in, uint8_t *d_out, int32_t *d_status, void *stream);
+    const uint8_t *d_in, size_t in_bytes, uint8_t *d_out, size_t out_bytes, int32_t *d_status,
+    void *stream);
 
 /* ---------------------------------------------------------------------------
  * Wire-record framing: ssl3_get_record (ssl/s3_pkt.c:279-495)

@@ -16,8 +16,9 @@
  * numbers with near-carry starts, counter-SplitMix64 plaintexts, tamper rule),
  * so the GPU test regenerates the same batch on the device and compares.
  *
- * usage: batch_digest AEAD N_RECORDS N_SESSIONS SEED TAMPER_EVERY LEN|@lengths.u32
+ * usage: batch_digest AEAD N_RECORDS N_SESSIONS SEED TAMPER_EVERY LEN|@lengths.u32 [interleave]
  *   AEAD: aes-128-gcm | aes-256-gcm | chacha20-poly1305 | chacha20-poly1305-old
+ *   interleave: records dealt to sessions round-robin (workload.py session_plan)
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -63,10 +64,11 @@ hex(const unsigned char *d, char *out)
 int
 main(int argc, char **argv)
 {
-	if (argc != 7) {
-		fprintf(stderr, "usage: %s AEAD N S SEED TAMPER_EVERY LEN|@file\n", argv[0]);
+	if (argc != 7 && argc != 8) {
+		fprintf(stderr, "usage: %s AEAD N S SEED TAMPER_EVERY LEN|@file [interleave]\n", argv[0]);
 		return 2;
 	}
+	const int interleave = argc == 8 && !strcmp(argv[7], "interleave");
 	const char *name = argv[1];
 	long n = atol(argv[2]), S = atol(argv[3]);
 	uint64_t seed = strtoull(argv[4], NULL, 0);
@@ -131,8 +133,8 @@ main(int argc, char **argv)
 	SHA256_Init(&ho);
 	long bad = 0;
 	for (long r = 0; r < n; r++) {
-		long s = r / per < S - 1 ? r / per : S - 1;
-		uint64_t seq = seq0[s] + (uint64_t)(r % per);
+		long s = interleave ? r % S : (r / per < S - 1 ? r / per : S - 1);
+		uint64_t seq = seq0[s] + (uint64_t)(interleave ? r / S : r % per);
 		size_t len = lens[r];
 		fill(seed, r, pt, len);
 		unsigned char ad[13], nonce[12];
@@ -188,8 +190,8 @@ main(int argc, char **argv)
 	for (long i = 0; i < n; i++)
 		payload += lens[i];
 	printf("{\"aead\": \"%s\", \"records\": %ld, \"sessions\": %ld, \"seed\": %llu, "
-	    "\"tamper_every\": %ld, \"payload_bytes\": %lld, \"bad_record_mac\": %ld, "
+	    "\"tamper_every\": %ld, \"interleave\": %s, \"payload_bytes\": %lld, \"bad_record_mac\": %ld, "
 	    "\"sealed_sha256\": \"%s\", \"opened_sha256\": \"%s\"}\n", name, n, S,
-	    (unsigned long long)seed, tamper, payload, bad, h1, h2);
+	    (unsigned long long)seed, tamper, interleave ? "true" : "false", payload, bad, h1, h2);
 	return 0;
 }

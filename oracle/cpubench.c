@@ -10,7 +10,8 @@
  * (EVP_AEAD_CTX_init) and ciphertext preparation excluded from timing
  * (SURVEY.md §8d "CPU baseline").
  *
- * usage: cpubench LIB AEAD OP REC_LEN NREC THREADS SECONDS
+ * usage: cpubench LIB AEAD OP REC_LEN|@lengths.u32 NREC THREADS SECONDS
+ *   @file: NREC little-endian uint32 record lengths (the config-D Zipf mix)
  *   AEAD: aes-128-gcm | aes-256-gcm | chacha20-poly1305
  *   OP:   open | seal | both  (both = seal then open per record, config C)
  * prints one JSON object.
@@ -40,12 +41,13 @@ struct rec {
 	unsigned char nonce[12], ad[13];
 	unsigned char *ct;	/* ct || tag */
 	unsigned char *pt;
+	size_t len;
 	int sess;
 };
 
 static EVP_AEAD_CTX ctxs[NSESS];
 static struct rec *recs;
-static size_t rec_len, nrec;
+static size_t rec_len, max_len, nrec;
 static int op;	/* 0 open, 1 seal, 2 both */
 static double budget;
 
@@ -87,7 +89,7 @@ static void *
 worker(void *arg)
 {
 	struct targ *t = arg;
-	unsigned char *out = malloc(rec_len + 16);
+	unsigned char *out = malloc(max_len + 16);
 	size_t i = t->lo, out_len;
 	double t0 = now(), t1;
 
@@ -97,16 +99,16 @@ worker(void *arg)
 		int ok = 1;
 		if (op == 0 || op == 2) {
 			if (op == 2)
-				ok &= p_seal(c, out, &out_len, rec_len + 16, r->nonce, 12,
-				    r->pt, rec_len, r->ad, 13);
-			ok &= p_open(c, out, &out_len, rec_len, r->nonce, 12, r->ct,
-			    rec_len + 16, r->ad, 13);
+				ok &= p_seal(c, out, &out_len, r->len + 16, r->nonce, 12,
+				    r->pt, r->len, r->ad, 13);
+			ok &= p_open(c, out, &out_len, r->len, r->nonce, 12, r->ct,
+			    r->len + 16, r->ad, 13);
 		} else {
-			ok &= p_seal(c, out, &out_len, rec_len + 16, r->nonce, 12, r->pt,
-			    rec_len, r->ad, 13);
+			ok &= p_seal(c, out, &out_len, r->len + 16, r->nonce, 12, r->pt,
+			    r->len, r->ad, 13);
 		}
 		t->failures += !ok;
-		t->bytes += rec_len;
+		t->bytes += r->len;
 		t->records++;
 		if (++i == t->hi)
 			i = t->lo;
@@ -160,8 +162,20 @@ main(int argc, char **argv)
 	}
 	aead = which();
 	op = !strcmp(argv[3], "open") ? 0 : !strcmp(argv[3], "seal") ? 1 : 2;
-	rec_len = strtoul(argv[4], NULL, 0);
 	nrec = strtoul(argv[5], NULL, 0);
+	uint32_t *lens = NULL;
+	if (argv[4][0] == '@') {
+		FILE *f = fopen(argv[4] + 1, "rb");
+		lens = malloc(4 * (nrec ? nrec : 1));
+		if (!f || fread(lens, 4, nrec, f) != nrec) {
+			fprintf(stderr, "cannot read %zu lengths from %s\n", nrec, argv[4] + 1);
+			return 2;
+		}
+		fclose(f);
+		rec_len = 0;
+	} else {
+		rec_len = strtoul(argv[4], NULL, 0);
+	}
 	threads = atoi(argv[6]);
 	budget = atof(argv[7]);
 	if (threads < 1 || nrec < (size_t)threads) {
@@ -182,15 +196,18 @@ main(int argc, char **argv)
 		struct rec *r = &recs[k];
 		size_t ol;
 		r->sess = (int)(k % NSESS);
-		r->pt = malloc(rec_len ? rec_len : 1);
-		r->ct = malloc(rec_len + 16);
-		fill(0xC0FFEEULL + k, r->pt, rec_len);
+		r->len = lens ? lens[k] : rec_len;
+		if (r->len > max_len)
+			max_len = r->len;
+		r->pt = malloc(r->len ? r->len : 1);
+		r->ct = malloc(r->len + 16);
+		fill(0xC0FFEEULL + k, r->pt, r->len);
 		fill(0xABCDULL + k, r->nonce, 12);
 		fill(0x1234ULL + k, r->ad, 13);
-		r->ad[11] = (unsigned char)(rec_len >> 8);
-		r->ad[12] = (unsigned char)rec_len;
-		if (!p_seal(&ctxs[r->sess], r->ct, &ol, rec_len + 16, r->nonce, 12,
-		    r->pt, rec_len, r->ad, 13)) {
+		r->ad[11] = (unsigned char)(r->len >> 8);
+		r->ad[12] = (unsigned char)r->len;
+		if (!p_seal(&ctxs[r->sess], r->ct, &ol, r->len + 16, r->nonce, 12,
+		    r->pt, r->len, r->ad, 13)) {
 			fprintf(stderr, "seal failed\n");
 			return 1;
 		}

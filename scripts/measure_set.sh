@@ -1,0 +1,30 @@
+#!/bin/bash
+# Measurement set for a round (run on the GPU box via gpurun):
+#   bench lines: B (metric), B at S = 1 / 65,536 sessions and interleaved, C, D,
+#   the box's copy bandwidth; then PMC passes (scripts/pmc.sh) for B, C and D.
+# usage: scripts/measure_set.sh TAG [--no-pmc]
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=$1
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd $R
+run() {  # name, bench args...
+  local n=$1; shift
+  timeout -k 10 300 python bench.py "$@" > $O/bench_$n.json 2> $O/bench_$n.err
+  local rc=$?
+  echo "bench $n rc=$rc $(cut -c1-200 $O/bench_$n.json)"
+  return $rc
+}
+run copy --mode copy --steps 20 &&
+run B &&
+run B_S1 --sessions 1 --no-cpu-baseline &&
+run B_S65536 --sessions 65536 --no-cpu-baseline &&
+run B_inter1024 --sessions 1024 --interleave --no-cpu-baseline &&
+run C --config C &&
+run D --config D || exit $?
+[ "$2" = "--no-pmc" ] && exit 0
+for c in B C D; do
+  bash scripts/pmc.sh $TAG/pmc$c --config $c || exit $?
+done
+exit 0

@@ -53,7 +53,7 @@ WIRE_RESULT_DTYPE = np.dtype([("first", "<u4"), ("records", "<u4"), ("delivered"
                               ("reserved", "<u4", (2,))])
 assert WIRE_STREAM_DTYPE.itemsize == 32 and WIRE_RESULT_DTYPE.itemsize == 32
 WIRE_FIRST_PACKET = 1
-REC_BAD_MAC, REC_PUBLIC_INVALID, REC_SKIPPED, REC_OVERFLOW = -1, -2, -3, -4
+REC_BAD_MAC, REC_PUBLIC_INVALID, REC_SKIPPED, REC_OVERFLOW, REC_OUT_OF_BOUNDS = -1, -2, -3, -4, -5
 
 RECORD_DTYPE = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("seq", "<u8"),
                          ("session", "<u4"), ("len_type", "<u4")])
@@ -119,8 +119,8 @@ def load_library(path: str = LIBPATH) -> C.CDLL:
         "tlsgpu_sessions_create": (i32, [vp, u32, C.POINTER(vp)]),
         "tlsgpu_sessions_destroy": (None, [vp]),
         "tlsgpu_sessions_install": (i32, [vp, u32, u32, vp]),
-        "tlsgpu_open_batch": (i32, [vp, vp, u32, vp, vp, vp, vp]),
-        "tlsgpu_seal_batch": (i32, [vp, vp, u32, vp, vp, vp, vp]),
+        "tlsgpu_open_batch": (i32, [vp, vp, u32, vp, C.c_size_t, vp, C.c_size_t, vp, vp]),
+        "tlsgpu_seal_batch": (i32, [vp, vp, u32, vp, C.c_size_t, vp, C.c_size_t, vp, vp]),
         "tlsgpu_fill_synthetic": (i32, [vp, vp, u64, u32, u32, u64, u64, vp]),
         "tlsgpu_fill_synthetic_spans": (i32, [vp, vp, vp, vp, u32, u64, u64, vp]),
         "tlsgpu_last_error": (C.c_char_p, []),
@@ -373,18 +373,19 @@ def open_wire(table: "SessionTable", d_streams: int, n_streams: int, d_wire: int
            "tlsgpu_open_wire")
 
 
-def open_batch(table: SessionTable, d_recs: int, n: int, d_in: int, d_out: int,
-               d_status: int, stream: int | None = None) -> None:
-    """Decrypt n device-resident records (tls1_enc(s, 0) per record)."""
-    _check(table.lib.tlsgpu_open_batch(table.handle, d_recs, n, d_in, d_out, d_status, stream),
-           "tlsgpu_open_batch")
+def open_batch(table: SessionTable, d_recs: int, n: int, d_in: int, in_bytes: int, d_out: int,
+               out_bytes: int, d_status: int, stream: int | None = None) -> None:
+    """Decrypt n device-resident records (tls1_enc(s, 0) per record); d_in /
+    d_out hold in_bytes / out_bytes (records outside get REC_OUT_OF_BOUNDS)."""
+    _check(table.lib.tlsgpu_open_batch(table.handle, d_recs, n, d_in, in_bytes, d_out, out_bytes,
+                                       d_status, stream), "tlsgpu_open_batch")
 
 
-def seal_batch(table: SessionTable, d_recs: int, n: int, d_in: int, d_out: int,
-               d_status: int, stream: int | None = None) -> None:
+def seal_batch(table: SessionTable, d_recs: int, n: int, d_in: int, in_bytes: int, d_out: int,
+               out_bytes: int, d_status: int, stream: int | None = None) -> None:
     """Encrypt n device-resident records (tls1_enc(s, 1) per record)."""
-    _check(table.lib.tlsgpu_seal_batch(table.handle, d_recs, n, d_in, d_out, d_status, stream),
-           "tlsgpu_seal_batch")
+    _check(table.lib.tlsgpu_seal_batch(table.handle, d_recs, n, d_in, in_bytes, d_out, out_bytes,
+                                       d_status, stream), "tlsgpu_seal_batch")
 
 
 class _EvpCtx(C.Structure):

@@ -81,8 +81,8 @@ class RecordBatch:
 
     def run(self, table: SessionTable, stream: int | None = None) -> None:
         fn = seal_batch if self.mode == "seal" else open_batch
-        fn(table, self.d_recs.ptr, self.n, self.d_in.ptr, self.d_out.ptr, self.d_status.ptr,
-           stream)
+        fn(table, self.d_recs.ptr, self.n, self.d_in.ptr, self.d_in.nbytes, self.d_out.ptr,
+           self.d_out.nbytes, self.d_status.ptr, stream)
 
     def results(self):
         """[(status, output_bytes)] — output length = status when >= 0, else the

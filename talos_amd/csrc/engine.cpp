@@ -328,8 +328,24 @@ static uint32_t g_pack = []() {
   return v ? (uint32_t)strtoul(v, nullptr, 0) : 1u;
 }();
 
+// Per-wave-session kernel (gcm_pw.hip): env TLSGPU_PWS=0 never, 1 always,
+// unset = automatic (short session runs, tlsgpu_internal.h pws_selected).
+static uint32_t g_pws = []() {
+  const char* v = getenv("TLSGPU_PWS");
+  if (!v || !*v) return 0u;
+  return *v == '0' ? 1u : 2u;
+}();
+
+// bounds: {in_bytes, out_bytes} of a caller's TLS batch (checked by a pre-pass
+// that hands the kernels a sanitized copy of the descriptors), or null for
+// descriptors the engine built itself (raw EVP jobs, wire framing).
+struct Bounds {
+  uint64_t in_bytes, out_bytes;
+};
+
 static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const uint8_t* d_in,
-                     uint8_t* d_out, int32_t* d_status, hipStream_t s, bool seal, bool raw) {
+                     uint8_t* d_out, int32_t* d_status, hipStream_t s, bool seal, bool raw,
+                     const Bounds* bounds = nullptr) {
   BatchArgs a = {};
   a.sessions = t->d_sess;
   a.gcm_tables = t->d_gcm;
@@ -344,23 +360,48 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   a.dbg = g_phase_stats;
   a.bs16_min = g_bs16_min;
   a.pack = g_pack;
+  a.pws = g_pws;
   int groups = groups_for(t->eng, n, &a.records_per_group);
   // records whose session is empty/invalid keep this status
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)d_status, (int)TLSGPU_REC_PUBLIC_INVALID, n, s));
   const int impl = raw ? TLSGPU_GCM_TTABLE : g_gcm_impl.load();
+  const bool gcm_pre =
+      impl != TLSGPU_GCM_TTABLE && (t->have[TLSGPU_AES_128_GCM] || t->have[TLSGPU_AES_256_GCM]);
+  // per-stream scratch: [RecPre x n (queue kernels) | kCtlBytes control words |
+  // checked descriptors x n].  Control words per key size k (0: AES-128, 1:
+  // AES-256): selection words at 16 k, per-workgroup record counters of the
+  // per-wave-session kernel at 1024 (k + 1).
+  constexpr size_t kCtlBytes = 4096;
+  const size_t pre_bytes = gcm_pre ? sizeof(RecPre) * (size_t)n + kCtlBytes : 0;
+  uint8_t* scratch = nullptr;
+  if (pre_bytes || bounds) {
+    scratch = (uint8_t*)pre_scratch(t->eng, s,
+                                    pre_bytes + (bounds ? sizeof(tlsgpu_record) * (size_t)n : 0));
+    if (!scratch) return fail(TLSGPU_ENOMEM, "batch scratch (%u records)", n);
+  }
+  if (bounds) {
+    auto* safe = reinterpret_cast<tlsgpu_record*>(scratch + pre_bytes);
+    if (launch_check_bounds(reinterpret_cast<const tlsgpu_record*>(d_descs), safe, n, t->d_sess,
+                            t->capacity, bounds->in_bytes, bounds->out_bytes, seal, d_status, s))
+      return fail(TLSGPU_EHIP, "bounds launch: %s", hipGetErrorString(hipGetLastError()));
+    a.descs = safe;
+  }
   RecPre* pre = nullptr;  // per-record constants of the queue kernels (per-stream scratch)
-  if (impl != TLSGPU_GCM_TTABLE && (t->have[TLSGPU_AES_128_GCM] || t->have[TLSGPU_AES_256_GCM])) {
-    pre = (RecPre*)pre_scratch(t->eng, s, sizeof(RecPre) * (size_t)n + 256);
-    if (!pre) return fail(TLSGPU_ENOMEM, "RecPre scratch (%u records)", n);
-    if (impl == TLSGPU_GCM_QUEUE && a.pack)  // the prep passes' "packable record" flags
-      HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(pre + n), 0, 2, s));
+  uint8_t* ctl = nullptr;
+  if (gcm_pre) {
+    pre = reinterpret_cast<RecPre*>(scratch);
+    ctl = reinterpret_cast<uint8_t*>(pre + n);
+    if (impl == TLSGPU_GCM_QUEUE) HIPCHK(hipMemsetAsync(ctl, 0, kCtlBytes, s));
   }
   for (int rounds : {10, 14}) {
     if (!t->have[rounds == 10 ? TLSGPU_AES_128_GCM : TLSGPU_AES_256_GCM]) continue;
-    // one flag word per key size: a short AES-128 record must not send the
-    // AES-256 pass to the pack variant
-    if (pre && impl == TLSGPU_GCM_QUEUE && a.pack)
-      a.short_flag = reinterpret_cast<uint32_t*>(pre + n) + (rounds == 10 ? 0 : 1);
+    // selection words and counters per key size: a short AES-128 record must
+    // not send the AES-256 pass to the pack variant
+    if (ctl && impl == TLSGPU_GCM_QUEUE) {
+      const int k = rounds == 10 ? 0 : 1;
+      a.sel = reinterpret_cast<uint32_t*>(ctl + 16 * k);
+      a.wg_next = reinterpret_cast<uint32_t*>(ctl + 1024 * (k + 1));
+    }
     int rc;
     if (impl == TLSGPU_GCM_TTABLE) {
       rc = launch_gcm(a, seal, raw, rounds, groups, s);
@@ -393,25 +434,27 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
 }
 
 extern "C" int tlsgpu_open_batch(tlsgpu_sessions* t, const tlsgpu_record* d_recs, uint32_t n,
-                                 const uint8_t* d_in, uint8_t* d_out, int32_t* d_status,
-                                 void* stream) {
+                                 const uint8_t* d_in, size_t in_bytes, uint8_t* d_out,
+                                 size_t out_bytes, int32_t* d_status, void* stream) {
   if (!t || (n && (!d_recs || !d_in || !d_out || !d_status)))
     return fail(TLSGPU_EINVAL, "bad arguments");
   if (n == 0) return TLSGPU_OK;
   HIPCHK(hipSetDevice(t->eng->device));
+  const Bounds b = {in_bytes, out_bytes};
   return run_batch(t, d_recs, n, d_in, d_out, d_status,
-                   stream ? (hipStream_t)stream : t->eng->stream, false, false);
+                   stream ? (hipStream_t)stream : t->eng->stream, false, false, &b);
 }
 
 extern "C" int tlsgpu_seal_batch(tlsgpu_sessions* t, const tlsgpu_record* d_recs, uint32_t n,
-                                 const uint8_t* d_in, uint8_t* d_out, int32_t* d_status,
-                                 void* stream) {
+                                 const uint8_t* d_in, size_t in_bytes, uint8_t* d_out,
+                                 size_t out_bytes, int32_t* d_status, void* stream) {
   if (!t || (n && (!d_recs || !d_in || !d_out || !d_status)))
     return fail(TLSGPU_EINVAL, "bad arguments");
   if (n == 0) return TLSGPU_OK;
   HIPCHK(hipSetDevice(t->eng->device));
+  const Bounds b = {in_bytes, out_bytes};
   return run_batch(t, d_recs, n, d_in, d_out, d_status,
-                   stream ? (hipStream_t)stream : t->eng->stream, true, false);
+                   stream ? (hipStream_t)stream : t->eng->stream, true, false, &b);
 }
 
 extern "C" int tlsgpu_open_wire(tlsgpu_sessions* t, const tlsgpu_wire_stream* d_streams,

@@ -23,7 +23,11 @@ constexpr uint32_t Q_OFF = R4_OFF + 64;      // hybrid kernel: per-run record qu
 constexpr uint32_t DBG_OFF = Q_OFF + 16;     // hybrid kernel: phase counters (diagnostic)
 constexpr uint32_t PLAN_OFF = DBG_OFF + 32 * 8;  // queue kernel: per-run pack plan
 constexpr uint32_t kPlanCap = 2048;                // records planned per run (runs split)
+#ifdef TG_LDS_BYTES  // a translation unit with its own LDS plan (gcm_pw.hip)
+constexpr uint32_t LDS_BYTES = TG_LDS_BYTES;
+#else
 constexpr uint32_t LDS_BYTES = PLAN_OFF + 4 * kPlanCap;
+#endif
 
 __shared__ __attribute__((aligned(16))) uint8_t s_lds[LDS_BYTES];
 
@@ -246,11 +250,20 @@ __device__ __forceinline__ void aes_ctr16x2(uint32_t ka[4], uint32_t kb[4], uint
 }
 
 // ---------------------------------------------------------------------------
-// GHASH helpers
+// GHASH helpers.  The record code (gcm_blocks*, gcm_finish, gcm_record_x4) is
+// generic in a GHASH policy G with two members:
+//   G::mul64(x, o)      o = x * H^64 (LE words), the per-lane Horner step;
+//   G::shoup(X, e, Z)   Z = X * H^e, e = 1..65 (BE words), the chain weights.
+// GhLane: the session's 64 KiB byte-position table and Shoup tables in LDS,
+// shared by the workgroup (queue kernel, one session per run).  GhNib
+// (gcm_pw.hip): a per-wave 8 KiB nibble-position table and Shoup tables read
+// from HBM/L2 (per-wave-session kernel, any session per wave).
 struct GhLane {
   bool c2, c1;       // word-rotation selects for m = lane % 16
   uint32_t r;        // byte rotation
   uint32_t cq[4];    // slot bytes: cq[q].byte[i] = ((4q + i + m) & 15) * 16
+  __device__ __forceinline__ void mul64(const uint32_t x[4], uint32_t o[4]) const;
+  __device__ __forceinline__ void shoup(const uint32_t X[4], uint32_t e, uint32_t Z[4]) const;
 };
 
 __device__ __forceinline__ GhLane gh_lane(uint32_t lane) {
@@ -381,6 +394,13 @@ __device__ __forceinline__ void mul_shoup(const uint32_t X[4], uint32_t e, uint3
   Z[0] = z0; Z[1] = z1; Z[2] = z2; Z[3] = z3;
 }
 
+__device__ __forceinline__ void GhLane::mul64(const uint32_t x[4], uint32_t o[4]) const {
+  mul_k(x, o, *this);
+}
+__device__ __forceinline__ void GhLane::shoup(const uint32_t X[4], uint32_t e, uint32_t Z[4]) const {
+  mul_shoup(X, e, Z);
+}
+
 // Two independent Shoup multiplies, interleaved; e == 0 gives zero.
 __device__ __forceinline__ void mul_shoup2(const uint32_t A[4], uint32_t ea, uint32_t ZA[4],
                                            const uint32_t B[4], uint32_t eb, uint32_t ZB[4]) {
@@ -493,14 +513,15 @@ struct RecCtx {
 // BE64(ct bits) joins lane (nb % 64)'s chain at j = nb (gcm128.c:1477-1500),
 // then each lane's value still needs the weight H^e, e = nb + 1 - (index of
 // the chain's last element).  Returns the BE chain value and e (0 = empty).
+template <class G>
 __device__ __forceinline__ uint32_t gcm_close_chain(const RecCtx& rc, uint32_t (&x)[4],
                                                     uint32_t (&xb)[4], uint32_t lane,
-                                                    const GhLane& gl) {
+                                                    const G& gl) {
   const uint32_t n = rc.n;
   const uint32_t nb = (n + 15) >> 4;
   const uint32_t lstar = nb & 63;
   uint32_t xk[4];
-  mul_k(x, xk, gl);
+  gl.mul64(x, xk);
   if (lane == lstar) {
     uint64_t ab = rc.aad_len * 8, cb = (uint64_t)n * 8;
     x[0] = xk[0] ^ bswap32((uint32_t)(ab >> 32));
@@ -556,13 +577,13 @@ __device__ __forceinline__ void gcm_tag(const RecCtx& rc, uint32_t (&y)[4], cons
 }
 
 // Finish one record (chains -> weights -> tag).
-template <bool SEAL>
+template <bool SEAL, class G>
 __device__ __forceinline__ void gcm_finish(const RecCtx& rc, uint32_t (&x)[4], const uint32_t ek0[4],
                                            const DevSession* __restrict__ S, int32_t* status_slot,
-                                           uint32_t lane, const GhLane& gl) {
+                                           uint32_t lane, const G& gl) {
   uint32_t xb[4], y[4] = {0, 0, 0, 0};
   const uint32_t e = gcm_close_chain(rc, x, xb, lane, gl);
-  if (e != 0) mul_shoup(xb, e, y);
+  if (e != 0) gl.shoup(xb, e, y);
   gcm_tag<SEAL>(rc, y, ek0, S, status_slot, lane);
 }
 
@@ -585,11 +606,11 @@ __device__ __forceinline__ void gcm_finish2(const RecCtx (&rc)[2], uint32_t (&x)
 // (start is a multiple of 64: block i belongs to lane i % 64's chain).
 // FAST: counters < 2^16 and the per-record constants `rcc` were precomputed
 // (wave-uniform values); otherwise `cc` (ctr_setup) is used.
-template <bool SEAL, int ROUNDS, bool FAST>
+template <bool SEAL, int ROUNDS, bool FAST, class G>
 __device__ __forceinline__ void gcm_blocks(const RecCtx& rc, const DevSession* __restrict__ S,
                                            const RecConsts& rcc, const CtrConst& cc,
                                            uint32_t (&x)[4], uint32_t start, uint32_t lane,
-                                           uint32_t laneoff, const GhLane& gl) {
+                                           uint32_t laneoff, const G& gl) {
   cu32* rk = as_const(S->rk);
   cu32* rkr = as_const(S->rk_rot);
   const uint32_t n = rc.n;
@@ -633,11 +654,11 @@ __device__ __forceinline__ void gcm_blocks(const RecCtx& rc, const DevSession* _
       store_block(rc.dst + 16u * i, 16, aligned, o0);
       store_block(rc.dst + 16u * (i + kWave), 16, aligned, o1);
       uint32_t xk[4];
-      mul_k(x, xk, gl);
+      gl.mul64(x, xk);
       const uint32_t* g0 = SEAL ? o0 : c0;
       const uint32_t* g1 = SEAL ? o1 : c1;
       x[0] = xk[0] ^ g0[0]; x[1] = xk[1] ^ g0[1]; x[2] = xk[2] ^ g0[2]; x[3] = xk[3] ^ g0[3];
-      mul_k(x, xk, gl);
+      gl.mul64(x, xk);
       x[0] = xk[0] ^ g1[0]; x[1] = xk[1] ^ g1[1]; x[2] = xk[2] ^ g1[2]; x[3] = xk[3] ^ g1[3];
 #pragma unroll
       for (int w = 0; w < 4; w++) { c0[w] = n0[w]; c1[w] = n1[w]; }
@@ -665,10 +686,10 @@ __device__ __forceinline__ void gcm_blocks(const RecCtx& rc, const DevSession* _
       store_block(rc.dst + 16u * i0, nb0, aligned, o0);
       if (a1) store_block(rc.dst + 16u * i1, nb1, aligned, o1);
       uint32_t xk[4];
-      mul_k(x, xk, gl);
+      gl.mul64(x, xk);
       const uint32_t* g0 = SEAL ? o0 : in0;
       x[0] = xk[0] ^ g0[0]; x[1] = xk[1] ^ g0[1]; x[2] = xk[2] ^ g0[2]; x[3] = xk[3] ^ g0[3];
-      mul_k(x, xk, gl);
+      gl.mul64(x, xk);
       if (a1) {
         const uint32_t* g1 = SEAL ? o1 : in1;
         x[0] = xk[0] ^ g1[0]; x[1] = xk[1] ^ g1[1]; x[2] = xk[2] ^ g1[2]; x[3] = xk[3] ^ g1[3];
@@ -693,7 +714,7 @@ __device__ __forceinline__ void gcm_blocks(const RecCtx& rc, const DevSession* _
     uint32_t ob[4] = {in[0] ^ ks[0], in[1] ^ ks[1], in[2] ^ ks[2], in[3] ^ ks[3]};
     if (active) store_block(rc.dst + 16u * i, nbytes, aligned, ob);
     uint32_t xk[4];
-    mul_k(x, xk, gl);
+    gl.mul64(x, xk);
     if (active) {
       const uint32_t* c = SEAL ? ob : in;
       x[0] = xk[0] ^ c[0]; x[1] = xk[1] ^ c[1]; x[2] = xk[2] ^ c[2]; x[3] = xk[3] ^ c[3];
@@ -849,11 +870,11 @@ __device__ __forceinline__ void aes_ctr16xN(uint32_t (&ks)[NB][4], const uint32_
 // into the AES rounds of the following group (the chain's LDS round trips then
 // overlap the AES lookups instead of trailing them).  Advances `start` past
 // the groups done; the caller finishes the record with gcm_blocks.
-template <bool SEAL, int ROUNDS, int NB>
+template <bool SEAL, int ROUNDS, int NB, class G>
 __device__ __forceinline__ void gcm_blocks_xN(const RecCtx& rc, const DevSession* __restrict__ S,
                                               const RecConsts& rcc, uint32_t (&x)[4],
                                               uint32_t& start, uint32_t lane, uint32_t laneoff,
-                                              const GhLane& gl) {
+                                              const G& gl) {
   const bool aligned = ((((uintptr_t)rc.src) | ((uintptr_t)rc.dst)) & 15) == 0;
 #ifndef TG_XN_UNALIGNED
   if (!aligned) return;
@@ -870,7 +891,7 @@ __device__ __forceinline__ void gcm_blocks_xN(const RecCtx& rc, const DevSession
   for (int b = 0; b < NB; b++) load_block(rc.src + 16u * (start + kWave * b + lane), 16, aligned, c[b]);
   auto ghash_step = [&](int b) {
     uint32_t xk[4];
-    mul_k(x, xk, gl);
+    gl.mul64(x, xk);
     x[0] = xk[0] ^ gp[b][0]; x[1] = xk[1] ^ gp[b][1]; x[2] = xk[2] ^ gp[b][2]; x[3] = xk[3] ^ gp[b][3];
   };
   // GHASH step b of the previous group after AES round 3 + 2b (all NB steps
@@ -914,10 +935,10 @@ __device__ __forceinline__ void gcm_blocks_xN(const RecCtx& rc, const DevSession
 }
 
 // gcm_record<SEAL, ROUNDS, true> with the NB-wide full-block loop first.
-template <bool SEAL, int ROUNDS, int NB = 4>
+template <bool SEAL, int ROUNDS, int NB = 4, class G = GhLane>
 __device__ void gcm_record_x4(const RecCtx& rc, const DevSession* __restrict__ S,
                               const RecConsts& rcc, int32_t* status_slot, uint32_t lane,
-                              uint32_t laneoff, const GhLane& gl,
+                              uint32_t laneoff, const G& gl,
                               unsigned long long* dbg = nullptr) {
   PhaseClock pc(dbg);
   uint32_t x[4] = {0, 0, 0, 0};
@@ -1077,7 +1098,7 @@ __device__ __forceinline__ void parse_raw(const RawJob& j, const DevSession* __r
 
 // ---------------------------------------------------------------------------
 // Workgroup prologue / session table staging
-template <int NT>
+template <int NT, bool R4 = true>
 __device__ void fill_aes_lds() {
   for (uint32_t t = threadIdx.x; t < 1024; t += NT) {  // 1024 x 64 B = 64 KiB
     const uint32_t row = t >> 2, part = t & 3;
@@ -1088,7 +1109,7 @@ __device__ void fill_aes_lds() {
     dst[0] = w; dst[1] = w; dst[2] = w; dst[3] = w;
   }
   const uint32_t t = threadIdx.x;
-  if (t < 16) {  // rem_4bit >> 32 (gcm128.c:327-331), derived by four x-shifts
+  if (R4 && t < 16) {  // rem_4bit >> 32 (gcm128.c:327-331), derived by four x-shifts
     uint64_t hi = 0, lo = t;
     for (int k = 0; k < 4; k++) {
       uint64_t c = lo & 1;

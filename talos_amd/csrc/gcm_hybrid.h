@@ -490,8 +490,15 @@ template <bool SEAL, int ROUNDS, int NT, int BSW, int NB, bool PACK = false>
 __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
                                                        const RecPre* __restrict__ pre) {
   // pack and no-pack variants are separate kernels (the pack code costs the
-  // long-record loop SGPR spills); the prep pass's flag picks the one that runs
-  if (a.short_flag && (as_const(a.short_flag)[0] != 0) != PACK) return;
+  // long-record loop SGPR spills), and the per-wave-session kernel replaces both
+  // when session runs are short; the prep pass's selection words pick one
+  if (a.sel) {
+    cu32* f = as_const(a.sel);
+    if (pws_selected(a.pws, f[1], f[2])) return;
+    if ((a.pack != 0 && f[0] != 0) != PACK) return;
+  } else if (PACK) {
+    return;
+  }
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t laneoff = (lane & 31) * 4;
@@ -665,12 +672,29 @@ __global__ __launch_bounds__(256) void gcm_prep_kernel(BatchArgs a, RecPre* __re
   te[threadIdx.x] = g_te0.v[threadIdx.x];
   __syncthreads();
   const uint32_t r = blockIdx.x * 256 + threadIdx.x;
-  if (r >= a.n) return;
-  const tlsgpu_record d = reinterpret_cast<const tlsgpu_record*>(a.descs)[r];
-  if (d.session >= a.n_sessions) return;
-  const DevSession* S = a.sessions + d.session;
-  if (!is_gcm(S->kind) || (int)S->rounds != ROUNDS) return;
-  if (a.short_flag && pack_need<SEAL>(d.len_type, S->tag_len) <= kPackMaxNeed) *a.short_flag = 1u;
+  const tlsgpu_record* D = reinterpret_cast<const tlsgpu_record*>(a.descs);
+  // selection words (a.sel): records of this key size and session-run starts
+  // among them, one atomic per wave
+  bool mine = false, run_start = false;
+  tlsgpu_record d = {};
+  const DevSession* S = nullptr;
+  if (r < a.n) {
+    d = D[r];
+    if (d.session < a.n_sessions) {
+      S = a.sessions + d.session;
+      mine = is_gcm(S->kind) && (int)S->rounds == ROUNDS;
+      run_start = mine && (r == 0 || D[r - 1].session != d.session);
+    }
+  }
+  if (a.sel) {
+    const uint64_t m = __ballot(mine), rs = __ballot(run_start);
+    if ((threadIdx.x & 63) == 0 && m) {
+      atomicAdd(a.sel + 2, (uint32_t)__builtin_popcountll(m));
+      atomicAdd(a.sel + 1, (uint32_t)__builtin_popcountll(rs));
+    }
+  }
+  if (!mine) return;
+  if (a.sel && pack_need<SEAL>(d.len_type, S->tag_len) <= kPackMaxNeed) a.sel[0] = 1u;
   auto T0 = [&](uint32_t w, int b) { return te[(w >> (8 * b)) & 0xFF]; };
   auto T1 = [&](uint32_t w, int b) { return rotl32(te[(w >> (8 * b)) & 0xFF], 8); };
   auto SB = [&](uint32_t w, int b) { return (te[(w >> (8 * b)) & 0xFF] >> 8) & 0xFF; };

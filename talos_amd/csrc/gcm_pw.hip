@@ -1,0 +1,223 @@
+// gcm_pw.hip — the per-wave-session AES-GCM TLS kernel.
+//
+// The queue kernel (gcm_hybrid.h) shares one session's 64 KiB GHASH byte table
+// and 16.6 KiB of Shoup tables in LDS across its 16 waves, so it works through
+// a batch one session run at a time with a workgroup barrier between runs.
+// When runs are short — many connections with a few records each, or records
+// of different connections interleaved, as a server's batch arrives — most of
+// the 16 waves idle at every run boundary (1 record per session: 1 busy wave of
+// 16, measured 9x slower).  Here every wave is independent:
+//   * the AES T-tables (64 KiB, session independent) stay shared;
+//   * each of the 12 waves owns an 8 KiB nibble-position table of its current
+//     session's H^64 (T[h][v][p] = nibble v at nibble p of half h, times H^64),
+//     rebuilt from the session's 2 KiB basis (DevGcmTables::basis, L2) when the
+//     wave's next record belongs to another session: 32 conflict-free
+//     ds_read_b128 per Horner step instead of the byte table's 16;
+//   * the chain weights H^1..H^65 come from the session's Shoup tables in HBM
+//     (one 256-B table per lane, L2-resident), the rem_4bit reduction is done
+//     on the VALU (rem * 0xE1 carry-less, gcm128.c:327-331);
+//   * waves pull single records from a per-workgroup counter in global memory.
+// LDS: 64 KiB AES + 12 x 8 KiB = 160 KiB, one 768-thread workgroup per CU.
+#define TG_LDS_BYTES 163840
+#include "gcm_hybrid.h"
+
+namespace tg {
+
+constexpr int kPwThreads = 768;
+constexpr int kPwWaves = kPwThreads / kWave;
+constexpr uint32_t PW_TAB_OFF = 65536;
+constexpr uint32_t PW_TAB_BYTES = 8192;  // 2 halves x 16 values x 16 positions x 16 B
+static_assert(PW_TAB_OFF + kPwWaves * PW_TAB_BYTES <= LDS_BYTES, "per-wave tables exceed LDS");
+
+#ifndef TG_PW_NB
+#define TG_PW_NB 2
+#endif
+#ifndef TG_PW_SHOUP_BATCH
+#define TG_PW_SHOUP_BATCH 16
+#endif
+
+// rem_4bit[r] >> 32 (gcm128.c:327-331) on the VALU: (r * 0xE1, carry-less) << 21,
+// 0xE1 = x^0 + x^5 + x^6 + x^7, so r*0xE1 = r ^ ((r ^ r<<1 ^ r<<2) << 5).
+__device__ __forceinline__ uint32_t rem4(uint32_t r) {
+  const uint32_t a = xor3(r, r << 1, r << 2);
+  return (r << 21) ^ (a << 26);
+}
+
+struct GhNib {
+  uint32_t base;     // LDS byte offset of this wave's table
+  uint32_t sw;       // m >= 8 (m = lane % 16): swap the words of each 64-bit half
+  uint32_t s;        // then rotate each half right by 4 * (m & 7) bits
+  uint32_t cq[4];    // cq[pl].byte[b] = ((k + m) & 15) * 16, k = 8(pl>>1) + 2b + (pl&1)
+  const DevGcmTables* tab;  // the session's tables in HBM
+
+  // o = x * H^64 (LE words).  Half h of x rotated right by m nibbles puts
+  // nibble (k + m) % 16 at nibble k; the nibbles are split into byte planes so
+  // one v_perm forms [0, 0, nibble, position * 16] = the entry's address.
+  // Lanes of a ds_read_b128 lane group have distinct m, so distinct positions,
+  // so distinct quad-banks: conflict-free.
+  __device__ __forceinline__ void mul64(const uint32_t x[4], uint32_t o[4]) const {
+    uint32_t acc[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int h = 0; h < 2; h++) {  // 16 lookups in flight per half
+      const uint32_t lo = x[2 * h], hi = x[2 * h + 1];
+      const uint32_t a = sw ? hi : lo, b = sw ? lo : hi;
+      const uint32_t ylo = __builtin_amdgcn_alignbit(b, a, s);
+      const uint32_t yhi = __builtin_amdgcn_alignbit(a, b, s);
+      const uint32_t pl[4] = {ylo & 0x0F0F0F0Fu, (ylo >> 4) & 0x0F0F0F0Fu, yhi & 0x0F0F0F0Fu,
+                              (yhi >> 4) & 0x0F0F0F0Fu};
+      uint4 v[16];
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++)
+          v[4 * q + bb] = lds_u128(base + 4096u * h +
+                                   __builtin_amdgcn_perm(pl[q], cq[q],
+                                                         0x0C0C0000u | ((4u + bb) << 8) | bb));
+#pragma unroll
+      for (int k = 0; k < 16; k += 2) {
+        acc[0] = xor3(acc[0], v[k].x, v[k + 1].x);
+        acc[1] = xor3(acc[1], v[k].y, v[k + 1].y);
+        acc[2] = xor3(acc[2], v[k].z, v[k + 1].z);
+        acc[3] = xor3(acc[3], v[k].w, v[k + 1].w);
+      }
+    }
+    o[0] = acc[0]; o[1] = acc[1]; o[2] = acc[2]; o[3] = acc[3];
+  }
+
+  // Z = X * H^e (Shoup 4-bit, gcm128.c:333-393), BE words, table from HBM
+  // (L2 after the kernel's prefetch at record start).  The 32 table entries
+  // depend only on X's nibbles: loaded PWS_SHOUP_BATCH at a time ahead of the
+  // serial shift/reduce chain.
+  __device__ __forceinline__ void shoup(const uint32_t X[4], uint32_t e, uint32_t Z[4]) const {
+    constexpr int kB = TG_PW_SHOUP_BATCH;
+    const uint8_t* T = reinterpret_cast<const uint8_t*>(&tab->shoup[e - 1][0][0]);
+    uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+#pragma unroll
+    for (int g = 0; g < 32 / kB; g++) {
+      uint4 m[kB];
+#pragma unroll
+      for (int i = 0; i < kB; i++) {
+        const int k = kB * g + i;
+        const uint32_t nib = (X[3 - k / 8] >> (4 * (k % 8))) & 0xF;
+        m[i] = gload16(T + nib * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < kB; i++) {
+        if (g != 0 || i != 0) {
+          const uint32_t rem = z3 & 0xF;
+          z3 = __builtin_amdgcn_alignbit(z2, z3, 4);
+          z2 = __builtin_amdgcn_alignbit(z1, z2, 4);
+          z1 = __builtin_amdgcn_alignbit(z0, z1, 4);
+          z0 = (z0 >> 4) ^ rem4(rem);
+        }
+        z0 ^= m[i].x; z1 ^= m[i].y; z2 ^= m[i].z; z3 ^= m[i].w;
+      }
+    }
+    Z[0] = z0; Z[1] = z1; Z[2] = z2; Z[3] = z3;
+  }
+
+  // This wave's table for session tables `t` (from basis[q] = H^64 * x^q, LE
+  // words; bit t of the byte at position j is x^(8j + 7 - t), load_session_tables).
+  // Lane l builds position p = l % 16 of half h = (l / 16) % 2, values
+  // 8g .. 8g + 7 with g = l / 32.
+  __device__ __forceinline__ void build(uint32_t lane) const {
+    const uint32_t p = lane & 15, h = (lane >> 4) & 1, g = lane >> 5;
+    const uint32_t i = 16 * h + p, j = i >> 1, sh = 4 * (i & 1);
+    uint4 B[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) B[t] = gload16(&tab->basis[8 * j + 7 - sh - t][0]);
+    const uint32_t m3 = g ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const uint32_t m0 = (u & 1) ? 0xFFFFFFFFu : 0u, m1 = (u & 2) ? 0xFFFFFFFFu : 0u;
+      const uint32_t m2 = (u & 4) ? 0xFFFFFFFFu : 0u;
+      const uint4 e = make_uint4((B[0].x & m0) ^ (B[1].x & m1) ^ (B[2].x & m2) ^ (B[3].x & m3),
+                                 (B[0].y & m0) ^ (B[1].y & m1) ^ (B[2].y & m2) ^ (B[3].y & m3),
+                                 (B[0].z & m0) ^ (B[1].z & m1) ^ (B[2].z & m2) ^ (B[3].z & m3),
+                                 (B[0].w & m0) ^ (B[1].w & m1) ^ (B[2].w & m2) ^ (B[3].w & m3));
+      *reinterpret_cast<uint4*>(s_lds + base + 4096u * h + (8u * g + u) * 256u + p * 16u) = e;
+    }
+    // the wave's own later lookups read what its lanes just wrote
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+};
+
+__device__ __forceinline__ GhNib gh_nib(uint32_t lane, uint32_t base) {
+  GhNib g;
+  const uint32_t m = lane & 15;
+  g.base = base;
+  g.sw = m >> 3;
+  g.s = 4 * (m & 7);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const uint32_t k = 8 * (q >> 1) + 2 * b + (q & 1);
+      v |= (((k + m) & 15u) << 4) << (8 * b);
+    }
+    g.cq[q] = v;
+  }
+  g.tab = nullptr;
+  return g;
+}
+
+template <bool SEAL, int ROUNDS>
+__global__ __launch_bounds__(kPwThreads, 1) void gcm_pw_kernel(BatchArgs a,
+                                                               const RecPre* __restrict__ pre) {
+  cu32* f = as_const(a.sel);
+  if (!pws_selected(a.pws, f[1], f[2])) return;  // the queue kernel runs this batch
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t laneoff = (lane & 31) * 4;
+  const tlsgpu_record* D = reinterpret_cast<const tlsgpu_record*>(a.descs);
+  fill_aes_lds<kPwThreads, false>();
+  __syncthreads();
+  GhNib g = gh_nib(lane, PW_TAB_OFF + wave * PW_TAB_BYTES);
+  const uint32_t rlo = blockIdx.x * a.records_per_group;
+  const uint32_t rhi = min(a.n, rlo + a.records_per_group);
+  uint32_t* next = a.wg_next + blockIdx.x;
+  uint32_t cur = 0xFFFFFFFFu;
+  for (;;) {
+    const uint32_t r = rlo + queue_take(next, 1, lane);
+    if (r >= rhi) break;
+    const tlsgpu_record d = load_desc(D + r);
+    if (d.session >= a.n_sessions) continue;
+    const DevSession* __restrict__ S = a.sessions + d.session;
+    if (!is_gcm(as_const(&S->kind)[0]) || (int)as_const(&S->rounds)[0] != ROUNDS) continue;
+    if (d.session != cur) {
+      g.tab = a.gcm_tables + d.session;
+      g.build(lane);
+      cur = d.session;
+    }
+    RecCtx rc;
+    if (!parse_tls<SEAL>(d, S, a.in, a.out, a.status + r, lane, rc)) continue;
+    // this lane's chain weight H^e, e = 1 + ((nb - lane) mod 64) (gcm_close_chain):
+    // its 256-B Shoup table towards L2 now, read at the record's finish
+    const uint32_t e = 1u + ((((rc.n + 15) >> 4) - lane) & 63u);
+    Prefetch<2> pf;
+    pf.v[0] = *gld<uint32_t>(&g.tab->shoup[e - 1][0][0]);
+    pf.v[1] = *gld<uint32_t>(&g.tab->shoup[e - 1][8][0]);
+    const RecConsts rcc = rec_consts_of(pre + r);
+    gcm_record_x4<SEAL, ROUNDS, TG_PW_NB>(rc, S, rcc, a.status + r, lane, laneoff, g);
+    prefetch_done(pf);
+  }
+}
+
+int launch_gcm_pw(const BatchArgs& a, const RecPre* pre, bool seal, int rounds, int groups,
+                  hipStream_t s) {
+  if (a.n == 0 || !a.sel || !a.wg_next) return 0;
+  const dim3 g(groups), b(kPwThreads);
+  if (rounds == 10) {
+    if (seal) hipLaunchKernelGGL((gcm_pw_kernel<true, 10>), g, b, 0, s, a, pre);
+    else hipLaunchKernelGGL((gcm_pw_kernel<false, 10>), g, b, 0, s, a, pre);
+  } else {
+    if (seal) hipLaunchKernelGGL((gcm_pw_kernel<true, 14>), g, b, 0, s, a, pre);
+    else hipLaunchKernelGGL((gcm_pw_kernel<false, 14>), g, b, 0, s, a, pre);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace tg

@@ -33,7 +33,7 @@ int launch_gcm_queue(const BatchArgs& a, const RecPre* pre, bool seal, int round
     if (seal) hipLaunchKernelGGL((gcm_hy_kernel<true, 14, 1024, 0, TG_QUEUE_NB>), g, b, 0, s, a, pre);
     else hipLaunchKernelGGL((gcm_hy_kernel<false, 14, 1024, 0, TG_QUEUE_NB>), g, b, 0, s, a, pre);
   }
-  if (a.short_flag) {  // the pack variant: runs instead when the prep pass saw a short record
+  if (a.sel) {  // the pack variant: runs instead when the prep pass saw a short record
     if (rounds == 10) {
       if (seal) hipLaunchKernelGGL((gcm_hy_kernel<true, 10, 1024, 0, TG_QUEUE_NB, true>), g, b, 0, s, a, pre);
       else hipLaunchKernelGGL((gcm_hy_kernel<false, 10, 1024, 0, TG_QUEUE_NB, true>), g, b, 0, s, a, pre);
@@ -42,6 +42,8 @@ int launch_gcm_queue(const BatchArgs& a, const RecPre* pre, bool seal, int round
       else hipLaunchKernelGGL((gcm_hy_kernel<false, 14, 1024, 0, TG_QUEUE_NB, true>), g, b, 0, s, a, pre);
     }
   }
+  if (a.sel && a.pws != 1 && hipGetLastError() == hipSuccess)  // per-wave sessions (gcm_pw.hip)
+    return launch_gcm_pw(a, pre, seal, rounds, groups, s);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -222,6 +222,43 @@ int launch_fill_synthetic_spans(uint8_t* d_out, const uint64_t* d_offs, const ui
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// Batch ABI bounds (tlsgpu_open_batch / _seal_batch take the sizes of d_in and
+// d_out): a record whose input or output span leaves its buffer is dropped
+// from the kernels' copy of the descriptors (session 0xFFFFFFFF, which every
+// batch kernel skips) and gets TLSGPU_REC_OUT_OF_BOUNDS.  Output span = the
+// plaintext on open (fragment - explicit nonce - tag), the fragment on seal.
+__global__ void check_record_bounds(const tlsgpu_record* __restrict__ recs,
+                                    tlsgpu_record* __restrict__ safe, uint32_t n,
+                                    const DevSession* __restrict__ sessions, uint32_t n_sessions,
+                                    uint64_t in_bytes, uint64_t out_bytes, int seal,
+                                    int32_t* __restrict__ status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  tlsgpu_record r = recs[i];
+  if (r.session < n_sessions) {
+    const DevSession& S = sessions[r.session];
+    const uint64_t eiv = S.nonce_in_record ? 8u : 0u, tag = S.tag_len;
+    const uint64_t len = r.len_type & 0xFFFFFFu;
+    const uint64_t in_len = len;
+    const uint64_t out_len = seal ? len + eiv + tag : (len >= eiv + tag ? len - eiv - tag : 0);
+    if (r.in_off > in_bytes || in_len > in_bytes - r.in_off || r.out_off > out_bytes ||
+        out_len > out_bytes - r.out_off) {
+      r.session = 0xFFFFFFFFu;
+      status[i] = TLSGPU_REC_OUT_OF_BOUNDS;
+    }
+  }
+  safe[i] = r;
+}
+
+int launch_check_bounds(const tlsgpu_record* recs, tlsgpu_record* safe, uint32_t n,
+                        const DevSession* sessions, uint32_t n_sessions, uint64_t in_bytes,
+                        uint64_t out_bytes, bool seal, int32_t* status, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(check_record_bounds, dim3((n + 255) / 256), dim3(256), 0, s, recs, safe, n,
+                     sessions, n_sessions, in_bytes, out_bytes, seal ? 1 : 0, status);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_session_install(DevSession* sessions, DevGcmTables* tables,
                            const tlsgpu_session_params* d_params, uint32_t first, uint32_t n,
                            hipStream_t s) {

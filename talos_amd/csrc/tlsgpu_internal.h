@@ -154,10 +154,24 @@ struct BatchArgs {
                                     // aligned) take the packed bitsliced path; 0 = never
   uint32_t pack;                    // queue kernel: short records of one session share a
                                     // wave (gcm_pack); 0 = off
-  uint32_t* short_flag;             // set by the prep pass when a record can be packed; the
-                                    // queue kernel's pack / no-pack variants both launch and
-                                    // the one that does not match returns (null: no flag)
+  uint32_t* sel;                    // queue impl: 4 selection words of this key size, filled
+                                    // by the prep pass: [0] a record can be packed, [1] session
+                                    // runs (records whose session differs from the previous
+                                    // record's), [2] records.  The queue kernel's no-pack / pack
+                                    // variants and the per-wave-session kernel all launch; the
+                                    // ones the words do not select return (null: queue no-pack)
+  uint32_t pws;                     // per-wave-session kernel: 0 auto (runs shorter than
+                                    // kPwsRun records on average), 1 never, 2 always
+  uint32_t* wg_next;                // per-wave-session kernel: one record counter per workgroup
 };
+
+// Average session-run length below which the per-wave-session kernel (gcm_pw.hip)
+// replaces the queue kernel: a run shorter than the workgroup's wave count leaves
+// waves idle at the run barrier.
+constexpr uint32_t kPwsRun = 12;
+__host__ __device__ __forceinline__ bool pws_selected(uint32_t mode, uint32_t runs, uint32_t recs) {
+  return mode == 2 || (mode == 0 && runs * kPwsRun > recs);
+}
 
 // Per-record constants of the hybrid kernel (gcm_prep_kernel, one per record,
 // 48 B in a stream-ordered scratch buffer; read back with s_load).  All in the
@@ -179,6 +193,8 @@ int launch_gcm(const BatchArgs& a, bool seal, bool raw, int rounds, int groups,
 int launch_gcm_prep(const BatchArgs& a, RecPre* pre, bool seal, int rounds, hipStream_t s);
 int launch_gcm_queue(const BatchArgs& a, const RecPre* pre, bool seal, int rounds, int groups,
                      hipStream_t s);
+int launch_gcm_pw(const BatchArgs& a, const RecPre* pre, bool seal, int rounds, int groups,
+                  hipStream_t s);
 int launch_gcm_hy10(const BatchArgs& a, const RecPre* pre, bool seal, int bs_waves, int groups,
                     hipStream_t s);
 int launch_gcm_fused10(const BatchArgs& a, const RecPre* pre, bool seal, int groups, hipStream_t s);
@@ -199,6 +215,9 @@ int launch_wire_finish(uint32_t n_streams, tlsgpu_wire_result* results, int32_t*
                        hipStream_t s);
 int launch_fill_synthetic(uint8_t* d_out, uint64_t stride, uint32_t span_len,
                           uint32_t n, uint64_t seed, uint64_t index0, hipStream_t s);
+int launch_check_bounds(const tlsgpu_record* recs, tlsgpu_record* safe, uint32_t n,
+                        const DevSession* sessions, uint32_t n_sessions, uint64_t in_bytes,
+                        uint64_t out_bytes, bool seal, int32_t* status, hipStream_t s);
 int launch_fill_synthetic_spans(uint8_t* d_out, const uint64_t* d_offs, const uint32_t* d_lens,
                                 uint32_t n, uint64_t seed, uint64_t index0, hipStream_t s);
 }  // namespace tg

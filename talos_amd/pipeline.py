@@ -50,8 +50,8 @@ class HostPipeline:
             lo, hi = self.body_lo[k], min(self.body_hi[k], wl.body_bytes)
             _check(lib.tlsgpu_memcpy(eng.handle, wl.d_body.ptr + lo, self.h_body.value + lo,
                                      hi - lo, s), "H2D")
-            open_batch(wl.table, wl.d_open.ptr + 32 * a, b - a, wl.d_body.ptr, wl.d_out.ptr,
-                       wl.d_status.ptr + 4 * a, s)
+            open_batch(wl.table, wl.d_open.ptr + 32 * a, b - a, wl.d_body.ptr, wl.d_body.nbytes,
+                       wl.d_out.ptr, wl.d_out.nbytes, wl.d_status.ptr + 4 * a, s)
             olo, ohi = self.out_lo[k], self.out_hi[k]
             _check(lib.tlsgpu_memcpy(eng.handle, self.h_out.value + olo, wl.d_out.ptr + olo,
                                      ohi - olo, s), "D2H")

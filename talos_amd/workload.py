@@ -50,9 +50,13 @@ def zipf_lengths(n: int, seed: int, lo: int = 64, hi: int = 16384, alpha: float 
     return rng.choice(ls, size=n, p=p).astype(np.int64)
 
 
-def session_plan(kind: int, n_records: int, n_sessions: int, seed: int):
+def session_plan(kind: int, n_records: int, n_sessions: int, seed: int,
+                 interleave: bool = False):
     """(session params, start seqs, per-record session, per-record seq) of a
-    workload; oracle/batch_digest.c restates the same rule in C."""
+    workload; oracle/batch_digest.c restates the same rule in C.  Records are
+    grouped by session (record r -> session r // (R / S)), or with
+    `interleave` dealt round-robin (r -> r % S, the k-th record of a session
+    has seq start + k) as a many-connection server batch would arrive."""
     params, start_seq = [], []
     for s in range(n_sessions):
         key = fill_bytes(seed ^ KEY_TAG, s, KEY_LEN[kind])
@@ -65,10 +69,15 @@ def session_plan(kind: int, n_records: int, n_sessions: int, seed: int):
         elif s % 7 == 2:
             sq = (sq | 0xFFFFFFFF) - 5
         start_seq.append(sq & M64)
-    per = max(1, n_records // n_sessions)
     r = np.arange(n_records, dtype=np.int64)
-    session = np.minimum(r // per, n_sessions - 1).astype(np.uint32)
-    seq = np.array(start_seq, dtype=np.uint64)[session] + (r % per).astype(np.uint64)
+    if interleave:
+        session = (r % n_sessions).astype(np.uint32)
+        k = r // n_sessions
+    else:
+        per = max(1, n_records // n_sessions)
+        session = np.minimum(r // per, n_sessions - 1).astype(np.uint32)
+        k = r % per
+    seq = np.array(start_seq, dtype=np.uint64)[session] + k.astype(np.uint64)
     return params, start_seq, session, seq
 
 
@@ -81,7 +90,8 @@ class Workload:
     """
 
     def __init__(self, engine, kind: int, n_records: int, n_sessions: int, seed: int,
-                 lengths=None, record_len: int = 16384, index0: int = 0, tamper_every: int = 0):
+                 lengths=None, record_len: int = 16384, index0: int = 0, tamper_every: int = 0,
+                 interleave: bool = False):
         self.engine = engine
         self.kind = kind
         self.n = n_records
@@ -100,7 +110,7 @@ class Workload:
 
         # sessions, record -> session map and sequence numbers
         self.params, self.start_seq, self.session, self.seq = session_plan(
-            kind, n_records, n_sessions, seed)
+            kind, n_records, n_sessions, seed, interleave)
         self.table = SessionTable(engine, n_sessions)
         self.table.install(0, self.params)
         self.rtype = np.full(n_records, 23, dtype=np.uint32)
@@ -188,12 +198,12 @@ class Workload:
         return h.hexdigest()
 
     def seal(self, stream=None):
-        seal_batch(self.table, self.d_seal.ptr, self.n, self.d_pt.ptr, self.d_body.ptr,
-                   self.d_status.ptr, stream)
+        seal_batch(self.table, self.d_seal.ptr, self.n, self.d_pt.ptr, self.d_pt.nbytes,
+                   self.d_body.ptr, self.d_body.nbytes, self.d_status.ptr, stream)
 
     def open(self, stream=None):
-        open_batch(self.table, self.d_open.ptr, self.n, self.d_body.ptr, self.d_out.ptr,
-                   self.d_status.ptr, stream)
+        open_batch(self.table, self.d_open.ptr, self.n, self.d_body.ptr, self.d_body.nbytes,
+                   self.d_out.ptr, self.d_out.nbytes, self.d_status.ptr, stream)
 
     def status(self) -> np.ndarray:
         return self.d_status.download().view(np.int32)[:self.n]

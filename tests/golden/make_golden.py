@@ -143,11 +143,15 @@ BATCHES = {
     # session-count sensitivity: one session, one record per session
     "B_S1": ("aes-128-gcm", 65536, 1, 0x5EED0001, 1024, 16384),
     "B_Sn": ("aes-128-gcm", 65536, 65536, 0x5EED0001, 1024, 16384),
+    # records of 1,024 connections interleaved (a many-connection server batch)
+    "B_inter": ("aes-128-gcm", 65536, 1024, 0x5EED0001, 1024, 16384, "interleave"),
+    "D_inter": ("aes-256-gcm", 1 << 18, 8192, 0x5EED0003, 1024, "zipf", "interleave"),
     # small batches the CPU restatement re-derives in seconds (tests/test_oracle_kat.py)
     "B_small": ("aes-128-gcm", 96, 8, 0x5EED0001, 16, 16384),
     "C_small": ("chacha20-poly1305", 512, 32, 0x5EED0002, 64, 1400),
     "D_small": ("aes-256-gcm", 256, 16, 0x5EED0003, 32, "zipf"),
     "old_small": ("chacha20-poly1305-old", 128, 8, 0x5EED0005, 16, 1000),
+    "inter_small": ("aes-256-gcm", 200, 7, 0x5EED0006, 16, "zipf", "interleave"),
 }
 
 
@@ -160,7 +164,7 @@ def make_batch_digests():
     from talos_amd.workload import zipf_lengths
     exe = os.path.join(ROOT, "oracle", "_ref", "batch_digest")
     out = {}
-    for name, (aead, n, S, seed, tamper, ln) in BATCHES.items():
+    for name, (aead, n, S, seed, tamper, ln, *order) in BATCHES.items():
         with tempfile.NamedTemporaryFile(suffix=".u32") as f:
             if ln == "zipf":
                 f.write(zipf_lengths(n, seed).astype(np.uint32).tobytes())
@@ -168,7 +172,7 @@ def make_batch_digests():
                 arg = "@" + f.name
             else:
                 arg = str(ln)
-            r = subprocess.run([exe, aead, str(n), str(S), hex(seed), str(tamper), arg],
+            r = subprocess.run([exe, aead, str(n), str(S), hex(seed), str(tamper), arg] + order,
                                check=True, capture_output=True, text=True)
         d = json.loads(r.stdout)
         d["lengths"] = ln

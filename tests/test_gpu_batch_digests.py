@@ -42,7 +42,8 @@ def _batches():
     return json.load(open(os.path.join(GOLD, "batch_digests.json")))["batches"]
 
 
-@pytest.mark.parametrize("name", ["B", "C", "D", "B_S1", "B_Sn", "old_small", "D_small"])
+@pytest.mark.parametrize("name", ["B", "C", "D", "B_S1", "B_Sn", "B_inter", "D_inter", "old_small",
+                                  "D_small", "inter_small"])
 def test_batch_digest_matches_reference(ta, engine, name):
     from talos_amd.workload import Workload, zipf_lengths
     d = _batches()[name]
@@ -50,7 +51,7 @@ def test_batch_digest_matches_reference(ta, engine, name):
     n, S, seed, te = d["records"], d["sessions"], d["seed"], d["tamper_every"]
     zipf = d["lengths"] == "zipf"
     wl = Workload(engine, kind, n, S, seed, lengths=zipf_lengths(n, seed) if zipf else None,
-                  record_len=0 if zipf else d["lengths"])
+                  record_len=0 if zipf else d["lengths"], interleave=d.get("interleave", False))
     try:
         assert int(wl.lengths.sum()) == d["payload_bytes"]
         assert wl.sealed_digest() == d["sealed_sha256"], "sealed bodies differ from the reference"

@@ -417,3 +417,66 @@ def test_batch_packs_disabled_env(ta):
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=100,
                        env=env, cwd=ROOT)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("mode", ["seal", "open"])
+def test_batch_bounds(ta, engine, oracle, mode):
+    """tlsgpu_open/seal_batch take the buffer sizes: a record whose input or
+    output span leaves its buffer gets REC_OUT_OF_BOUNDS and nothing of it is
+    written; the other records of the batch are unaffected."""
+    import numpy as np
+    from talos_amd.batch import RecordBatch
+    rnd = random.Random(77)
+    kinds = [po.AES_128_GCM, po.CHACHA20_POLY1305]
+    params = _mk_sessions(ta, rnd, kinds)
+    table = ta.SessionTable(engine, 2)
+    table.install(0, params)
+    osess = _oracle_sessions(oracle, params)
+    pts = [bytes(rnd.getrandbits(8) for _ in range(n)) for n in (100, 2000, 16384, 77)]
+    recs = [(i % 2, 5 + i, 23, pt, kinds[i % 2]) for i, pt in enumerate(pts)]
+    if mode == "open":
+        recs = [(sid, seq, rt, oracle.tls_seal(osess[sid], seq, rt, pt), k)
+                for sid, seq, rt, pt, k in recs]
+    b = RecordBatch(engine, recs, mode)
+    descs = b.d_recs.download().view(ta.RECORD_DTYPE).copy()
+    descs[1]["in_off"] = b.d_in.nbytes - 10             # input runs past d_in
+    descs[2]["out_off"] = b.d_out.nbytes - 100          # output runs past d_out
+    descs[3]["in_off"] = (1 << 63) + 5                  # offset overflow
+    b.d_recs.upload(descs.view(np.uint8))
+    b.run(table)
+    res = b.results()
+    assert [s for s, _ in res[1:]] == [ta.REC_OUT_OF_BOUNDS] * 3
+    sid, seq, rt, payload, _ = recs[0]
+    want = (oracle.tls_seal(osess[sid], seq, rt, payload) if mode == "seal" else pts[0])
+    assert res[0] == (len(want), want)
+    out = b.d_out.download()
+    for i in (1, 2, 3):   # untouched output regions keep the 0xA5 fill
+        o = int(descs[i]["out_off"]) if i != 2 else None
+        if o is not None and o < len(out):
+            assert (out[o:o + 32] == 0xA5).all()
+    assert (out[-100:] == 0xA5).all()
+    table.close()
+
+
+def test_batch_per_wave_session_kernel_forced(ta):
+    """TLSGPU_PWS=1: every queue-impl GCM batch runs on the per-wave-session
+    kernel (gcm_pw.hip: per-wave nibble GHASH tables, Shoup weights from HBM,
+    no session runs) — the full length matrix, misaligned and in-place
+    buffers, short records, interleaved sessions of mixed kinds and tamper
+    zero-fill, against the oracle, in a child process with the variable set."""
+    import subprocess
+    code = ("import sys; sys.path[:0] = [%r, %r]\n"
+            "import test_gpu_parity as t, pyoracle as po, talos_amd as ta\n"
+            "ta.load_library(); e = ta.Engine(0); o = po.Oracle()\n"
+            "for k in (po.AES_128_GCM, po.AES_256_GCM):\n"
+            "    t._run_seal_open(ta, e, o, [k] * 3, t.LENGTHS, seed=51)\n"
+            "    t._run_seal_open(ta, e, o, [k] * 2, t.BS_LENGTHS, seed=52, in_shift=3, out_shift=5)\n"
+            "    t._run_seal_open(ta, e, o, [k] * 2, t.PACK_LENGTHS, seed=53, in_place=True)\n"
+            "    t._run_seal_open(ta, e, o, [k] * 7, [1, 17, 300, 1400, 5000, 16384], grouped=False, seed=54)\n"
+            "t._run_seal_open(ta, e, o, [po.AES_128_GCM, po.AES_256_GCM, po.CHACHA20_POLY1305,\n"
+            "                 po.AES_256_GCM, po.AES_128_GCM], [0, 33, 999, 16384], grouped=False, seed=55)\n"
+            "e.close(); print('ok')\n") % (os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle"))
+    env = dict(os.environ, TLSGPU_PWS="1", TLSGPU_GCM_IMPL="queue")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=110,
+                       env=env, cwd=ROOT)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]

@@ -126,7 +126,7 @@ def test_batch_digests_oracle(oracle, name):
     n, S, seed, te = d["records"], d["sessions"], d["seed"], d["tamper_every"]
     lengths = (zipf_lengths(n, seed) if d["lengths"] == "zipf"
                else np.full(n, d["lengths"], dtype=np.int64))
-    params, _, session, seq = session_plan(kind, n, S, seed)
+    params, _, session, seq = session_plan(kind, n, S, seed, d.get("interleave", False))
     sess = [oracle.tls_session(kind, p.key, p.fixed_iv) for p in params]
     oracle.lib.oracle_fill_bytes.argtypes = [C.c_uint64, C.c_uint64, C.c_void_p, C.c_size_t]
     eiv = 8 if kind in (po.AES_128_GCM, po.AES_256_GCM) else 0
