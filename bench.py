@@ -163,7 +163,9 @@ def main():
                     help="deal records to sessions round-robin (a many-connection server "
                          "batch) instead of grouping each session's records")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", default="device", choices=["device", "host", "wire", "copy"],
+    ap.add_argument("--host-streams", type=int, default=0, help="host mode: pipeline streams")
+    ap.add_argument("--host-chunk-mib", type=int, default=0, help="host mode: chunk size")
+    ap.add_argument("--mode", default="device", choices=["device", "host", "wire", "copy", "pcie"],
                     help="host: pinned host buffers + H2D/D2H overlap (PCIe-inclusive rate); "
                          "wire: raw TLS wire streams through tlsgpu_open_wire (framing + "
                          "in-place open, SURVEY.md §8f-1); copy: the box's achievable "
@@ -179,6 +181,8 @@ def main():
     eng = ta.Engine(device_for(local, ta.device_count()))  # first GPU runtime user
     if args.mode == "copy":
         return copy_mode(args, eng)
+    if args.mode == "pcie":
+        return pcie_mode(args, eng)
     cp = ControlPlane(world)   # gloo control plane: barrier + max over ranks only
 
     kind_name, per_gpu, sessions, rec_len, seed, op = CONFIGS[args.config]
@@ -330,28 +334,74 @@ def copy_mode(args, eng):
 
 
 def host_mode(args, eng, wl, kind_name, total_len):
-    """PCIe-inclusive rate: pinned host fragments in, pinned host plaintext out."""
+    """PCIe-inclusive rate (north_star: the path starts and ends in host memory):
+    pinned host fragments in, pinned host plaintext out, through the C-ABI
+    tlsgpu_open_host (chunked multi-stream H2D / kernel / D2H pipeline)."""
     import talos_amd as ta
     from talos_amd.pipeline import HostPipeline
+    if args.host_streams or args.host_chunk_mib:
+        ta.host_pipeline(eng, args.host_streams, args.host_chunk_mib << 20)
     pipe = HostPipeline(wl)
     for _ in range(max(1, args.warmup)):
         pipe.run()
-    wl.verify_open()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         pipe.run()
     dt = time.perf_counter() - t0
-    for i in (0, wl.n // 2, wl.n - 1):
-        if not wl.tampered[i]:
-            assert pipe.host_plaintext(i) == wl.d_pt.download(int(wl.lengths[i]),
-                                                              int(wl.pt_off[i])).tobytes()
+    # every status exact; sampled plaintexts equal the originals, tampered zeroed
+    st = pipe.status()
+    want = np.where(wl.tampered, -1, wl.lengths).astype(np.int32)
+    assert np.array_equal(st, want), int((st != want).sum())
+    rng = np.random.default_rng(1)
+    for i in list(rng.choice(wl.n, 32, replace=False)) + list(np.nonzero(wl.tampered)[0][:4]):
+        got = pipe.host_plaintext(int(i))
+        exp = (bytes(int(wl.lengths[i])) if wl.tampered[i] else
+               wl.d_pt.download(int(wl.lengths[i]), int(wl.pt_off[i])).tobytes())
+        assert got == exp, i
     print(json.dumps({"metric": f"GiB/s host-resident {kind_name} TLS record open "
-                                "(pinned H2D + kernel + D2H, 4 streams, 32 chunks)",
+                                "(tlsgpu_open_host: pinned H2D + kernels + D2H, pipelined)",
                       "value": round(total_len * args.steps / dt / GIB, 3), "unit": "GiB/s",
                       "steps": args.steps, "records": wl.n,
-                      "ms_per_step": round(dt * 1e3 / args.steps, 3)}), flush=True)
+                      "h2d_bytes_per_step": wl.body_bytes, "d2h_bytes_per_step": wl.pt_bytes,
+                      "ms_per_step": round(dt * 1e3 / args.steps, 3),
+                      "compute_streams": args.host_streams or 2, "chunk_mib": args.host_chunk_mib or 32,
+                      "timing": "wall clock around each synchronous tlsgpu_open_host call"}),
+          flush=True)
     pipe.close()
     wl.free()
+    eng.close()
+
+
+def pcie_mode(args, eng):
+    """Raw pinned-host <-> HBM copy rates of this box (the ceiling of --mode host):
+    1 GiB H2D alone, D2H alone, and both at once on two streams."""
+    import ctypes as C
+    import talos_amd as ta
+    lib = eng.lib
+    nbytes = 1 << 30
+    h1, h2 = C.c_void_p(), C.c_void_p()
+    ta._check(lib.tlsgpu_host_alloc(eng.handle, nbytes, C.byref(h1)), "host_alloc")
+    ta._check(lib.tlsgpu_host_alloc(eng.handle, nbytes, C.byref(h2)), "host_alloc")
+    d1, d2 = ta.DeviceBuffer(eng, nbytes), ta.DeviceBuffer(eng, nbytes)
+    s1, s2 = eng.new_stream(), eng.new_stream()
+    C.memset(h1, 0x5A, nbytes)
+    res = {}
+    for name, jobs in (("h2d", [(d1.ptr, h1.value, s1)]), ("d2h", [(h2.value, d2.ptr, s2)]),
+                       ("both", [(d1.ptr, h1.value, s1), (h2.value, d2.ptr, s2)])):
+        for rep in range(2):
+            t0 = time.perf_counter()
+            for dst, src, s in jobs:
+                ta._check(lib.tlsgpu_memcpy(eng.handle, dst, src, nbytes, s), "memcpy")
+            for _, _, s in jobs:
+                eng.sync_stream(s)
+            dt = time.perf_counter() - t0
+        res[name + "_GBps"] = round(len(jobs) * nbytes / dt / 1e9, 2)
+    print(json.dumps({"metric": "pinned host <-> HBM copy rate (hipMemcpyAsync, 1 GiB)", **res}),
+          flush=True)
+    lib.tlsgpu_host_free(eng.handle, h1)
+    lib.tlsgpu_host_free(eng.handle, h2)
+    d1.free()
+    d2.free()
     eng.close()
 
 

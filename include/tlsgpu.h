@@ -139,6 +139,30 @@ int tlsgpu_seal_batch(tlsgpu_sessions *t, const tlsgpu_record *d_recs, uint32_t 
     void *stream);
 
 /* ---------------------------------------------------------------------------
+ * Host-resident batch open: records that start and end in
+ * host memory, as socket buffers do.  Replaces, for a batch of connections,
+ * ssl3_read_n's BIO_read into rbuf (ssl/s3_pkt.c:134-267), tls1_enc(s, 0)
+ * and the copy of the plaintext to the application buffer (s3_pkt.c:957).
+ *
+ * h_recs / h_in / h_out / h_status are HOST pointers (pinned memory from
+ * tlsgpu_host_alloc for full PCIe rate; pageable memory works, slower).
+ * Descriptor offsets are relative to h_in / h_out exactly as for
+ * tlsgpu_open_batch; h_out == h_in opens in place.  The engine mirrors the
+ * buffers in HBM and pipelines the batch in chunks (H2D of chunk k+1 and D2H
+ * of chunk k-1 on their own streams overlap the kernels of chunk k) when
+ * the records' in_off and out_off ascend with the record index; otherwise it
+ * runs the batch as one chunk.  Synchronous: returns when h_out and h_status
+ * are final.  Bytes of h_out outside the records' plaintext spans are
+ * unspecified afterwards (in place: the headers, explicit nonces and tags are
+ * written back unchanged). */
+int tlsgpu_open_host(tlsgpu_sessions *t, const tlsgpu_record *h_recs, uint32_t n,
+    const uint8_t *h_in, size_t in_bytes, uint8_t *h_out, size_t out_bytes, int32_t *h_status);
+/* Pipeline shape of tlsgpu_open_host: `streams` compute streams (1..8, default
+ * 2; copies in and out have a stream each), chunks of about `chunk_bytes`
+ * input bytes (default 32 MiB). */
+int tlsgpu_host_pipeline(tlsgpu_engine *e, unsigned streams, size_t chunk_bytes);
+
+/* ---------------------------------------------------------------------------
  * Wire-record framing: ssl3_get_record (ssl/s3_pkt.c:279-495)
  * for the AEAD suites over raw read-ahead bytes, many connections at once.
  *

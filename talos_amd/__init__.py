@@ -129,6 +129,8 @@ def load_library(path: str = LIBPATH) -> C.CDLL:
         "tlsgpu_aes_ecb_bitsliced": (i32, [vp, u32, vp, vp, u32, vp]),
         "tlsgpu_debug_phase_stats": (i32, [vp, C.POINTER(C.c_ulonglong), i32]),
         "tlsgpu_open_wire": (i32, [vp, vp, u32, vp, u32, vp, vp, vp, vp, vp]),
+        "tlsgpu_open_host": (i32, [vp, vp, u32, vp, C.c_size_t, vp, C.c_size_t, vp]),
+        "tlsgpu_host_pipeline": (i32, [vp, C.c_uint, C.c_size_t]),
         "tlsgpu_evp_set_batching": (i32, [C.c_uint, C.c_uint, C.c_uint]),
         "tlsgpu_evp_batch_stats": (i32, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "tlsgpu_evp_call_stats": (i32, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
@@ -379,6 +381,20 @@ def open_batch(table: SessionTable, d_recs: int, n: int, d_in: int, in_bytes: in
     d_out hold in_bytes / out_bytes (records outside get REC_OUT_OF_BOUNDS)."""
     _check(table.lib.tlsgpu_open_batch(table.handle, d_recs, n, d_in, in_bytes, d_out, out_bytes,
                                        d_status, stream), "tlsgpu_open_batch")
+
+
+def open_host(table: SessionTable, h_recs: int, n: int, h_in: int, in_bytes: int, h_out: int,
+              out_bytes: int, h_status: int) -> None:
+    """Host-resident batch open (tlsgpu_open_host): host descriptors, fragments,
+    plaintext and statuses; synchronous, pipelined over several HIP streams."""
+    _check(table.lib.tlsgpu_open_host(table.handle, h_recs, n, h_in, in_bytes, h_out, out_bytes,
+                                      h_status), "tlsgpu_open_host")
+
+
+def host_pipeline(engine: "Engine", streams: int = 0, chunk_bytes: int = 0) -> None:
+    """Shape of the tlsgpu_open_host pipeline (0 = keep)."""
+    _check(engine.lib.tlsgpu_host_pipeline(engine.handle, streams, chunk_bytes),
+           "tlsgpu_host_pipeline")
 
 
 def seal_batch(table: SessionTable, d_recs: int, n: int, d_in: int, in_bytes: int, d_out: int,

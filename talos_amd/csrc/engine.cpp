@@ -63,12 +63,29 @@ struct PreScratch {
   size_t cap = 0;
 };
 
+// Host-resident pipeline state (tlsgpu_open_host): HBM mirrors of the host
+// buffers (grow-only), a copy-in stream, `nstreams` compute streams and a
+// copy-out stream, chained per chunk by events, so the host-to-device and
+// device-to-host DMA engines each stream continuously.
+struct HostPipe {
+  std::mutex mu;
+  unsigned nstreams = 2;
+  size_t chunk_bytes = (size_t)32 << 20;
+  std::vector<hipStream_t> streams;  // [0] copy in, [1] copy out, [2..] compute
+  std::vector<hipEvent_t> events;    // 2 per chunk
+  uint8_t *d_in = nullptr, *d_out = nullptr;
+  tlsgpu_record* d_recs = nullptr;
+  int32_t* d_status = nullptr;
+  size_t cap_in = 0, cap_out = 0, cap_recs = 0, cap_status = 0;
+};
+
 struct tlsgpu_engine {
   int device;
   hipStream_t stream;
   int num_cus;
   std::mutex pre_mu;
   std::vector<std::pair<hipStream_t, PreScratch>> pre;  // few streams per engine
+  HostPipe host;
 };
 
 // Scratch of at least `bytes` for stream s (enlarging waits for the stream's
@@ -102,6 +119,7 @@ struct tlsgpu_sessions {
   DevSession* d_sess;
   DevGcmTables* d_gcm;
   std::vector<int32_t> kinds;  // host mirror of installed kinds
+  std::vector<uint8_t> tag_lens;  // and tag lengths (host pipeline output spans)
   bool have[5];                // any session of kind k installed
 };
 
@@ -135,6 +153,12 @@ extern "C" void tlsgpu_engine_destroy(tlsgpu_engine* e) {
   (void)hipStreamSynchronize(e->stream);
   (void)hipDeviceSynchronize();  // batches on user streams may still use the scratch
   for (auto& kv : e->pre) (void)hipFree(kv.second.ptr);
+  for (hipStream_t hs : e->host.streams) (void)hipStreamDestroy(hs);  // host pipeline
+  for (hipEvent_t ev : e->host.events) (void)hipEventDestroy(ev);
+  (void)hipFree(e->host.d_in);
+  (void)hipFree(e->host.d_out);
+  (void)hipFree(e->host.d_recs);
+  (void)hipFree(e->host.d_status);
   (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -159,6 +183,7 @@ extern "C" int tlsgpu_sessions_create(tlsgpu_engine* e, uint32_t capacity, tlsgp
   t->eng = e;
   t->capacity = capacity;
   t->kinds.assign(capacity, 0);
+  t->tag_lens.assign(capacity, 16);
   memset(t->have, 0, sizeof(t->have));
   if (hipMalloc(&t->d_sess, sizeof(DevSession) * (size_t)capacity) != hipSuccess ||
       hipMalloc(&t->d_gcm, sizeof(DevGcmTables) * (size_t)capacity) != hipSuccess) {
@@ -217,6 +242,7 @@ extern "C" int tlsgpu_sessions_install(tlsgpu_sessions* t, uint32_t first, uint3
                 hipGetErrorString(err != hipSuccess ? err : serr));
   for (uint32_t i = 0; i < n; i++) {
     t->kinds[first + i] = params[i].aead;
+    t->tag_lens[first + i] = (uint8_t)(params[i].tag_len ? params[i].tag_len : 16);
     t->have[params[i].aead] = true;
   }
   return TLSGPU_OK;
@@ -455,6 +481,140 @@ extern "C" int tlsgpu_seal_batch(tlsgpu_sessions* t, const tlsgpu_record* d_recs
   const Bounds b = {in_bytes, out_bytes};
   return run_batch(t, d_recs, n, d_in, d_out, d_status,
                    stream ? (hipStream_t)stream : t->eng->stream, true, false, &b);
+}
+
+// grow-only device buffer
+static bool grow(void** p, size_t* cap, size_t want) {
+  if (*cap >= want) return true;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  if (hipMalloc(p, want ? want : 1) != hipSuccess) return false;
+  *cap = want;
+  return true;
+}
+
+extern "C" int tlsgpu_host_pipeline(tlsgpu_engine* e, unsigned streams, size_t chunk_bytes) {
+  if (!e || streams > 8) return fail(TLSGPU_EINVAL, "bad arguments");
+  std::lock_guard<std::mutex> lk(e->host.mu);
+  if (streams) e->host.nstreams = streams;
+  if (chunk_bytes) e->host.chunk_bytes = chunk_bytes;
+  return TLSGPU_OK;
+}
+
+extern "C" int tlsgpu_open_host(tlsgpu_sessions* t, const tlsgpu_record* h_recs, uint32_t n,
+                                const uint8_t* h_in, size_t in_bytes, uint8_t* h_out,
+                                size_t out_bytes, int32_t* h_status) {
+  if (!t || (n && (!h_recs || !h_in || !h_out || !h_status)))
+    return fail(TLSGPU_EINVAL, "bad arguments");
+  if (n == 0) return TLSGPU_OK;
+  tlsgpu_engine* e = t->eng;
+  HostPipe& hp = e->host;
+  std::lock_guard<std::mutex> lk(hp.mu);
+  HIPCHK(hipSetDevice(e->device));
+  const bool in_place = h_out == h_in;
+  if (in_place) out_bytes = in_bytes;
+  while (hp.streams.size() < 2 + hp.nstreams) {
+    hipStream_t hs;
+    HIPCHK(hipStreamCreateWithFlags(&hs, hipStreamNonBlocking));
+    hp.streams.push_back(hs);
+  }
+  if (!grow((void**)&hp.d_in, &hp.cap_in, in_bytes) ||
+      (!in_place && !grow((void**)&hp.d_out, &hp.cap_out, out_bytes)) ||
+      !grow((void**)&hp.d_status, &hp.cap_status, sizeof(int32_t) * (size_t)n) ||
+      !grow((void**)&hp.d_recs, &hp.cap_recs, sizeof(tlsgpu_record) * (size_t)n))
+    return fail(TLSGPU_ENOMEM, "host pipeline buffers (%zu + %zu bytes)", in_bytes, out_bytes);
+  uint8_t* d_in = hp.d_in;
+  uint8_t* d_out = in_place ? hp.d_in : hp.d_out;
+  // per-record spans (clamped to the buffers; the bounds pre-pass rejects the rest)
+  auto span_in = [&](const tlsgpu_record& r, uint64_t* lo, uint64_t* hi) {
+    *lo = std::min<uint64_t>(r.in_off, in_bytes);
+    *hi = std::min<uint64_t>(r.in_off + (r.len_type & 0xFFFFFFu), in_bytes);
+  };
+  // the plaintext span exactly (explicit nonce and tag excluded): a neighbouring
+  // chunk's D2H on another stream may own the next byte
+  auto span_out = [&](const tlsgpu_record& r, uint64_t* lo, uint64_t* hi) {
+    const uint64_t len = r.len_type & 0xFFFFFFu;
+    uint64_t over = 0;
+    if (r.session < t->capacity) {
+      const int k = t->kinds[r.session];
+      over = (k == TLSGPU_AES_128_GCM || k == TLSGPU_AES_256_GCM ? 8 : 0) + t->tag_lens[r.session];
+    }
+    *lo = std::min<uint64_t>(r.out_off, out_bytes);
+    *hi = std::min<uint64_t>(r.out_off + (len > over ? len - over : 0), out_bytes);
+  };
+  // chunks of ~chunk_bytes input when the layout ascends, else one chunk
+  bool ascending = true;
+  for (uint32_t i = 1; i < n && ascending; i++)
+    ascending = h_recs[i].in_off >= h_recs[i - 1].in_off &&
+                h_recs[i].out_off >= h_recs[i - 1].out_off;
+  // chunk sizes ramp up from 1 MiB and back down at the end, so the pipeline
+  // fills and drains on small transfers
+  std::vector<uint32_t> cuts{0};
+  if (ascending) {
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; i++) total += h_recs[i].len_type & 0xFFFFFFu;
+    uint64_t acc = 0, done = 0, target = std::min<uint64_t>(hp.chunk_bytes, 1u << 20);
+    for (uint32_t i = 0; i < n; i++) {
+      const uint64_t l = h_recs[i].len_type & 0xFFFFFFu;
+      acc += l;
+      done += l;
+      if (acc >= target && i + 1 < n) {
+        cuts.push_back(i + 1);
+        acc = 0;
+        const uint64_t left = total - done;
+        target = std::min<uint64_t>({(uint64_t)hp.chunk_bytes, 2 * target,
+                                     std::max<uint64_t>(left / 2, 1u << 20)});
+      }
+    }
+  }
+  cuts.push_back(n);
+  const size_t nchunks = cuts.size() - 1;
+  while (hp.events.size() < 2 * nchunks) {
+    hipEvent_t ev;
+    HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    hp.events.push_back(ev);
+  }
+  hipStream_t s_in = hp.streams[0], s_out = hp.streams[1];
+  const size_t ncomp = hp.streams.size() - 2;
+  // all descriptors in one copy ahead of the first chunk, all statuses in one after the last
+  HIPCHK(hipMemcpyAsync(hp.d_recs, h_recs, sizeof(tlsgpu_record) * (size_t)n,
+                        hipMemcpyHostToDevice, s_in));
+  for (size_t k = 0; k < nchunks; k++) {
+    const uint32_t a = cuts[k], b = cuts[k + 1];
+    hipStream_t hs = hp.streams[2 + k % ncomp];
+    hipEvent_t ev_in = hp.events[2 * k], ev_done = hp.events[2 * k + 1];
+    uint64_t ilo = UINT64_MAX, ihi = 0, olo = UINT64_MAX, ohi = 0;
+    for (uint32_t i = a; i < b; i++) {
+      uint64_t l, h;
+      span_in(h_recs[i], &l, &h);
+      ilo = std::min(ilo, l);
+      ihi = std::max(ihi, h);
+      span_out(h_recs[i], &l, &h);
+      olo = std::min(olo, l);
+      ohi = std::max(ohi, h);
+    }
+    if (!ascending) {  // one chunk: the whole buffers
+      ilo = 0; ihi = in_bytes; olo = 0; ohi = out_bytes;
+    }
+    // copy in (DMA engine 1) -> kernels (compute stream) -> copy out (DMA engine 2)
+    if (ihi > ilo)
+      HIPCHK(hipMemcpyAsync(d_in + ilo, h_in + ilo, ihi - ilo, hipMemcpyHostToDevice, s_in));
+    HIPCHK(hipEventRecord(ev_in, s_in));
+    HIPCHK(hipStreamWaitEvent(hs, ev_in, 0));
+    const Bounds bd = {in_bytes, out_bytes};
+    const int rc = run_batch(t, hp.d_recs + a, b - a, d_in, d_out, hp.d_status + a, hs, false, false,
+                             &bd);
+    if (rc != TLSGPU_OK) return rc;
+    HIPCHK(hipEventRecord(ev_done, hs));
+    HIPCHK(hipStreamWaitEvent(s_out, ev_done, 0));
+    if (ohi > olo)
+      HIPCHK(hipMemcpyAsync(h_out + olo, d_out + olo, ohi - olo, hipMemcpyDeviceToHost, s_out));
+  }
+  HIPCHK(hipMemcpyAsync(h_status, hp.d_status, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost,
+                        s_out));
+  for (hipStream_t hs : hp.streams) HIPCHK(hipStreamSynchronize(hs));
+  return TLSGPU_OK;
 }
 
 extern "C" int tlsgpu_open_wire(tlsgpu_sessions* t, const tlsgpu_wire_stream* d_streams,
