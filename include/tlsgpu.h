@@ -214,6 +214,51 @@ int tlsgpu_open_wire(tlsgpu_sessions *t, const tlsgpu_wire_stream *d_streams,
     uint32_t n_streams, uint8_t *d_wire, uint32_t max_records, tlsgpu_record *d_recs,
     int32_t *d_status, tlsgpu_wire_result *d_results, uint32_t *d_total, void *stream);
 
+/* ---------------------------------------------------------------------------
+ * Write-side framing: ssl3_write_bytes + do_ssl3_write
+ * (ssl/s3_pkt.c:501-557, 560-762) for the AEAD suites, many connections at
+ * once.  Each stream is one connection's SSL_write: data_len bytes of
+ * application data at d_data + data_off, split into records of at most
+ * max_fragment bytes (max_send_fragment, s3_pkt.c:531-536; a zero-length
+ * write sends nothing, :593-594), each written to d_wire as the 5-byte header
+ * (type, version, length = explicit nonce + ciphertext + tag, :662-677, :733)
+ * followed by tls1_enc(s, 1)'s fragment (explicit nonce = sequence number for
+ * GCM, t1_enc.c:887-914), back to back from d_wire + wire_off.  Sequence
+ * numbers run seq, seq + 1, ... (t1_enc.c:258-266).  The sealed records also
+ * get descriptors in d_recs (slots reserved per stream, like tlsgpu_open_wire;
+ * streams that do not fit max_records are cut at a record boundary) and a
+ * status each.  data_bytes / wire_bytes bound the buffers
+ * (TLSGPU_REC_OUT_OF_BOUNDS).  tlsgpu_seal_wire_size gives a stream's wire
+ * bytes.  Asynchronous. */
+typedef struct tlsgpu_write_stream {
+	uint64_t data_off;	/* application data at d_data + data_off */
+	uint64_t wire_off;	/* the stream's records go to d_wire + wire_off */
+	uint64_t seq;		/* write sequence number of the first record */
+	uint32_t data_len;	/* bytes to send (ssl3_write_bytes' len) */
+	uint32_t session;	/* write-direction session id */
+	uint16_t version;	/* s->version, e.g. 0x0303 */
+	uint8_t type;		/* content type, 23 = application data */
+	uint8_t reserved;
+	uint32_t max_fragment;	/* s->max_send_fragment; 0 = 16384 */
+} tlsgpu_write_stream;
+
+typedef struct tlsgpu_write_result {
+	uint32_t first;		/* index of the stream's first record in d_recs / d_status */
+	uint32_t records;	/* records written */
+	uint64_t wire_len;	/* bytes written from wire_off (headers + fragments) */
+	uint64_t next_seq;	/* the write sequence number after the last record */
+	uint64_t reserved;
+} tlsgpu_write_result;
+
+int tlsgpu_seal_wire(tlsgpu_sessions *t, const tlsgpu_write_stream *d_streams,
+    uint32_t n_streams, const uint8_t *d_data, size_t data_bytes, uint8_t *d_wire,
+    size_t wire_bytes, uint32_t max_records, tlsgpu_record *d_recs, int32_t *d_status,
+    tlsgpu_write_result *d_results, uint32_t *d_total, void *stream);
+/* Wire bytes of one stream: ceil(len / frag) records of 5 + explicit nonce
+ * (8 for GCM, 0 for ChaCha) + fragment + tag_len bytes (0 when len == 0). */
+uint64_t tlsgpu_seal_wire_size(int aead, uint32_t data_len, uint32_t max_fragment,
+    uint32_t tag_len);
+
 /* GCM TLS batch kernel selection (process-wide; results are identical).
  * TLSGPU_GCM_QUEUE (default): a prep pass computes every record's E_K(J0) and
  * round-1/2 constants, then 16 T-table waves per CU (AES rounds as LDS

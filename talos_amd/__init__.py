@@ -53,6 +53,13 @@ WIRE_RESULT_DTYPE = np.dtype([("first", "<u4"), ("records", "<u4"), ("delivered"
                               ("reserved", "<u4", (2,))])
 assert WIRE_STREAM_DTYPE.itemsize == 32 and WIRE_RESULT_DTYPE.itemsize == 32
 WIRE_FIRST_PACKET = 1
+# tlsgpu_write_stream / tlsgpu_write_result (include/tlsgpu.h)
+WRITE_STREAM_DTYPE = np.dtype([("data_off", "<u8"), ("wire_off", "<u8"), ("seq", "<u8"),
+                               ("data_len", "<u4"), ("session", "<u4"), ("version", "<u2"),
+                               ("type", "u1"), ("reserved", "u1"), ("max_fragment", "<u4")])
+WRITE_RESULT_DTYPE = np.dtype([("first", "<u4"), ("records", "<u4"), ("wire_len", "<u8"),
+                               ("next_seq", "<u8"), ("reserved", "<u8")])
+assert WRITE_STREAM_DTYPE.itemsize == 40 and WRITE_RESULT_DTYPE.itemsize == 32
 REC_BAD_MAC, REC_PUBLIC_INVALID, REC_SKIPPED, REC_OVERFLOW, REC_OUT_OF_BOUNDS = -1, -2, -3, -4, -5
 
 RECORD_DTYPE = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("seq", "<u8"),
@@ -130,6 +137,9 @@ def load_library(path: str = LIBPATH) -> C.CDLL:
         "tlsgpu_debug_phase_stats": (i32, [vp, C.POINTER(C.c_ulonglong), i32]),
         "tlsgpu_open_wire": (i32, [vp, vp, u32, vp, u32, vp, vp, vp, vp, vp]),
         "tlsgpu_open_host": (i32, [vp, vp, u32, vp, C.c_size_t, vp, C.c_size_t, vp]),
+        "tlsgpu_seal_wire": (i32, [vp, vp, u32, vp, C.c_size_t, vp, C.c_size_t, u32, vp, vp, vp,
+                                   vp, vp]),
+        "tlsgpu_seal_wire_size": (u64, [i32, u32, u32, u32]),
         "tlsgpu_host_pipeline": (i32, [vp, C.c_uint, C.c_size_t]),
         "tlsgpu_evp_set_batching": (i32, [C.c_uint, C.c_uint, C.c_uint]),
         "tlsgpu_evp_batch_stats": (i32, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
@@ -381,6 +391,20 @@ def open_batch(table: SessionTable, d_recs: int, n: int, d_in: int, in_bytes: in
     d_out hold in_bytes / out_bytes (records outside get REC_OUT_OF_BOUNDS)."""
     _check(table.lib.tlsgpu_open_batch(table.handle, d_recs, n, d_in, in_bytes, d_out, out_bytes,
                                        d_status, stream), "tlsgpu_open_batch")
+
+
+def seal_wire(table: SessionTable, d_streams: int, n_streams: int, d_data: int, data_bytes: int,
+              d_wire: int, wire_bytes: int, max_records: int, d_recs: int, d_status: int,
+              d_results: int, d_total: int, stream: int | None = None) -> None:
+    """Fragment, frame and seal application data of many connections
+    (tlsgpu_seal_wire: ssl3_write_bytes + do_ssl3_write for AEAD suites)."""
+    _check(table.lib.tlsgpu_seal_wire(table.handle, d_streams, n_streams, d_data, data_bytes,
+                                      d_wire, wire_bytes, max_records, d_recs, d_status,
+                                      d_results, d_total, stream), "tlsgpu_seal_wire")
+
+
+def seal_wire_size(aead: int, data_len: int, max_fragment: int = 0, tag_len: int = 0) -> int:
+    return int(load_library().tlsgpu_seal_wire_size(aead, data_len, max_fragment, tag_len))
 
 
 def open_host(table: SessionTable, h_recs: int, n: int, h_in: int, in_bytes: int, h_out: int,

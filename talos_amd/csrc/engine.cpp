@@ -642,6 +642,38 @@ extern "C" int tlsgpu_open_wire(tlsgpu_sessions* t, const tlsgpu_wire_stream* d_
   return TLSGPU_OK;
 }
 
+extern "C" int tlsgpu_seal_wire(tlsgpu_sessions* t, const tlsgpu_write_stream* d_streams,
+                                uint32_t n_streams, const uint8_t* d_data, size_t data_bytes,
+                                uint8_t* d_wire, size_t wire_bytes, uint32_t max_records,
+                                tlsgpu_record* d_recs, int32_t* d_status,
+                                tlsgpu_write_result* d_results, uint32_t* d_total, void* stream) {
+  if (!t || !d_total || (n_streams && (!d_streams || !d_data || !d_wire || !d_results)) ||
+      (max_records && (!d_recs || !d_status)))
+    return fail(TLSGPU_EINVAL, "bad arguments");
+  HIPCHK(hipSetDevice(t->eng->device));
+  hipStream_t s = stream ? (hipStream_t)stream : t->eng->stream;
+  HIPCHK(hipMemsetAsync(d_total, 0, sizeof(uint32_t), s));
+  if (n_streams == 0) return TLSGPU_OK;
+  // unused record slots name no session (0xFFFFFFFF): the seal kernels skip them
+  if (max_records) HIPCHK(hipMemsetAsync(d_recs, 0xFF, sizeof(tlsgpu_record) * (size_t)max_records, s));
+  if (launch_wire_seal_frame(d_streams, n_streams, t->d_sess, t->capacity, d_wire, wire_bytes,
+                             max_records, d_recs, d_results, d_total, s))
+    return fail(TLSGPU_EHIP, "wire seal frame launch: %s", hipGetErrorString(hipGetLastError()));
+  if (max_records) {
+    const Bounds b = {data_bytes, wire_bytes};
+    return run_batch(t, d_recs, max_records, d_data, d_wire, d_status, s, true, false, &b);
+  }
+  return TLSGPU_OK;
+}
+
+extern "C" uint64_t tlsgpu_seal_wire_size(int aead, uint32_t data_len, uint32_t max_fragment,
+                                          uint32_t tag_len) {
+  const uint32_t frag = max_fragment == 0 || max_fragment > 16384 ? 16384 : max_fragment;
+  const uint64_t nrec = ((uint64_t)data_len + frag - 1) / frag;
+  const uint64_t eiv = aead == TLSGPU_AES_128_GCM || aead == TLSGPU_AES_256_GCM ? 8 : 0;
+  return data_len + nrec * (5 + eiv + (tag_len ? tag_len : 16));
+}
+
 extern "C" int tlsgpu_fill_synthetic(tlsgpu_engine* e, uint8_t* d_out, uint64_t stride,
                                      uint32_t span_len, uint32_t n, uint64_t seed,
                                      uint64_t index0, void* stream) {

@@ -211,6 +211,10 @@ int launch_wire_frame(const tlsgpu_wire_stream* streams, uint32_t n_streams, con
                       const DevSession* sessions, uint32_t n_sessions, uint32_t max_records,
                       tlsgpu_record* recs, tlsgpu_wire_result* results, uint32_t* total,
                       hipStream_t s);
+int launch_wire_seal_frame(const tlsgpu_write_stream* streams, uint32_t n_streams,
+                           const DevSession* sessions, uint32_t n_sessions, uint8_t* wire,
+                           uint64_t wire_bytes, uint32_t max_records, tlsgpu_record* recs,
+                           tlsgpu_write_result* results, uint32_t* total, hipStream_t s);
 int launch_wire_finish(uint32_t n_streams, tlsgpu_wire_result* results, int32_t* status,
                        hipStream_t s);
 int launch_fill_synthetic(uint8_t* d_out, uint64_t stride, uint32_t span_len,

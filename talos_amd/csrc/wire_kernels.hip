@@ -207,6 +207,70 @@ __global__ __launch_bounds__(256) void wire_finish_kernel(uint32_t n_streams,
   results[s] = r;
 }
 
+// Write-side framing (ssl3_write_bytes / do_ssl3_write, s3_pkt.c:501-762), one
+// lane per stream: reserves the stream's record slots, writes each record's
+// 5-byte header and its seal descriptor (fragment at header + 5; the seal
+// kernels write explicit nonce || ciphertext || tag there).
+__global__ __launch_bounds__(256) void wire_seal_frame_kernel(
+    const tlsgpu_write_stream* __restrict__ streams, uint32_t n_streams,
+    const DevSession* __restrict__ sessions, uint32_t n_sessions, uint8_t* __restrict__ wire,
+    uint64_t wire_bytes, uint32_t max_records, tlsgpu_record* __restrict__ recs,
+    tlsgpu_write_result* __restrict__ results, uint32_t* __restrict__ total) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_streams) return;
+  const tlsgpu_write_stream st = streams[i];
+  tlsgpu_write_result res = {};
+  res.next_seq = st.seq;
+  const bool ok = st.session < n_sessions && sessions[st.session].kind != 0;
+  const uint32_t frag = st.max_fragment == 0 || st.max_fragment > kMaxPlain ? kMaxPlain
+                                                                           : st.max_fragment;
+  uint32_t nrec = ok ? (st.data_len + frag - 1) / frag : 0;  // len 0: nothing (:593-594)
+  const uint32_t first = nrec ? atomicAdd(total, nrec) : 0;
+  if (first >= max_records) nrec = 0;
+  else if (first + nrec > max_records) nrec = max_records - first;
+  res.first = first;
+  if (nrec) {
+    const DevSession& S = sessions[st.session];
+    const uint32_t over = (S.nonce_in_record ? 8u : 0u) + S.tag_len;  // eivlen + tag
+    uint64_t pos = st.wire_off;
+    for (uint32_t k = 0; k < nrec; k++) {
+      const uint32_t len = min(frag, st.data_len - k * frag);
+      const uint32_t L = len + over;  // the length field (s3_pkt.c:733)
+      if (pos + kHdr + L <= wire_bytes) {
+        uint8_t* h = wire + pos;
+        h[0] = st.type;
+        h[1] = (uint8_t)(st.version >> 8);
+        h[2] = (uint8_t)st.version;
+        h[3] = (uint8_t)(L >> 8);
+        h[4] = (uint8_t)L;
+      }
+      tlsgpu_record d;
+      d.in_off = st.data_off + (uint64_t)k * frag;
+      d.out_off = pos + kHdr;
+      d.seq = st.seq + k;
+      d.session = st.session;
+      d.len_type = TLSGPU_LEN_TYPE(len, st.type);
+      recs[first + k] = d;
+      pos += kHdr + L;
+    }
+    res.records = nrec;
+    res.wire_len = pos - st.wire_off;
+    res.next_seq = st.seq + nrec;
+  }
+  results[i] = res;
+}
+
+int launch_wire_seal_frame(const tlsgpu_write_stream* streams, uint32_t n_streams,
+                           const DevSession* sessions, uint32_t n_sessions, uint8_t* wire,
+                           uint64_t wire_bytes, uint32_t max_records, tlsgpu_record* recs,
+                           tlsgpu_write_result* results, uint32_t* total, hipStream_t s) {
+  if (n_streams == 0) return 0;
+  hipLaunchKernelGGL(wire_seal_frame_kernel, dim3((n_streams + 255) / 256), dim3(256), 0, s, streams,
+                     n_streams, sessions, n_sessions, wire, wire_bytes, max_records, recs, results,
+                     total);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_wire_frame(const tlsgpu_wire_stream* streams, uint32_t n_streams, const uint8_t* wire,
                       const DevSession* sessions, uint32_t n_sessions, uint32_t max_records,
                       tlsgpu_record* recs, tlsgpu_wire_result* results, uint32_t* total,
