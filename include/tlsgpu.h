@@ -296,6 +296,9 @@ int tlsgpu_evp_batch_stats(uint64_t *batches, uint64_t *jobs);
  * not), process-wide since load.  Lets a caller that interposed the library
  * under an unchanged libssl check that every TLS record went through it. */
 int tlsgpu_evp_call_stats(uint64_t *seal_calls, uint64_t *open_calls);
+/* GPU programs run by the EVP_aes_{128,256}_gcm EVP_CIPHER objects
+ * (include/tlsgpu_evp.h), process-wide since load. */
+int tlsgpu_evp_cipher_stats(uint64_t *programs);
 
 /* Diagnostic: hybrid-kernel phase timing.  With TLSGPU_PHASE_STATS=1 in the
  * environment, the first call allocates 32 device counters (shader cycles and

@@ -37,7 +37,59 @@ typedef struct evp_aead_ctx_st {
 
 #define EVP_AEAD_MAX_TAG_LENGTH 16	/* evp.h:1252 */
 #define EVP_AEAD_DEFAULT_TAG_LENGTH 0	/* evp.h:1257 */
+
+/* Legacy EVP_CIPHER GCM surface.  Layouts of LibreSSL
+ * 2.4.1's public structs (evp.h:297-313, 405-423): libcrypto's generic
+ * EVP_CipherInit_ex / EVP_CipherUpdate / EVP_CIPHER_CTX_ctrl / _copy /
+ * _cleanup (crypto/evp/evp_enc.c) call the function pointers of the object
+ * EVP_aes_*_gcm() returns, so exporting these two getters is the whole
+ * interposition. */
+typedef struct evp_cipher_st EVP_CIPHER;
+typedef struct evp_cipher_ctx_st EVP_CIPHER_CTX;
+typedef struct asn1_type_st ASN1_TYPE;
+#define EVP_MAX_IV_LENGTH 16		/* evp.h:79 */
+#define EVP_MAX_BLOCK_LENGTH 32		/* evp.h:80 */
+struct evp_cipher_st {
+	int nid;
+	int block_size;
+	int key_len;
+	int iv_len;
+	unsigned long flags;
+	int (*init)(EVP_CIPHER_CTX *ctx, const unsigned char *key, const unsigned char *iv,
+	    int enc);
+	int (*do_cipher)(EVP_CIPHER_CTX *ctx, unsigned char *out, const unsigned char *in,
+	    size_t inl);
+	int (*cleanup)(EVP_CIPHER_CTX *);
+	int ctx_size;
+	int (*set_asn1_parameters)(EVP_CIPHER_CTX *, ASN1_TYPE *);
+	int (*get_asn1_parameters)(EVP_CIPHER_CTX *, ASN1_TYPE *);
+	int (*ctrl)(EVP_CIPHER_CTX *, int type, int arg, void *ptr);
+	void *app_data;
+};
+struct evp_cipher_ctx_st {
+	const EVP_CIPHER *cipher;
+	ENGINE *engine;
+	int encrypt;
+	int buf_len;
+	unsigned char oiv[EVP_MAX_IV_LENGTH];
+	unsigned char iv[EVP_MAX_IV_LENGTH];
+	unsigned char buf[EVP_MAX_BLOCK_LENGTH];
+	int num;
+	void *app_data;
+	int key_len;
+	unsigned long flags;
+	void *cipher_data;
+	int final_used;
+	int block_mask;
+	unsigned char final[EVP_MAX_BLOCK_LENGTH];
+};
 #endif
+
+/* e_aes.c:1054-1059: AES-128/256 GCM as EVP_CIPHERs (the init / do_cipher /
+ * ctrl / cleanup of e_aes.c:687-1047, cipher work on the GPU).  AES-192-GCM
+ * is not provided by this engine. */
+const EVP_CIPHER *EVP_aes_128_gcm(void);
+const EVP_CIPHER *EVP_aes_256_gcm(void);
 
 /* evp.h:1211-1223 */
 const EVP_AEAD *EVP_aead_aes_128_gcm(void);

@@ -20,6 +20,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <unistd.h>
 #include <thread>
 #include <vector>
 
@@ -1201,6 +1202,339 @@ error:
   memset(out, 0, max_out_len);  // evp_aead.c:137-143
   *out_len = 0;
   return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Legacy EVP_CIPHER GCM surface (crypto/evp/e_aes.c:687-1059).
+// The object's function pointers are called by the generic EVP_Cipher* code of
+// whatever libcrypto the application links; the cipher work runs as programs
+// of GCM128 steps on the gcm_stream kernel (one launch per call).
+namespace {
+enum {
+  kCtrlInit = 0x0, kCtrlCopy = 0x8, kGcmSetIvlen = 0x9, kGcmGetTag = 0x10, kGcmSetTag = 0x11,
+  kGcmSetIvFixed = 0x12, kGcmIvGen = 0x13, kAeadTls1Aad = 0x16, kGcmSetIvInv = 0x18,
+  kTlsExplicitIv = 8, kTlsTag = 16,  // EVP_GCM_TLS_EXPLICIT_IV_LEN / _TAG_LEN (evp.h:394-398)
+};
+// EVP_CIPH_GCM_MODE | CUSTOM_IV | ALWAYS_CALL_INIT | CTRL_INIT | CUSTOM_COPY |
+// FLAG_DEFAULT_ASN1 | FLAG_FIPS | FLAG_CUSTOM_CIPHER | FLAG_AEAD_CIPHER (e_aes.c:1049-1059)
+constexpr unsigned long kGcmCipherFlags =
+    0x6 | 0x10 | 0x20 | 0x40 | 0x400 | 0x1000 | 0x4000 | 0x100000 | 0x200000;
+
+// EVP_AES_GCM_CTX (e_aes.c:74-85) with the GCM128 state on the device
+struct GpuGcm {
+  tlsgpu_sessions* sess;  // one-session table: key schedule, H tables
+  GcmStream* d_st;        // GCM128_CONTEXT
+  unsigned char key[32];
+  int key_set, iv_set;
+  unsigned char* iv;      // ctx->iv, or heap for IVs longer than 16 bytes
+  int ivlen, taglen, iv_gen, tls_aad_len;
+};
+
+std::atomic<uint64_t> g_cipher_programs{0};
+
+// One program of GCM128 steps.  Step i reads in[i] (host, len[i] bytes) and
+// writes out[i] (host, len[i] bytes; TAG: len bytes of tag).  Returns the rc
+// of the last step run (gcm128.c conventions), or -100 on a runtime failure.
+struct Step {
+  uint32_t kind;
+  const unsigned char* in;
+  unsigned char* out;
+  size_t len;
+};
+int run_program(GpuGcm* g, const Step* steps, int nsteps) {
+  tlsgpu_engine* e = g->sess->eng;
+  auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+  size_t total = al(sizeof(GcmStreamOp) * (size_t)nsteps);
+  std::vector<size_t> o_in(nsteps), o_out(nsteps);
+  for (int i = 0; i < nsteps; i++) {
+    o_in[i] = total;
+    total += al(steps[i].in ? steps[i].len : 0);
+    o_out[i] = total;
+    total += al(steps[i].out ? steps[i].len : 0);
+  }
+  if (!t_stage.ensure(e->device, total)) return -100;
+  uint8_t* b = t_stage.d_buf;
+  hipStream_t s = t_stage.stream;
+  std::vector<GcmStreamOp> ops(nsteps);
+  for (int i = 0; i < nsteps; i++) {
+    ops[i].kind = steps[i].kind;
+    ops[i].reserved = 0;
+    ops[i].len = steps[i].len;
+    ops[i].in = steps[i].in ? (uint64_t)(b + o_in[i]) : 0;
+    ops[i].out = steps[i].out ? (uint64_t)(b + o_out[i]) : 0;
+    if (steps[i].in && steps[i].len &&
+        hipMemcpyAsync(b + o_in[i], steps[i].in, steps[i].len, hipMemcpyHostToDevice, s))
+      return -100;
+  }
+  if (hipMemcpyAsync(b, ops.data(), sizeof(GcmStreamOp) * nsteps, hipMemcpyHostToDevice, s) ||
+      launch_gcm_stream(g->sess->d_sess, g->sess->d_gcm, 0, g->d_st,
+                        reinterpret_cast<const GcmStreamOp*>(b), (uint32_t)nsteps, s))
+    return -100;
+  int32_t rc = -100;
+  if (hipMemcpyAsync(&rc, &g->d_st->rc, sizeof(rc), hipMemcpyDeviceToHost, s) ||
+      hipStreamSynchronize(s))
+    return -100;
+  for (int i = 0; i < nsteps; i++)
+    if (steps[i].out && steps[i].len &&
+        hipMemcpy(steps[i].out, b + o_out[i], steps[i].len, hipMemcpyDeviceToHost))
+      return -100;
+  g_cipher_programs.fetch_add(1, std::memory_order_relaxed);
+  return rc;
+}
+
+bool gcm_set_key(GpuGcm* g, const unsigned char* key, int key_len) {
+  tlsgpu_engine* e = default_engine();
+  if (!e) return false;
+  if (!g->sess && tlsgpu_sessions_create(e, 1, &g->sess) != TLSGPU_OK) return false;
+  if (!g->d_st) {
+    if (hipSetDevice(e->device) != hipSuccess ||
+        hipMalloc((void**)&g->d_st, sizeof(GcmStream)) != hipSuccess) {
+      g->d_st = nullptr;
+      return false;
+    }
+  }
+  if (hipMemset(g->d_st, 0, sizeof(GcmStream)) != hipSuccess) return false;
+  tlsgpu_session_params p;
+  memset(&p, 0, sizeof(p));
+  p.aead = key_len == 16 ? TLSGPU_AES_128_GCM : TLSGPU_AES_256_GCM;
+  p.key_len = (uint32_t)key_len;
+  memcpy(p.key, key, key_len);
+  p.version = 0x0303;
+  memcpy(g->key, key, key_len);
+  const bool ok = tlsgpu_sessions_install(g->sess, 0, 1, &p) == TLSGPU_OK;
+  memset(&p, 0, sizeof(p));
+  return ok;
+}
+
+int gcm_setiv(GpuGcm* g, const unsigned char* iv, int ivlen) {
+  const Step st = {GCM_OP_SETIV, iv, nullptr, (size_t)ivlen};
+  return run_program(g, &st, 1);
+}
+
+// ctr64_inc (e_aes.c:697-712)
+void ctr64_inc(unsigned char* counter) {
+  for (int n = 7; n >= 0; n--)
+    if (++counter[n]) return;
+}
+
+int gcm_ctrl(EVP_CIPHER_CTX* c, int type, int arg, void* ptr);
+
+int gcm_init_key(EVP_CIPHER_CTX* ctx, const unsigned char* key, const unsigned char* iv, int enc) {
+  (void)enc;
+  auto* g = (GpuGcm*)ctx->cipher_data;
+  if (!iv && !key) return 1;
+  if (key) {
+    if (ctx->key_len != 16 && ctx->key_len != 32) return 0;
+    if (!gcm_set_key(g, key, ctx->key_len)) return 0;
+    if (iv == nullptr && g->iv_set) iv = g->iv;
+    if (iv) {
+      if (gcm_setiv(g, iv, g->ivlen) != 0) return 0;
+      g->iv_set = 1;
+    }
+    g->key_set = 1;
+  } else {
+    if (g->key_set) {
+      if (gcm_setiv(g, iv, g->ivlen) != 0) return 0;
+    } else {
+      memcpy(g->iv, iv, g->ivlen);
+    }
+    g->iv_set = 1;
+    g->iv_gen = 0;
+  }
+  return 1;
+}
+
+int gcm_ctrl(EVP_CIPHER_CTX* c, int type, int arg, void* ptr) {
+  auto* g = (GpuGcm*)c->cipher_data;
+  switch (type) {
+    case kCtrlInit:
+      memset(g, 0, sizeof(*g));
+      g->ivlen = c->cipher->iv_len;
+      g->iv = c->iv;
+      g->taglen = -1;
+      g->tls_aad_len = -1;
+      return 1;
+    case kGcmSetIvlen:
+      if (arg <= 0) return 0;
+      if (arg > EVP_MAX_IV_LENGTH && arg > g->ivlen) {
+        if (g->iv != c->iv) free(g->iv);
+        g->iv = (unsigned char*)malloc(arg);
+        if (!g->iv) return 0;
+      }
+      g->ivlen = arg;
+      return 1;
+    case kGcmSetTag:
+      if (arg <= 0 || arg > 16 || c->encrypt) return 0;
+      memcpy(c->buf, ptr, arg);
+      g->taglen = arg;
+      return 1;
+    case kGcmGetTag:
+      if (arg <= 0 || arg > 16 || !c->encrypt || g->taglen < 0) return 0;
+      memcpy(ptr, c->buf, arg);
+      return 1;
+    case kGcmSetIvFixed:
+      if (arg == -1) {
+        memcpy(g->iv, ptr, g->ivlen);
+        g->iv_gen = 1;
+        return 1;
+      }
+      if (arg < 4 || (g->ivlen - arg) < 8) return 0;
+      if (arg) memcpy(g->iv, ptr, arg);
+      if (c->encrypt && getentropy(g->iv + arg, g->ivlen - arg) != 0) return 0;
+      g->iv_gen = 1;
+      return 1;
+    case kGcmIvGen:
+      if (g->iv_gen == 0 || g->key_set == 0) return 0;
+      if (gcm_setiv(g, g->iv, g->ivlen) != 0) return 0;
+      if (arg <= 0 || arg > g->ivlen) arg = g->ivlen;
+      memcpy(ptr, g->iv + g->ivlen - arg, arg);
+      ctr64_inc(g->iv + g->ivlen - 8);
+      g->iv_set = 1;
+      return 1;
+    case kGcmSetIvInv:
+      if (g->iv_gen == 0 || g->key_set == 0 || c->encrypt) return 0;
+      memcpy(g->iv + g->ivlen - arg, ptr, arg);
+      if (gcm_setiv(g, g->iv, g->ivlen) != 0) return 0;
+      g->iv_set = 1;
+      return 1;
+    case kAeadTls1Aad: {
+      if (arg != 13) return 0;
+      memcpy(c->buf, ptr, arg);
+      g->tls_aad_len = arg;
+      unsigned int len = c->buf[arg - 2] << 8 | c->buf[arg - 1];
+      len -= kTlsExplicitIv;            // correct length for the explicit IV
+      if (!c->encrypt) len -= kTlsTag;  // and the tag when decrypting
+      c->buf[arg - 2] = len >> 8;
+      c->buf[arg - 1] = len & 0xff;
+      return kTlsTag;  // extra padding: the tag appended to the record
+    }
+    case kCtrlCopy: {  // the GCM state and the key schedule get their own device copies
+      auto* out = (EVP_CIPHER_CTX*)ptr;
+      auto* go = (GpuGcm*)out->cipher_data;
+      go->sess = nullptr;
+      go->d_st = nullptr;
+      if (g->key_set) {
+        if (!gcm_set_key(go, g->key, c->key_len)) return 0;
+        if (hipMemcpy(go->d_st, g->d_st, sizeof(GcmStream), hipMemcpyDeviceToDevice) != hipSuccess)
+          return 0;
+      }
+      if (g->iv == c->iv) {
+        go->iv = out->iv;
+      } else {
+        go->iv = (unsigned char*)malloc(g->ivlen);
+        if (!go->iv) return 0;
+        memcpy(go->iv, g->iv, g->ivlen);
+      }
+      return 1;
+    }
+    default:
+      return -1;
+  }
+}
+
+// aes_gcm_tls_cipher (e_aes.c:917-985): one TLS record in place
+int gcm_tls_cipher(EVP_CIPHER_CTX* ctx, unsigned char* out, const unsigned char* in, size_t len) {
+  auto* g = (GpuGcm*)ctx->cipher_data;
+  int rv = -1;
+  if (out != in || len < (size_t)(kTlsExplicitIv + kTlsTag)) return -1;
+  // IV from the record (decrypt) or generated and written to it (encrypt);
+  // the setiv of IV_GEN / SET_IV_INV runs as the program's first step
+  if (ctx->encrypt) {
+    if (g->iv_gen == 0 || g->key_set == 0) goto err;
+    memcpy(out, g->iv + g->ivlen - kTlsExplicitIv, kTlsExplicitIv);
+  } else {
+    if (g->iv_gen == 0 || g->key_set == 0) goto err;
+    memcpy(g->iv + g->ivlen - kTlsExplicitIv, out, kTlsExplicitIv);
+  }
+  {
+    unsigned char iv[64];
+    if (g->ivlen > (int)sizeof(iv)) goto err;
+    memcpy(iv, g->iv, g->ivlen);
+    if (ctx->encrypt) ctr64_inc(g->iv + g->ivlen - 8);
+    g->iv_set = 1;
+    const size_t plen = len - kTlsExplicitIv - kTlsTag;
+    unsigned char* p = out + kTlsExplicitIv;
+    unsigned char tag[16];
+    const Step prog[4] = {{GCM_OP_SETIV, iv, nullptr, (size_t)g->ivlen},
+                          {GCM_OP_AAD, ctx->buf, nullptr, (size_t)g->tls_aad_len},
+                          {ctx->encrypt ? (uint32_t)GCM_OP_ENCRYPT : (uint32_t)GCM_OP_DECRYPT,
+                           in + kTlsExplicitIv, p, plen},
+                          {GCM_OP_TAG, nullptr, ctx->encrypt ? p + plen : tag, (size_t)kTlsTag}};
+    if (run_program(g, prog, 4) != 0) goto err;
+    if (ctx->encrypt) {
+      rv = (int)(plen + kTlsExplicitIv + kTlsTag);
+    } else {
+      memcpy(ctx->buf, tag, kTlsTag);
+      if (memcmp(ctx->buf, in + kTlsExplicitIv + plen, kTlsTag)) {  // wipe on mismatch
+        memset(p, 0, plen);
+        goto err;
+      }
+      rv = (int)plen;
+    }
+  }
+err:
+  g->iv_set = 0;
+  g->tls_aad_len = -1;
+  return rv;
+}
+
+// aes_gcm_cipher (e_aes.c:987-1047)
+int gcm_cipher(EVP_CIPHER_CTX* ctx, unsigned char* out, const unsigned char* in, size_t len) {
+  auto* g = (GpuGcm*)ctx->cipher_data;
+  if (!g->key_set) return -1;
+  if (g->tls_aad_len >= 0) return gcm_tls_cipher(ctx, out, in, len);
+  if (!g->iv_set) return -1;
+  if (in) {
+    Step st;
+    if (out == nullptr) {
+      st = {GCM_OP_AAD, in, nullptr, len};
+    } else {
+      st = {ctx->encrypt ? (uint32_t)GCM_OP_ENCRYPT : (uint32_t)GCM_OP_DECRYPT, in, out, len};
+    }
+    if (run_program(g, &st, 1) != 0) return -1;
+    return (int)len;
+  }
+  if (!ctx->encrypt) {
+    if (g->taglen < 0) return -1;
+    const Step st = {GCM_OP_FINISH, ctx->buf, nullptr, (size_t)g->taglen};
+    if (run_program(g, &st, 1) != 0) return -1;
+    g->iv_set = 0;
+    return 0;
+  }
+  const Step st = {GCM_OP_TAG, nullptr, ctx->buf, 16};
+  if (run_program(g, &st, 1) != 0) return -1;
+  g->taglen = 16;
+  g->iv_set = 0;  // don't reuse the IV
+  return 0;
+}
+
+// aes_gcm_cleanup (e_aes.c:686-695)
+int gcm_cleanup(EVP_CIPHER_CTX* c) {
+  auto* g = (GpuGcm*)c->cipher_data;
+  if (!g) return 1;
+  if (g->iv != c->iv) free(g->iv);
+  if (g->d_st) {
+    (void)hipMemset(g->d_st, 0, sizeof(GcmStream));
+    (void)hipFree(g->d_st);
+  }
+  if (g->sess) tlsgpu_sessions_destroy(g->sess);
+  memset(g, 0, sizeof(*g));
+  return 1;
+}
+
+const EVP_CIPHER k_aes_128_gcm = {895, 1, 16, 12, kGcmCipherFlags, gcm_init_key, gcm_cipher,
+                                  gcm_cleanup, (int)sizeof(GpuGcm), nullptr, nullptr, gcm_ctrl,
+                                  nullptr};
+const EVP_CIPHER k_aes_256_gcm = {901, 1, 32, 12, kGcmCipherFlags, gcm_init_key, gcm_cipher,
+                                  gcm_cleanup, (int)sizeof(GpuGcm), nullptr, nullptr, gcm_ctrl,
+                                  nullptr};
+}  // namespace
+
+extern "C" const EVP_CIPHER* EVP_aes_128_gcm(void) { return &k_aes_128_gcm; }
+extern "C" const EVP_CIPHER* EVP_aes_256_gcm(void) { return &k_aes_256_gcm; }
+extern "C" int tlsgpu_evp_cipher_stats(uint64_t* programs) {
+  if (programs) *programs = g_cipher_programs.load();
+  return TLSGPU_OK;
 }
 
 // ---------------------------------------------------------------------------

@@ -60,6 +60,28 @@ struct RawJob {
   uint64_t max_out;    // bytes zero-filled on failure
 };
 
+// Streaming GCM state of one EVP_CIPHER context (GCM128_CONTEXT,
+// crypto/modes/modes_lcl.h:79-95), in device memory; byte strings as
+// big-endian words.  Operated on by gcm_stream.hip.
+struct alignas(16) GcmStream {
+  uint32_t Yi[4], EKi[4], EK0[4], Xi[4];
+  uint64_t len_aad, len_data;
+  uint32_t mres, ares;
+  int32_t rc;       // result of the program's last step (gcm128.c return values;
+                    // FINISH: 0 tag equal, 1 differs, -1 no tag)
+  uint32_t reserved;
+};
+enum GcmOpKind : uint32_t {
+  GCM_OP_SETIV = 0, GCM_OP_AAD = 1, GCM_OP_ENCRYPT = 2, GCM_OP_DECRYPT = 3, GCM_OP_FINISH = 4,
+  GCM_OP_TAG = 5
+};
+struct GcmStreamOp {
+  uint32_t kind;    // GcmOpKind
+  uint32_t reserved;
+  uint64_t len;
+  uint64_t in, out; // device pointers
+};
+
 // Kernel launch parameters for the GCM / ChaCha batch kernels.
 // Global-address-space views of generic pointers.  Record pointers reach the
 // kernels through descriptors, structs and lane shuffles, where the compiler
@@ -195,6 +217,8 @@ int launch_gcm_queue(const BatchArgs& a, const RecPre* pre, bool seal, int round
                      hipStream_t s);
 int launch_gcm_pw(const BatchArgs& a, const RecPre* pre, bool seal, int rounds, int groups,
                   hipStream_t s);
+int launch_gcm_stream(const DevSession* sessions, const DevGcmTables* tables, uint32_t session,
+                      GcmStream* st, const GcmStreamOp* ops, uint32_t nops, hipStream_t s);
 int launch_gcm_hy10(const BatchArgs& a, const RecPre* pre, bool seal, int bs_waves, int groups,
                     hipStream_t s);
 int launch_gcm_fused10(const BatchArgs& a, const RecPre* pre, bool seal, int groups, hipStream_t s);
