@@ -157,6 +157,26 @@ int tlsgpu_seal_batch(tlsgpu_sessions *t, const tlsgpu_record *d_recs, uint32_t 
  * written back unchanged). */
 int tlsgpu_open_host(tlsgpu_sessions *t, const tlsgpu_record *h_recs, uint32_t n,
     const uint8_t *h_in, size_t in_bytes, uint8_t *h_out, size_t out_bytes, int32_t *h_status);
+/* The write direction: plaintext records in host memory (h_in) sealed into
+ * host fragments (h_out, explicit nonce || ciphertext || tag at out_off;
+ * headers are the caller's, or use tlsgpu_seal_wire).  Not in place. */
+int tlsgpu_seal_host(tlsgpu_sessions *t, const tlsgpu_record *h_recs, uint32_t n,
+    const uint8_t *h_in, size_t in_bytes, uint8_t *h_out, size_t out_bytes, int32_t *h_status);
+
+/* TaLoS plaintext-processing hooks (src/talos/enclaveshim/tls_processing_interface.h:
+ * tls_processing_ssl_read / _ssl_write, called from ssl3_read_bytes after
+ * decryption and from do_ssl3_write before encryption, s3_pkt.c.patch:39-52,
+ * 19-33).  The host-resident calls run them on the host plaintext of each
+ * record: on_read after tlsgpu_open_host has the batch in h_out (records with
+ * status >= 0, in record order), on_write before tlsgpu_seal_host copies the
+ * batch to the device (in record order; the hook may rewrite the bytes in
+ * place, not their length).  `session` and `seq` stand in for the SSL*.
+ * NULL clears a hook.  Device-resident callers run their own hook after
+ * their D2H of a delivered record. */
+typedef void (*tlsgpu_plaintext_hook)(void *user, uint32_t session, uint64_t seq, uint8_t *data,
+    uint32_t len);
+int tlsgpu_set_plaintext_hooks(tlsgpu_engine *e, tlsgpu_plaintext_hook on_read,
+    tlsgpu_plaintext_hook on_write, void *user);
 /* Pipeline shape of tlsgpu_open_host: `streams` compute streams (1..8, default
  * 2; copies in and out have a stream each), chunks of about `chunk_bytes`
  * input bytes (default 32 MiB). */

@@ -141,6 +141,9 @@ def load_library(path: str = LIBPATH) -> C.CDLL:
                                    vp, vp]),
         "tlsgpu_seal_wire_size": (u64, [i32, u32, u32, u32]),
         "tlsgpu_host_pipeline": (i32, [vp, C.c_uint, C.c_size_t]),
+        "tlsgpu_seal_host": (i32, [vp, vp, u32, vp, C.c_size_t, vp, C.c_size_t, vp]),
+        "tlsgpu_set_plaintext_hooks": (i32, [vp, vp, vp, vp]),
+        "tlsgpu_evp_cipher_stats": (i32, [C.POINTER(C.c_uint64)]),
         "tlsgpu_evp_set_batching": (i32, [C.c_uint, C.c_uint, C.c_uint]),
         "tlsgpu_evp_batch_stats": (i32, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "tlsgpu_evp_call_stats": (i32, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
@@ -413,6 +416,29 @@ def open_host(table: SessionTable, h_recs: int, n: int, h_in: int, in_bytes: int
     plaintext and statuses; synchronous, pipelined over several HIP streams."""
     _check(table.lib.tlsgpu_open_host(table.handle, h_recs, n, h_in, in_bytes, h_out, out_bytes,
                                       h_status), "tlsgpu_open_host")
+
+
+def seal_host(table: SessionTable, h_recs: int, n: int, h_in: int, in_bytes: int, h_out: int,
+              out_bytes: int, h_status: int) -> None:
+    """Host-resident batch seal (tlsgpu_seal_host)."""
+    _check(table.lib.tlsgpu_seal_host(table.handle, h_recs, n, h_in, in_bytes, h_out, out_bytes,
+                                      h_status), "tlsgpu_seal_host")
+
+
+PLAINTEXT_HOOK = C.CFUNCTYPE(None, C.c_void_p, C.c_uint32, C.c_uint64, C.POINTER(C.c_uint8),
+                             C.c_uint32)
+
+
+def set_plaintext_hooks(engine: "Engine", on_read=None, on_write=None) -> tuple:
+    """Install TaLoS-style plaintext hooks (tlsgpu_set_plaintext_hooks); Python
+    callables f(session, seq, data_ptr, length).  Returns the ctypes callbacks,
+    which the caller keeps alive while they are installed."""
+    cbs = tuple(PLAINTEXT_HOOK((lambda f: lambda u, s, q, d, n: f(s, q, d, n))(f)) if f else None
+                for f in (on_read, on_write))
+    _check(engine.lib.tlsgpu_set_plaintext_hooks(
+        engine.handle, C.cast(cbs[0], C.c_void_p) if cbs[0] else None,
+        C.cast(cbs[1], C.c_void_p) if cbs[1] else None, None), "tlsgpu_set_plaintext_hooks")
+    return cbs
 
 
 def host_pipeline(engine: "Engine", streams: int = 0, chunk_bytes: int = 0) -> None:

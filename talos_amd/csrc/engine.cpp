@@ -78,6 +78,8 @@ struct HostPipe {
   tlsgpu_record* d_recs = nullptr;
   int32_t* d_status = nullptr;
   size_t cap_in = 0, cap_out = 0, cap_recs = 0, cap_status = 0;
+  tlsgpu_plaintext_hook on_read = nullptr, on_write = nullptr;  // TaLoS hooks
+  void* hook_user = nullptr;
 };
 
 struct tlsgpu_engine {
@@ -503,9 +505,13 @@ extern "C" int tlsgpu_host_pipeline(tlsgpu_engine* e, unsigned streams, size_t c
   return TLSGPU_OK;
 }
 
-extern "C" int tlsgpu_open_host(tlsgpu_sessions* t, const tlsgpu_record* h_recs, uint32_t n,
-                                const uint8_t* h_in, size_t in_bytes, uint8_t* h_out,
-                                size_t out_bytes, int32_t* h_status) {
+// The host-resident pipeline for both directions (tlsgpu_open_host /
+// tlsgpu_seal_host).  Open: in = record fragments, out = plaintext; seal: in =
+// plaintext, out = fragments.  The TaLoS plaintext hooks run on the host
+// plaintext: after the batch for reads, before its first copy for writes.
+static int host_batch(tlsgpu_sessions* t, bool seal, const tlsgpu_record* h_recs, uint32_t n,
+                      const uint8_t* h_in, size_t in_bytes, uint8_t* h_out, size_t out_bytes,
+                      int32_t* h_status) {
   if (!t || (n && (!h_recs || !h_in || !h_out || !h_status)))
     return fail(TLSGPU_EINVAL, "bad arguments");
   if (n == 0) return TLSGPU_OK;
@@ -513,6 +519,14 @@ extern "C" int tlsgpu_open_host(tlsgpu_sessions* t, const tlsgpu_record* h_recs,
   HostPipe& hp = e->host;
   std::lock_guard<std::mutex> lk(hp.mu);
   HIPCHK(hipSetDevice(e->device));
+  if (seal && hp.on_write) {  // tls_processing_ssl_write (s3_pkt.c.patch:19-33 placement)
+    for (uint32_t i = 0; i < n; i++) {
+      const uint64_t len = h_recs[i].len_type & 0xFFFFFFu;
+      if (h_recs[i].session < t->capacity && h_recs[i].in_off + len <= in_bytes)
+        hp.on_write(hp.hook_user, h_recs[i].session, h_recs[i].seq,
+                    const_cast<uint8_t*>(h_in) + h_recs[i].in_off, (uint32_t)len);
+    }
+  }
   const bool in_place = h_out == h_in;
   if (in_place) out_bytes = in_bytes;
   while (hp.streams.size() < 2 + hp.nstreams) {
@@ -532,8 +546,9 @@ extern "C" int tlsgpu_open_host(tlsgpu_sessions* t, const tlsgpu_record* h_recs,
     *lo = std::min<uint64_t>(r.in_off, in_bytes);
     *hi = std::min<uint64_t>(r.in_off + (r.len_type & 0xFFFFFFu), in_bytes);
   };
-  // the plaintext span exactly (explicit nonce and tag excluded): a neighbouring
-  // chunk's D2H on another stream may own the next byte
+  // the output span exactly (open: the plaintext, explicit nonce and tag
+  // excluded; seal: the fragment): a neighbouring chunk's D2H on another stream
+  // may own the next byte
   auto span_out = [&](const tlsgpu_record& r, uint64_t* lo, uint64_t* hi) {
     const uint64_t len = r.len_type & 0xFFFFFFu;
     uint64_t over = 0;
@@ -542,7 +557,8 @@ extern "C" int tlsgpu_open_host(tlsgpu_sessions* t, const tlsgpu_record* h_recs,
       over = (k == TLSGPU_AES_128_GCM || k == TLSGPU_AES_256_GCM ? 8 : 0) + t->tag_lens[r.session];
     }
     *lo = std::min<uint64_t>(r.out_off, out_bytes);
-    *hi = std::min<uint64_t>(r.out_off + (len > over ? len - over : 0), out_bytes);
+    *hi = std::min<uint64_t>(r.out_off + (seal ? len + over : (len > over ? len - over : 0)),
+                             out_bytes);
   };
   // chunks of ~chunk_bytes input when the layout ascends, else one chunk
   bool ascending = true;
@@ -604,7 +620,7 @@ extern "C" int tlsgpu_open_host(tlsgpu_sessions* t, const tlsgpu_record* h_recs,
     HIPCHK(hipEventRecord(ev_in, s_in));
     HIPCHK(hipStreamWaitEvent(hs, ev_in, 0));
     const Bounds bd = {in_bytes, out_bytes};
-    const int rc = run_batch(t, hp.d_recs + a, b - a, d_in, d_out, hp.d_status + a, hs, false, false,
+    const int rc = run_batch(t, hp.d_recs + a, b - a, d_in, d_out, hp.d_status + a, hs, seal, false,
                              &bd);
     if (rc != TLSGPU_OK) return rc;
     HIPCHK(hipEventRecord(ev_done, hs));
@@ -615,6 +631,35 @@ extern "C" int tlsgpu_open_host(tlsgpu_sessions* t, const tlsgpu_record* h_recs,
   HIPCHK(hipMemcpyAsync(h_status, hp.d_status, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost,
                         s_out));
   for (hipStream_t hs : hp.streams) HIPCHK(hipStreamSynchronize(hs));
+  if (!seal && hp.on_read) {  // tls_processing_ssl_read (s3_pkt.c.patch:39-52 placement)
+    for (uint32_t i = 0; i < n; i++)
+      if (h_status[i] >= 0)
+        hp.on_read(hp.hook_user, h_recs[i].session, h_recs[i].seq, h_out + h_recs[i].out_off,
+                   (uint32_t)h_status[i]);
+  }
+  return TLSGPU_OK;
+}
+
+extern "C" int tlsgpu_open_host(tlsgpu_sessions* t, const tlsgpu_record* h_recs, uint32_t n,
+                                const uint8_t* h_in, size_t in_bytes, uint8_t* h_out,
+                                size_t out_bytes, int32_t* h_status) {
+  return host_batch(t, false, h_recs, n, h_in, in_bytes, h_out, out_bytes, h_status);
+}
+
+extern "C" int tlsgpu_seal_host(tlsgpu_sessions* t, const tlsgpu_record* h_recs, uint32_t n,
+                                const uint8_t* h_in, size_t in_bytes, uint8_t* h_out,
+                                size_t out_bytes, int32_t* h_status) {
+  if (h_out == h_in && n) return fail(TLSGPU_EINVAL, "tlsgpu_seal_host cannot run in place");
+  return host_batch(t, true, h_recs, n, h_in, in_bytes, h_out, out_bytes, h_status);
+}
+
+extern "C" int tlsgpu_set_plaintext_hooks(tlsgpu_engine* e, tlsgpu_plaintext_hook on_read,
+                                          tlsgpu_plaintext_hook on_write, void* user) {
+  if (!e) return fail(TLSGPU_EINVAL, "null engine");
+  std::lock_guard<std::mutex> lk(e->host.mu);
+  e->host.on_read = on_read;
+  e->host.on_write = on_write;
+  e->host.hook_user = user;
   return TLSGPU_OK;
 }
 
