@@ -227,6 +227,14 @@ main(int argc, char **argv)
 		if (ta[i].secs > secs)
 			secs = ta[i].secs;
 	}
+	int (*bstats)(uint64_t *, uint64_t *) =
+	    (int (*)(uint64_t *, uint64_t *))dlsym(h, "tlsgpu_evp_batch_stats");
+	uint64_t nb = 0, nj = 0;
+	if (bstats)
+		bstats(&nb, &nj);
+	if (nb)
+		fprintf(stderr, "{\"evp_batches\": %llu, \"evp_jobs\": %llu}\n", (unsigned long long)nb,
+		    (unsigned long long)nj);
 	printf("{\"aead\": \"%s\", \"op\": \"%s\", \"rec_len\": %zu, \"threads\": %d, "
 	    "\"records\": %llu, \"bytes\": %llu, \"seconds\": %.4f, "
 	    "\"gib_per_s\": %.4f, \"failures\": %llu}\n",

@@ -21,6 +21,10 @@
 #include <mutex>
 #include <new>
 #include <unistd.h>
+#include <climits>
+#include <deque>
+#include <linux/futex.h>
+#include <sys/syscall.h>
 #include <thread>
 #include <vector>
 
@@ -372,9 +376,14 @@ struct Bounds {
   uint64_t in_bytes, out_bytes;
 };
 
+// `kinds`: bit k set = the batch may hold records of AEAD kind k (a kernel is
+// launched only for kinds that are installed AND in the mask; the EVP queue
+// passes the kinds its jobs use).
 static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const uint8_t* d_in,
                      uint8_t* d_out, int32_t* d_status, hipStream_t s, bool seal, bool raw,
-                     const Bounds* bounds = nullptr) {
+                     const Bounds* bounds = nullptr, unsigned kinds = ~0u) {
+  bool have[5];
+  for (int k = 0; k < 5; k++) have[k] = t->have[k] && ((kinds >> k) & 1u);
   BatchArgs a = {};
   a.sessions = t->d_sess;
   a.gcm_tables = t->d_gcm;
@@ -391,11 +400,18 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   a.pack = g_pack;
   a.pws = g_pws;
   int groups = groups_for(t->eng, n, &a.records_per_group);
+  if (raw) {
+    // raw EVP jobs: latency, not throughput — one workgroup per job, so a
+    // batch of jobs on different contexts runs side by side instead of one
+    // session run (table rebuild) after another inside one workgroup
+    a.records_per_group = 1;
+    groups = (int)n;
+  }
   // records whose session is empty/invalid keep this status
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)d_status, (int)TLSGPU_REC_PUBLIC_INVALID, n, s));
   const int impl = raw ? TLSGPU_GCM_TTABLE : g_gcm_impl.load();
   const bool gcm_pre =
-      impl != TLSGPU_GCM_TTABLE && (t->have[TLSGPU_AES_128_GCM] || t->have[TLSGPU_AES_256_GCM]);
+      impl != TLSGPU_GCM_TTABLE && (have[TLSGPU_AES_128_GCM] || have[TLSGPU_AES_256_GCM]);
   // per-stream scratch: [RecPre x n (queue kernels) | kCtlBytes control words |
   // checked descriptors x n].  Control words per key size k (0: AES-128, 1:
   // AES-256): selection words at 16 k, per-workgroup record counters of the
@@ -423,7 +439,7 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
     if (impl == TLSGPU_GCM_QUEUE) HIPCHK(hipMemsetAsync(ctl, 0, kCtlBytes, s));
   }
   for (int rounds : {10, 14}) {
-    if (!t->have[rounds == 10 ? TLSGPU_AES_128_GCM : TLSGPU_AES_256_GCM]) continue;
+    if (!have[rounds == 10 ? TLSGPU_AES_128_GCM : TLSGPU_AES_256_GCM]) continue;
     // selection words and counters per key size: a short AES-128 record must
     // not send the AES-256 pass to the pack variant
     if (ctl && impl == TLSGPU_GCM_QUEUE) {
@@ -456,7 +472,7 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
                   hipGetErrorString(hipGetLastError()));
     }
   }
-  if ((t->have[TLSGPU_CHACHA20_POLY1305] || t->have[TLSGPU_CHACHA20_POLY1305_OLD]) &&
+  if ((have[TLSGPU_CHACHA20_POLY1305] || have[TLSGPU_CHACHA20_POLY1305_OLD]) &&
       launch_chacha(a, seal, raw, groups, s))
     return fail(TLSGPU_EHIP, "chacha launch: %s", hipGetErrorString(hipGetLastError()));
   return TLSGPU_OK;
@@ -896,67 +912,126 @@ struct AeadState {
 //
 // With batching on (tlsgpu_evp_set_batching or TLSGPU_EVP_BATCH_US > 0),
 // EVP_AEAD_CTX_init installs the key into a slot of one shared device session
-// pool, and every EVP_AEAD_CTX_seal/open posts a job and blocks on it.  A
-// dispatcher thread collects the jobs that arrive within the window (or
-// max_jobs), packs their inputs into one pinned staging buffer, runs ONE raw
-// batch per direction over all of them (jobs sorted by session so the GCM
-// kernel reloads its tables once per context), copies the outputs back and
-// wakes the callers.  Results are the same as the per-call path, bit for bit;
-// calls stay synchronous for the caller, throughput comes from concurrency.
-struct EvpJob {
-  const AeadState* st;
-  bool seal;
-  unsigned char* out;
-  size_t max_out;
-  const unsigned char *nonce, *in, *ad;
-  size_t nonce_len, in_len, ad_len;
-  int32_t status;
-  bool done;
-  bool failed;
+// pool, and every EVP_AEAD_CTX_seal/open joins the batch being built and
+// blocks until it completes.  Batches live in a ring of kEvpSlots staging
+// slots (pinned host + device, one HIP stream each):
+//   caller      reserves a descriptor and byte ranges in the building slot
+//               (under the lock), copies its nonce / AD / input into the
+//               pinned slot itself (outside the lock, in parallel with the
+//               other callers), then sleeps on the slot's futex word;
+//   dispatcher  closes the building slot when the GPU is idle, the slot is
+//               full, or the window since its first job has passed; waits for
+//               the slot's writers, then issues one H2D, one raw batch per
+//               direction, one D2H and an event on the slot's stream;
+//   completer   waits on the events in order and wakes each slot's callers
+//               with ONE futex wake; every caller copies its own output out,
+//               and the last one returns the slot to the ring.
+// So at most kEvpSlots-1 batches are in flight while the next one fills, no
+// per-job work runs on the dispatcher, and results are the per-call path's,
+// bit for bit (same raw kernels).
+constexpr uint32_t kEvpSlots = 3;
+constexpr uint32_t kEvpMaxJobs = 1024;
+constexpr size_t kEvpDescBytes = sizeof(RawJob) * kEvpMaxJobs;
+constexpr size_t kEvpInBytes = 8u << 20, kEvpOutBytes = 8u << 20;
+constexpr size_t kEvpStatusOff = kEvpDescBytes + kEvpInBytes;   // int32 x kEvpMaxJobs
+constexpr size_t kEvpOutOff = kEvpStatusOff + 4 * kEvpMaxJobs;
+constexpr size_t kEvpSlotBytes = kEvpOutOff + kEvpOutBytes;
+
+struct EvpSlot {
+  uint8_t* h = nullptr;  // pinned: [RawJob x kEvpMaxJobs | inputs | status | outputs]
+  uint8_t* d = nullptr;  // device, same layout
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  // built under EvpBatcher::mu: seal descriptors from the front, open ones
+  // from the back, so each direction is one contiguous raw batch
+  uint32_t nseal = 0, nopen = 0;
+  unsigned kinds_seal = 0, kinds_open = 0;  // AEAD kinds present (run_batch masks)
+  size_t in_used = 0, out_used = 0;
+  std::chrono::steady_clock::time_point first, submitted_at;
+  std::atomic<uint32_t> writers{0};  // callers still copying in
+  std::atomic<uint32_t> readers{0};  // callers still copying out
+  std::atomic<uint32_t> gen{0};      // bumped on completion (futex word)
+  bool ok = false;
+  uint32_t jobs() const { return nseal + nopen; }
 };
 
 struct EvpBatcher {
   std::mutex mu;
-  std::condition_variable cv_work, cv_done;
-  std::vector<EvpJob*> q;
-  std::thread th;
-  bool stop = false;
-  unsigned window_us = 0, max_jobs = 4096;
+  std::condition_variable cv_disp, cv_comp, cv_slot;
+  EvpSlot slots[kEvpSlots];
+  EvpSlot* building = nullptr;  // the slot callers join (nullptr: all busy)
+  std::vector<EvpSlot*> free_ring;
+  std::deque<EvpSlot*> submitted;
+  uint32_t inflight = 0;
+  bool full = false;  // a caller found the building slot full
+  std::thread disp, comp;
+  unsigned window_us = 0, max_jobs = kEvpMaxJobs;
   tlsgpu_sessions* pool = nullptr;
-  std::vector<int> free_slots;
-  hipStream_t stream = nullptr;
-  uint8_t* h_stage = nullptr;
-  uint8_t* d_stage = nullptr;
-  size_t cap = 0;
+  std::vector<int> free_sessions;
   uint64_t batches = 0, jobs_done = 0;
-  void run(std::vector<EvpJob*>& jobs);
-  void loop();
+  // TLSGPU_EVP_STATS=1: nanoseconds summed over batches (printed at exit)
+  uint64_t ns_wait = 0, ns_writers = 0, ns_submit = 0, ns_gpu = 0;
+  void dispatch_loop();
+  void complete_loop();
+  void submit(EvpSlot* s);
+  void release(EvpSlot* s);
 };
 static EvpBatcher* g_batcher = nullptr;
 static std::mutex g_batcher_mu;
 
-// Per-thread staging for one call: device buffer + stream (calls on one ctx may
-// run concurrently from several threads, evp.h:1273-1274).
+static inline void futex_wait(std::atomic<uint32_t>* w, uint32_t v) {
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAIT_PRIVATE, v, nullptr, nullptr, 0);
+}
+static inline void futex_wake_all(std::atomic<uint32_t>* w) {
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAKE_PRIVATE, INT_MAX, nullptr, nullptr,
+          0);
+}
+
+// Per-thread staging for one call: pinned host + device buffer and a stream
+// (calls on one ctx may run concurrently from several threads,
+// evp.h:1273-1274).  Layout [RawJob | nonce | ad | in | status | out], so one
+// H2D covers the job up to its preset status and one D2H status and output.
+// Threads share kCallStreams streams per process (more streams than the
+// hardware queues, GPU_MAX_HW_QUEUES = 4, cost 3x in call rate at 64 threads:
+// tools/hip_latency); each thread waits on its own event, i.e. on its own
+// work and what was queued before it on that stream.
+constexpr int kCallStreams = 4;
+static hipStream_t g_call_streams[kCallStreams];
+static std::once_flag g_call_streams_once;
+static std::atomic<uint32_t> g_call_thread_seq{0};
+
 struct Staging {
   int device = -1;
   hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
   uint8_t* d_buf = nullptr;
+  uint8_t* h_buf = nullptr;
   size_t cap = 0;
   ~Staging() {
     if (d_buf) (void)hipFree(d_buf);
-    if (stream) (void)hipStreamDestroy(stream);
+    if (h_buf) (void)hipHostFree(h_buf);
+    if (done) (void)hipEventDestroy(done);
   }
   bool ensure(int dev, size_t bytes) {
     if (hipSetDevice(dev) != hipSuccess) return false;
-    if (!stream && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess)
-      return false;
+    if (!stream) {
+      bool ok = true;
+      std::call_once(g_call_streams_once, [&] {
+        for (hipStream_t& cs : g_call_streams)
+          ok &= hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) == hipSuccess;
+      });
+      if (!ok || hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess) return false;
+      stream = g_call_streams[g_call_thread_seq.fetch_add(1) % kCallStreams];
+    }
     device = dev;
     if (cap >= bytes) return true;
     if (d_buf) (void)hipFree(d_buf);
-    d_buf = nullptr;
+    if (h_buf) (void)hipHostFree(h_buf);
+    d_buf = h_buf = nullptr;
     cap = 0;
     size_t want = bytes < (1u << 20) ? (1u << 20) : bytes;
     if (hipMalloc(&d_buf, want) != hipSuccess) return false;
+    if (hipHostMalloc((void**)&h_buf, want, hipHostMallocDefault) != hipSuccess) return false;
     cap = want;
     return true;
   }
@@ -988,9 +1063,9 @@ extern "C" int EVP_AEAD_CTX_init(EVP_AEAD_CTX* ctx, const EVP_AEAD* aead, const 
   st->slot = -1;
   {
     std::lock_guard<std::mutex> lk(g_batcher_mu);
-    if (g_batcher && !g_batcher->free_slots.empty()) {
-      st->slot = g_batcher->free_slots.back();
-      g_batcher->free_slots.pop_back();
+    if (g_batcher && !g_batcher->free_sessions.empty()) {
+      st->slot = g_batcher->free_sessions.back();
+      g_batcher->free_sessions.pop_back();
       st->sess = g_batcher->pool;
     }
   }
@@ -1014,7 +1089,7 @@ extern "C" int EVP_AEAD_CTX_init(EVP_AEAD_CTX* ctx, const EVP_AEAD* aead, const 
       tlsgpu_sessions_destroy(st->sess);
     } else {
       std::lock_guard<std::mutex> lk(g_batcher_mu);
-      g_batcher->free_slots.push_back(st->slot);
+      g_batcher->free_sessions.push_back(st->slot);
     }
     delete st;
     return 0;
@@ -1037,7 +1112,7 @@ extern "C" void EVP_AEAD_CTX_cleanup(EVP_AEAD_CTX* ctx) {
     (void)hipMemset(st->sess->d_gcm + slot, 0, sizeof(DevGcmTables));
     if (pooled) {
       std::lock_guard<std::mutex> lk(g_batcher_mu);
-      g_batcher->free_slots.push_back((int)slot);
+      g_batcher->free_sessions.push_back((int)slot);
     } else {
       tlsgpu_sessions_destroy(st->sess);
     }
@@ -1079,78 +1154,72 @@ static int gpu_call(const AeadState* st, bool seal, unsigned char* out, size_t* 
   return r;
 }
 
-// Layout of the per-call staging buffer:
-// [RawJob | status | nonce | ad | in | out] each 256-B aligned.
+static int evp_queue_call(EvpBatcher* b, const AeadState* st, bool seal, unsigned char* out,
+                          size_t* out_len, size_t max_out_len, const unsigned char* nonce,
+                          size_t nonce_len, const unsigned char* in, size_t in_len,
+                          const unsigned char* ad, size_t ad_len);
+
 static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, size_t* out_len,
                          size_t max_out_len, const unsigned char* nonce, size_t nonce_len,
                          const unsigned char* in, size_t in_len, const unsigned char* ad,
                          size_t ad_len) {
-  if (st->slot & 0x40000000) {  // pooled context: post to the coalescing queue
-    EvpJob j = {st, seal, out, max_out_len, nonce, in, ad, nonce_len, in_len, ad_len,
-                TLSGPU_REC_BAD_MAC, false, false};
-    EvpBatcher* b = g_batcher;
-    std::unique_lock<std::mutex> lk(b->mu);
-    b->q.push_back(&j);
-    b->cv_work.notify_one();
-    b->cv_done.wait(lk, [&] { return j.done; });
-    lk.unlock();
-    if (j.failed) return -1;
-    if (j.status < 0) return 0;
-    *out_len = (size_t)j.status;
-    return 1;
+  const bool pooled = (st->slot & 0x40000000) != 0;
+  if (pooled) {  // pooled context: join the coalescing queue (large jobs run alone)
+    int r = evp_queue_call(g_batcher, st, seal, out, out_len, max_out_len, nonce, nonce_len, in,
+                           in_len, ad, ad_len);
+    if (r != -2) return r;
   }
-  auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-  size_t out_bytes = seal ? in_len + st->tag_len : (max_out_len > in_len ? max_out_len : in_len);
-  size_t o_job = 0, o_status = al(sizeof(RawJob)), o_nonce = o_status + 256;
-  size_t o_ad = o_nonce + al(nonce_len + 1), o_in = o_ad + al(ad_len + 1);
-  size_t o_out = o_in + al(in_len + 1), total = o_out + al(out_bytes + 1);
+  auto al = [](size_t v) { return (v + 15) & ~(size_t)15; };
+  const size_t out_bytes = seal ? in_len + st->tag_len : std::max(max_out_len, in_len);
+  const size_t o_nonce = al(sizeof(RawJob)), o_ad = o_nonce + al(nonce_len);
+  const size_t o_in = o_ad + al(ad_len), o_status = o_in + al(in_len);
+  const size_t o_out = o_status + 16, total = o_out + al(out_bytes + 1);
   tlsgpu_engine* e = st->sess->eng;
   if (!t_stage.ensure(e->device, total)) return -1;
-  uint8_t* b = t_stage.d_buf;
+  uint8_t* d = t_stage.d_buf;
+  uint8_t* h = t_stage.h_buf;
   hipStream_t s = t_stage.stream;
-  RawJob j;
-  j.in = (uint64_t)(b + o_in);
-  j.out = (uint64_t)(b + o_out);
-  j.nonce = (uint64_t)(b + o_nonce);
-  j.aad = (uint64_t)(b + o_ad);
-  j.in_len = (uint32_t)in_len;
-  j.nonce_len = (uint32_t)nonce_len;
-  j.aad_len = (uint32_t)ad_len;
-  j.session = 0;
-  j.max_out = max_out_len;
-  if (hipMemcpyAsync(b + o_job, &j, sizeof(j), hipMemcpyHostToDevice, s) != hipSuccess) return -1;
-  if (nonce_len && hipMemcpyAsync(b + o_nonce, nonce, nonce_len, hipMemcpyHostToDevice, s)) return -1;
-  if (ad_len && hipMemcpyAsync(b + o_ad, ad, ad_len, hipMemcpyHostToDevice, s)) return -1;
-  if (in_len && hipMemcpyAsync(b + o_in, in, in_len, hipMemcpyHostToDevice, s)) return -1;
+  RawJob* j = reinterpret_cast<RawJob*>(h);
+  j->in = (uint64_t)(d + o_in);
+  j->out = (uint64_t)(d + o_out);
+  j->nonce = (uint64_t)(d + o_nonce);
+  j->aad = (uint64_t)(d + o_ad);
+  j->in_len = (uint32_t)in_len;
+  j->nonce_len = (uint32_t)nonce_len;
+  j->aad_len = (uint32_t)ad_len;
+  j->session = (uint32_t)(st->slot & 0x3FFFFFFF);
+  j->max_out = max_out_len;
+  if (nonce_len) memcpy(h + o_nonce, nonce, nonce_len);
+  if (ad_len) memcpy(h + o_ad, ad, ad_len);
+  if (in_len) memcpy(h + o_in, in, in_len);
+  // a job the kernel rejects keeps this status (never a stale one)
+  *reinterpret_cast<int32_t*>(h + o_status) = TLSGPU_REC_PUBLIC_INVALID;
+  if (hipMemcpyAsync(d, h, o_status + 4, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
   BatchArgs a = {};
   a.sessions = st->sess->d_sess;
   a.gcm_tables = st->sess->d_gcm;
-  a.descs = b + o_job;
+  a.descs = d;
   a.n = 1;
   a.records_per_group = 1;
-  a.in = nullptr;
-  a.out = nullptr;
-  a.status = (int32_t*)(b + o_status);
+  a.status = reinterpret_cast<int32_t*>(d + o_status);
   a.n_sessions = st->sess->capacity;
-  // a job the kernel rejects keeps this status (never a stale one)
-  if (hipMemsetD32Async((hipDeviceptr_t)a.status, (int)TLSGPU_REC_PUBLIC_INVALID, 1, s) != hipSuccess)
-    return -1;
-  bool gcm = st->kind == TLSGPU_AES_128_GCM || st->kind == TLSGPU_AES_256_GCM;
+  const bool gcm = st->kind == TLSGPU_AES_128_GCM || st->kind == TLSGPU_AES_256_GCM;
   int rc = gcm ? launch_gcm(a, seal, true, st->kind == TLSGPU_AES_128_GCM ? 10 : 14, 1, s)
                : launch_chacha(a, seal, true, 1, s);
   if (rc) return -1;
-  int32_t status = TLSGPU_REC_BAD_MAC;
-  if (hipMemcpyAsync(&status, b + o_status, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
-  if (hipStreamSynchronize(s) != hipSuccess) return -1;
-  if (status < 0) {
-    // the kernel zero-filled max_out_len bytes of its output region
-    if (max_out_len &&
-        hipMemcpy(out, b + o_out, max_out_len, hipMemcpyDeviceToHost) != hipSuccess)
-      memset(out, 0, max_out_len);
+  // success writes at most in_len + tag (seal) / in_len - tag (open) bytes
+  const size_t back = seal ? in_len + st->tag_len : std::min(max_out_len, in_len);
+  if (hipMemcpyAsync(h + o_status, d + o_status, o_out - o_status + back, hipMemcpyDeviceToHost,
+                     s) != hipSuccess ||
+      hipEventRecord(t_stage.done, s) != hipSuccess ||
+      hipEventSynchronize(t_stage.done) != hipSuccess)
+    return -1;
+  const int32_t status = *reinterpret_cast<const int32_t*>(h + o_status);
+  if (status < 0) {  // the kernel's zero-fill of max_out_len bytes (evp_aead.c:137-143)
+    if (max_out_len) memset(out, 0, max_out_len);
     return 0;
   }
-  if (status && hipMemcpy(out, b + o_out, (size_t)status, hipMemcpyDeviceToHost) != hipSuccess)
-    return -1;
+  if (status) memcpy(out, h + o_out, (size_t)status);
   *out_len = (size_t)status;
   return 1;
 }
@@ -1583,115 +1652,176 @@ extern "C" int tlsgpu_evp_cipher_stats(uint64_t* programs) {
 }
 
 // ---------------------------------------------------------------------------
-// EVP coalescing queue: dispatcher
+// EVP coalescing queue: callers, dispatcher, completer
 
-void EvpBatcher::loop() {
-  std::unique_lock<std::mutex> lk(mu);
+// 1 / 0 / -1 as gpu_call; -2: the job is too large for a staging slot (the
+// caller runs it on its own staging instead).
+static int evp_queue_call(EvpBatcher* b, const AeadState* st, bool seal, unsigned char* out,
+                          size_t* out_len, size_t max_out_len, const unsigned char* nonce,
+                          size_t nonce_len, const unsigned char* in, size_t in_len,
+                          const unsigned char* ad, size_t ad_len) {
+  auto al = [](size_t v) { return (v + 15) & ~(size_t)15; };
+  const size_t need_in = al(nonce_len) + al(ad_len) + al(in_len);
+  const size_t out_bytes = seal ? in_len + st->tag_len : std::max(max_out_len, in_len);
+  const size_t need_out = al(out_bytes + 1);
+  if (need_in > kEvpInBytes / 4 || need_out > kEvpOutBytes / 4) return -2;
+  std::unique_lock<std::mutex> lk(b->mu);
+  EvpSlot* s;
   for (;;) {
-    cv_work.wait(lk, [&] { return stop || !q.empty(); });
-    if (q.empty() && stop) return;
-    const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(window_us);
-    while (!stop && q.size() < max_jobs &&
-           cv_work.wait_until(lk, deadline) != std::cv_status::timeout) {
+    s = b->building;
+    if (s && s->jobs() < b->max_jobs && s->in_used + need_in <= kEvpInBytes &&
+        s->out_used + need_out <= kEvpOutBytes)
+      break;
+    if (s && !b->full) {  // no room: have it dispatched now
+      b->full = true;
+      b->cv_disp.notify_one();
     }
-    std::vector<EvpJob*> jobs;
-    const size_t take = std::min<size_t>(q.size(), max_jobs);
-    jobs.assign(q.begin(), q.begin() + take);
-    q.erase(q.begin(), q.begin() + take);
-    lk.unlock();
-    run(jobs);
-    lk.lock();
-    for (EvpJob* j : jobs) j->done = true;
-    batches++;
-    jobs_done += jobs.size();
-    cv_done.notify_all();
+    b->cv_slot.wait(lk);
+  }
+  const bool first = s->jobs() == 0;
+  const uint32_t idx = seal ? s->nseal++ : kEvpMaxJobs - 1 - s->nopen++;
+  (seal ? s->kinds_seal : s->kinds_open) |= 1u << st->kind;
+  const size_t io = kEvpDescBytes + s->in_used, oo = kEvpOutOff + s->out_used;
+  s->in_used += need_in;
+  s->out_used += need_out;
+  s->writers.fetch_add(1, std::memory_order_relaxed);
+  const uint32_t gen = s->gen.load(std::memory_order_relaxed);
+  if (first) {
+    s->first = std::chrono::steady_clock::now();
+    b->cv_disp.notify_one();
+  }
+  lk.unlock();
+  RawJob* rj = reinterpret_cast<RawJob*>(s->h) + idx;
+  size_t o = io;
+  rj->nonce = (uint64_t)(s->d + o);
+  if (nonce_len) memcpy(s->h + o, nonce, nonce_len);
+  o += al(nonce_len);
+  rj->aad = (uint64_t)(s->d + o);
+  if (ad_len) memcpy(s->h + o, ad, ad_len);
+  o += al(ad_len);
+  rj->in = (uint64_t)(s->d + o);
+  if (in_len) memcpy(s->h + o, in, in_len);
+  rj->out = (uint64_t)(s->d + oo);
+  rj->in_len = (uint32_t)in_len;
+  rj->nonce_len = (uint32_t)nonce_len;
+  rj->aad_len = (uint32_t)ad_len;
+  rj->session = (uint32_t)(st->slot & 0x3FFFFFFF);
+  rj->max_out = max_out_len;
+  s->writers.fetch_sub(1, std::memory_order_release);
+  while (s->gen.load(std::memory_order_acquire) == gen) futex_wait(&s->gen, gen);
+  int r;
+  if (!s->ok) {
+    r = -1;
+  } else {
+    const int32_t status = reinterpret_cast<const int32_t*>(s->h + kEvpStatusOff)[idx];
+    if (status < 0) {  // the kernel's zero-fill (evp_aead.c:137-143)
+      if (max_out_len) memset(out, 0, max_out_len);
+      r = 0;
+    } else {
+      if (status) memcpy(out, s->h + oo, (size_t)status);
+      *out_len = (size_t)status;
+      r = 1;
+    }
+  }
+  if (s->readers.fetch_sub(1, std::memory_order_acq_rel) == 1) b->release(s);
+  return r;
+}
+
+// The last reader hands the slot back: it becomes the building slot if there
+// is none, else waits in the ring.
+void EvpBatcher::release(EvpSlot* s) {
+  std::lock_guard<std::mutex> lk(mu);
+  s->nseal = s->nopen = 0;
+  s->kinds_seal = s->kinds_open = 0;
+  s->in_used = s->out_used = 0;
+  if (!building) {
+    building = s;
+    full = false;
+    cv_slot.notify_all();
+  } else {
+    free_ring.push_back(s);
   }
 }
 
-void EvpBatcher::run(std::vector<EvpJob*>& jobs) {
-  // one raw batch per direction; sessions grouped inside each
-  std::stable_sort(jobs.begin(), jobs.end(), [](const EvpJob* a, const EvpJob* b) {
-    if (a->seal != b->seal) return a->seal > b->seal;
-    return (a->st->slot & 0x3FFFFFFF) < (b->st->slot & 0x3FFFFFFF);
-  });
-  const size_t n = jobs.size();
-  auto al = [](size_t v) { return (v + 15) & ~(size_t)15; };
-  // layout: [RawJob x n][status x n][inputs ...][outputs ...]
-  const size_t o_status = al(sizeof(RawJob) * n);
-  size_t o = al(o_status + 4 * n);
-  std::vector<size_t> o_nonce(n), o_ad(n), o_in(n), o_out(n), out_bytes(n);
-  for (size_t i = 0; i < n; i++) {
-    const EvpJob* j = jobs[i];
-    o_nonce[i] = o; o = al(o + j->nonce_len);
-    o_ad[i] = o;    o = al(o + j->ad_len);
-    o_in[i] = o;    o = al(o + j->in_len);
-  }
-  const size_t o_outputs = o;
-  for (size_t i = 0; i < n; i++) {
-    const EvpJob* j = jobs[i];
-    out_bytes[i] = j->seal ? j->in_len + j->st->tag_len : std::max(j->max_out, j->in_len);
-    o_out[i] = o;
-    o = al(o + out_bytes[i] + 1);
-  }
-  const size_t total = o;
-  auto fail_all = [&] {
-    for (EvpJob* j : jobs) j->failed = true;
-  };
-  if (hipSetDevice(pool->eng->device) != hipSuccess) return fail_all();
-  if (cap < total) {
-    if (h_stage) (void)hipHostFree(h_stage);
-    if (d_stage) (void)hipFree(d_stage);
-    h_stage = nullptr;
-    d_stage = nullptr;
-    cap = 0;
-    size_t want = std::max(total, (size_t)(4u << 20));
-    if (hipHostMalloc((void**)&h_stage, want, hipHostMallocDefault) != hipSuccess ||
-        hipMalloc((void**)&d_stage, want) != hipSuccess)
-      return fail_all();
-    cap = want;
-  }
-  RawJob* rj = reinterpret_cast<RawJob*>(h_stage);
-  for (size_t i = 0; i < n; i++) {
-    const EvpJob* j = jobs[i];
-    if (j->nonce_len) memcpy(h_stage + o_nonce[i], j->nonce, j->nonce_len);
-    if (j->ad_len) memcpy(h_stage + o_ad[i], j->ad, j->ad_len);
-    if (j->in_len) memcpy(h_stage + o_in[i], j->in, j->in_len);
-    rj[i].in = (uint64_t)(d_stage + o_in[i]);
-    rj[i].out = (uint64_t)(d_stage + o_out[i]);
-    rj[i].nonce = (uint64_t)(d_stage + o_nonce[i]);
-    rj[i].aad = (uint64_t)(d_stage + o_ad[i]);
-    rj[i].in_len = (uint32_t)j->in_len;
-    rj[i].nonce_len = (uint32_t)j->nonce_len;
-    rj[i].aad_len = (uint32_t)j->ad_len;
-    rj[i].session = (uint32_t)(j->st->slot & 0x3FFFFFFF);
-    rj[i].max_out = j->max_out;
-  }
-  if (hipMemcpyAsync(d_stage, h_stage, o_outputs, hipMemcpyHostToDevice, stream) != hipSuccess)
-    return fail_all();
-  size_t nseal = 0;
-  while (nseal < n && jobs[nseal]->seal) nseal++;
-  int32_t* d_status = reinterpret_cast<int32_t*>(d_stage + o_status);
-  if (nseal && run_batch(pool, d_stage, (uint32_t)nseal, nullptr, nullptr, d_status, stream, true,
-                         true) != TLSGPU_OK)
-    return fail_all();
-  if (n > nseal && run_batch(pool, d_stage + sizeof(RawJob) * nseal, (uint32_t)(n - nseal), nullptr,
-                             nullptr, d_status + nseal, stream, false, true) != TLSGPU_OK)
-    return fail_all();
-  if (hipMemcpyAsync(h_stage + o_status, d_stage + o_status, 4 * n, hipMemcpyDeviceToHost,
-                     stream) != hipSuccess ||
-      hipMemcpyAsync(h_stage + o_outputs, d_stage + o_outputs, total - o_outputs,
-                     hipMemcpyDeviceToHost, stream) != hipSuccess ||
-      hipStreamSynchronize(stream) != hipSuccess)
-    return fail_all();
-  const int32_t* hs = reinterpret_cast<const int32_t*>(h_stage + o_status);
-  for (size_t i = 0; i < n; i++) {
-    EvpJob* j = jobs[i];
-    j->status = hs[i];
-    if (hs[i] >= 0) {
-      if (hs[i]) memcpy(j->out, h_stage + o_out[i], (size_t)hs[i]);
-    } else if (j->max_out) {
-      memcpy(j->out, h_stage + o_out[i], j->max_out);  // the kernel's zero-fill
+void EvpBatcher::dispatch_loop() {
+  std::unique_lock<std::mutex> lk(mu);
+  for (;;) {
+    cv_disp.wait(lk, [&] { return building && building->jobs() > 0; });
+    // batching policy: go now when the GPU is idle or the slot is full,
+    // else when the window since the slot's first job has passed
+    const auto deadline = building->first + std::chrono::microseconds(window_us);
+    cv_disp.wait_until(lk, deadline, [&] { return inflight == 0 || full; });
+    EvpSlot* s = building;
+    full = false;
+    const auto t_close = std::chrono::steady_clock::now();
+    ns_wait += std::chrono::duration_cast<std::chrono::nanoseconds>(t_close - s->first).count();
+    if (free_ring.empty()) {
+      building = nullptr;
+    } else {
+      building = free_ring.back();
+      free_ring.pop_back();
+      cv_slot.notify_all();
     }
+    inflight++;
+    s->readers.store(s->jobs(), std::memory_order_relaxed);
+    lk.unlock();
+    while (s->writers.load(std::memory_order_acquire)) std::this_thread::yield();
+    const auto t_sub = std::chrono::steady_clock::now();
+    submit(s);
+    s->submitted_at = std::chrono::steady_clock::now();
+    lk.lock();
+    ns_writers += std::chrono::duration_cast<std::chrono::nanoseconds>(t_sub - t_close).count();
+    ns_submit +=
+        std::chrono::duration_cast<std::chrono::nanoseconds>(s->submitted_at - t_sub).count();
+    submitted.push_back(s);
+    cv_comp.notify_one();
+  }
+}
+
+void EvpBatcher::submit(EvpSlot* s) {
+  s->ok = false;
+  if (hipSetDevice(pool->eng->device) != hipSuccess) return;
+  const uint32_t ns = s->nseal, no = s->nopen;
+  int32_t* d_status = reinterpret_cast<int32_t*>(s->d + kEvpStatusOff);
+  const RawJob* d_desc = reinterpret_cast<const RawJob*>(s->d);
+  if (hipMemcpyAsync(s->d, s->h, kEvpDescBytes + s->in_used, hipMemcpyHostToDevice, s->stream) !=
+      hipSuccess)
+    return;
+  if (ns && run_batch(pool, d_desc, ns, nullptr, nullptr, d_status, s->stream, true, true,
+                     nullptr, s->kinds_seal) != TLSGPU_OK)
+    return;
+  if (no && run_batch(pool, d_desc + (kEvpMaxJobs - no), no, nullptr, nullptr,
+                      d_status + (kEvpMaxJobs - no), s->stream, false, true, nullptr,
+                      s->kinds_open) != TLSGPU_OK)
+    return;
+  if (hipMemcpyAsync(s->h + kEvpStatusOff, s->d + kEvpStatusOff,
+                     kEvpOutOff - kEvpStatusOff + s->out_used, hipMemcpyDeviceToHost,
+                     s->stream) != hipSuccess ||
+      hipEventRecord(s->done, s->stream) != hipSuccess)
+    return;
+  s->ok = true;
+}
+
+void EvpBatcher::complete_loop() {
+  std::unique_lock<std::mutex> lk(mu);
+  for (;;) {
+    cv_comp.wait(lk, [&] { return !submitted.empty(); });
+    EvpSlot* s = submitted.front();
+    submitted.pop_front();
+    lk.unlock();
+    if (s->ok && hipEventSynchronize(s->done) != hipSuccess) s->ok = false;
+    const uint64_t gpu_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                std::chrono::steady_clock::now() - s->submitted_at)
+                                .count();
+    const uint32_t n = s->jobs();
+    s->gen.fetch_add(1, std::memory_order_release);
+    futex_wake_all(&s->gen);
+    lk.lock();
+    batches++;
+    jobs_done += n;
+    ns_gpu += gpu_ns;
+    inflight--;
+    cv_disp.notify_one();
   }
 }
 
@@ -1701,7 +1831,7 @@ extern "C" int tlsgpu_evp_set_batching(unsigned window_us, unsigned max_jobs,
   if (g_batcher) {  // already running: adjust the window / batch size only
     std::lock_guard<std::mutex> lk2(g_batcher->mu);
     g_batcher->window_us = window_us;
-    if (max_jobs) g_batcher->max_jobs = max_jobs;
+    if (max_jobs) g_batcher->max_jobs = std::min(max_jobs, kEvpMaxJobs);
     return TLSGPU_OK;
   }
   if (window_us == 0 && max_jobs == 0) return TLSGPU_OK;  // stays off
@@ -1710,17 +1840,40 @@ extern "C" int tlsgpu_evp_set_batching(unsigned window_us, unsigned max_jobs,
   auto* b = new (std::nothrow) EvpBatcher();
   if (!b) return fail(TLSGPU_ENOMEM, "batcher");
   b->window_us = window_us;
-  b->max_jobs = max_jobs ? max_jobs : 4096;
+  b->max_jobs = max_jobs ? std::min(max_jobs, kEvpMaxJobs) : kEvpMaxJobs;
   const uint32_t cap = pool_sessions ? pool_sessions : 1024;
   int rc = tlsgpu_sessions_create(e, cap, &b->pool);
   if (rc != TLSGPU_OK) {
     delete b;
     return rc;
   }
+  // the batcher lives as long as the process (its threads never exit)
   HIPCHK(hipSetDevice(e->device));
-  HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
-  for (int i = (int)cap - 1; i >= 0; i--) b->free_slots.push_back(i);
-  b->th = std::thread([b] { b->loop(); });
+  for (EvpSlot& s : b->slots) {
+    HIPCHK(hipHostMalloc((void**)&s.h, kEvpSlotBytes, hipHostMallocDefault));
+    HIPCHK(hipMalloc((void**)&s.d, kEvpSlotBytes));
+    HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  }
+  b->building = &b->slots[0];
+  for (uint32_t i = kEvpSlots - 1; i >= 1; i--) b->free_ring.push_back(&b->slots[i]);
+  for (int i = (int)cap - 1; i >= 0; i--) b->free_sessions.push_back(i);
+  if (getenv("TLSGPU_EVP_STATS")) {
+    atexit([] {
+      EvpBatcher* q = g_batcher;
+      std::lock_guard<std::mutex> lk(q->mu);
+      const double nb = q->batches ? (double)q->batches : 1.0;
+      fprintf(stderr,
+              "{\"evp_queue\": {\"batches\": %llu, \"jobs\": %llu, \"jobs_per_batch\": %.2f, "
+              "\"us_first_to_close\": %.1f, \"us_writers\": %.1f, \"us_submit\": %.1f, "
+              "\"us_submit_to_done\": %.1f}}\n",
+              (unsigned long long)q->batches, (unsigned long long)q->jobs_done,
+              q->jobs_done / nb, q->ns_wait / nb / 1e3, q->ns_writers / nb / 1e3,
+              q->ns_submit / nb / 1e3, q->ns_gpu / nb / 1e3);
+    });
+  }
+  b->disp = std::thread([b] { b->dispatch_loop(); });
+  b->comp = std::thread([b] { b->complete_loop(); });
   g_batcher = b;
   return TLSGPU_OK;
 }

@@ -1,6 +1,6 @@
 // session_kernels.hip — device session install and synthetic-data kernels.
 //
-// tlsgpu_sessions_install() runs install_sessions: one thread per session does
+// tlsgpu_sessions_install() runs install_sessions: one wave per session does
 // what aead_aes_gcm_init / CRYPTO_gcm128_init (crypto/evp/e_aes.c:1372-1413,
 // crypto/modes/gcm128.c:681-747) and aead_chacha20_poly1305_init
 // (e_chacha20poly1305.c:52-79) do at ChangeCipherSpec, plus the GHASH power
@@ -92,11 +92,19 @@ __device__ inline void store_be(uint32_t* w, U128 v) {
   w[3] = (uint32_t)v.lo;
 }
 
-__global__ void install_sessions(DevSession* __restrict__ sessions,
-                                 DevGcmTables* __restrict__ tables,
-                                 const tlsgpu_session_params* __restrict__ params,
-                                 uint32_t first, uint32_t n) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per session (blockIdx.x = session index): the key schedule and H
+// are computed by every lane (wave-uniform), then the 65 GHASH powers, their
+// Shoup tables, the H^64 basis and the bitsliced round-key masks are split
+// over the lanes.  Lane e gets H^(e+1) by square-and-multiply from the seven
+// squarings H^(2^k), so the longest chain is 6 squarings + 6 products instead
+// of the 64 serial products of a one-thread-per-session form (487 us per
+// session on MI355X, which was the EVP_AEAD_CTX_init latency).
+__global__ __launch_bounds__(64) void install_sessions(DevSession* __restrict__ sessions,
+                                                       DevGcmTables* __restrict__ tables,
+                                                       const tlsgpu_session_params* __restrict__ params,
+                                                       uint32_t first, uint32_t n) {
+  const uint32_t i = blockIdx.x;
+  const uint32_t lane = threadIdx.x;
   if (i >= n) return;
   const tlsgpu_session_params p = params[i];
   DevSession s = {};
@@ -106,7 +114,7 @@ __global__ void install_sessions(DevSession* __restrict__ sessions,
   uint32_t want_key = p.aead == TLSGPU_AES_128_GCM ? 16 : 32;
   uint32_t tag = p.tag_len == 0 ? 16 : p.tag_len;
   if ((!gcm && !cc) || p.key_len != want_key || tag > 16 || p.fixed_iv_len > 12) {
-    sessions[id] = s;  // kind 0: empty / invalid
+    if (lane == 0) sessions[id] = s;  // kind 0: empty / invalid
     return;
   }
   s.kind = (uint32_t)p.aead;
@@ -119,7 +127,7 @@ __global__ void install_sessions(DevSession* __restrict__ sessions,
   for (uint32_t k = 0; k < p.fixed_iv_len; k++) s.fixed_nonce[k] = p.fixed_iv[k];
   if (cc) {
     for (int k = 0; k < 32; k++) s.chacha_key[k] = p.key[k];
-    sessions[id] = s;
+    if (lane == 0) sessions[id] = s;
     return;
   }
   uint32_t rk_be[60];
@@ -136,16 +144,25 @@ __global__ void install_sessions(DevSession* __restrict__ sessions,
     H.lo = (H.lo << 8) | hb[8 + k];
   }
   store_le(s.h_le, H);
-  sessions[id] = s;
+  if (lane == 0) sessions[id] = s;
 
   DevGcmTables* t = &tables[id];
-  for (int r = 0; r <= (int)s.rounds; r++)
-    for (int b = 0; b < 16; b++)
-      for (int k = 0; k < 8; k++)
-        t->bsrk[r][8 * b + k] = 0u - ((s.rk[4 * r + b / 4] >> (8 * (b % 4) + k)) & 1u);
-  U128 pw = H;  // H^e
-  U128 k64{0, 0};
-  for (int e = 1; e <= kPowMax; e++) {
+  // bitsliced AddRoundKey masks: (rounds + 1) x 128 words over the lanes
+  for (uint32_t w = lane; w < 128u * (s.rounds + 1); w += 64) {
+    const uint32_t r = w / 128, b = (w % 128) / 8, k = w % 8;
+    t->bsrk[r][8 * b + k] = 0u - ((s.rk[4 * r + b / 4] >> (8 * (b % 4) + k)) & 1u);
+  }
+  U128 sq[7];  // H^(2^k)
+  sq[0] = H;
+  for (int k = 1; k < 7; k++) sq[k] = gf_mul(sq[k - 1], sq[k - 1]);
+  for (uint32_t e = lane + 1; e <= (uint32_t)kPowMax; e += 64) {
+    U128 pw{0, 0};
+    bool have = false;
+    for (int k = 0; k < 7; k++) {
+      if (!((e >> k) & 1)) continue;
+      pw = have ? gf_mul(pw, sq[k]) : sq[k];
+      have = true;
+    }
     U128 m[16];
     m[0] = U128{0, 0};
     m[8] = pw;
@@ -155,13 +172,12 @@ __global__ void install_sessions(DevSession* __restrict__ sessions,
     for (int a = 2; a < 16; a <<= 1)
       for (int b = 1; b < a; b++) m[a + b] = U128{m[a].hi ^ m[b].hi, m[a].lo ^ m[b].lo};
     for (int v = 0; v < 16; v++) store_be(t->shoup[e - 1][v], m[v]);
-    if (e == 64) k64 = pw;
-    pw = gf_mul(pw, H);
   }
-  U128 b = k64;  // K * x^p
-  for (int p2 = 0; p2 < 128; p2++) {
-    store_le(t->basis[p2], b);
-    b = gf_mulx(b);
+  // basis[q] = K * x^q, K = H^64 = sq[6]; lanes q and q + 64
+  for (uint32_t q = lane; q < 128; q += 64) {
+    U128 b = sq[6];
+    for (uint32_t k = 0; k < q; k++) b = gf_mulx(b);
+    store_le(t->basis[q], b);
   }
 }
 
@@ -263,7 +279,7 @@ int launch_session_install(DevSession* sessions, DevGcmTables* tables,
                            const tlsgpu_session_params* d_params, uint32_t first, uint32_t n,
                            hipStream_t s) {
   if (n == 0) return 0;
-  hipLaunchKernelGGL(install_sessions, dim3((n + 63) / 64), dim3(64), 0, s, sessions, tables,
+  hipLaunchKernelGGL(install_sessions, dim3(n), dim3(64), 0, s, sessions, tables,
                      d_params, first, n);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -12,6 +12,7 @@ import os
 import random
 import sys
 
+import numpy as np
 import pytest
 
 from conftest import ROOT, load_aeadtests
@@ -109,6 +110,39 @@ def test_evp_gcm_odd_ivs(ta, oracle, name):
         assert ok == ok2 == 1 and got == exp
         ok3, back, _ = g.open(iv, got, ad)
         assert ok3 == 1 and back == pt
+        g.cleanup()
+
+
+@pytest.mark.parametrize("name", ["aes-128-gcm", "aes-256-gcm"])
+def test_evp_gcm_split_jobs(ta, oracle, name):
+    """Raw EVP jobs run one per workgroup with the blocks split over its 16
+    waves (gcm_raw_kernel): lengths around the 64-block step and the per-wave
+    range boundaries, a partial last range, jobs far above a TLS record, short
+    tags, odd IVs and long AAD; seal equals the oracle, open round-trips, and a
+    flipped byte anywhere zero-fills the whole max_out."""
+    kind = KINDS[name]
+    rnd = random.Random(91)
+    key = bytes(rnd.randrange(256) for _ in range(po.KEY_LEN[kind]))
+    for n, iv_len, ad_len, tag_len in ((0, 12, 0, 16), (1, 12, 13, 16), (1023, 12, 13, 16),
+                                       (1024, 12, 13, 16), (1025, 12, 13, 12),
+                                       (2048, 1, 0, 16), (16384, 12, 13, 16),
+                                       (16385, 60, 1000, 16), (65543, 12, 13, 14),
+                                       (200000, 12, 17, 16), (16 * 64 * 16 * 2 + 5, 8, 300, 16)):
+        iv = bytes(rnd.randrange(256) for _ in range(iv_len))
+        ad = bytes(rnd.randrange(256) for _ in range(ad_len))
+        pt = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8).tobytes()
+        octx = oracle.aead(kind, key, tag_len)
+        ok, exp = oracle.seal(octx, iv, pt, ad)
+        g = ta.EvpAead(kind, key, tag_len)
+        ok2, got, _ = g.seal(iv, pt, ad)
+        assert ok == ok2 == 1 and got == exp, (n, iv_len, ad_len, tag_len)
+        ok3, back, ol = g.open(iv, got, ad)
+        assert ok3 == 1 and back == pt and ol == n, n
+        if n:
+            bad = bytearray(got)
+            bad[rnd.randrange(len(bad))] ^= 0x04
+            ok4, z, ol = g.open(iv, bytes(bad), ad, max_out=n + 5)
+            assert ok4 == 0 and z == bytes(n + 5) and ol == 0, n
         g.cleanup()
 
 
