@@ -97,6 +97,14 @@ struct tlsgpu_engine {
 
 // Scratch of at least `bytes` for stream s (enlarging waits for the stream's
 // earlier work, which may still read the old buffer).
+// TLSGPU_PRE_POOL=1 (diagnostic): take the scratch from the stream-ordered
+// pool instead, as round 1 first did; tools/pool_probe.hip and DESIGN.md §4.1
+// explain why that is wrong on MI355X.
+static const bool g_pre_pool = [] {
+  const char* v = getenv("TLSGPU_PRE_POOL");
+  return v && *v == '1';
+}();
+
 static void* pre_scratch(tlsgpu_engine* e, hipStream_t s, size_t bytes) {
   std::lock_guard<std::mutex> g(e->pre_mu);
   PreScratch* ps = nullptr;
@@ -419,9 +427,15 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   constexpr size_t kCtlBytes = 4096;
   const size_t pre_bytes = gcm_pre ? sizeof(RecPre) * (size_t)n + kCtlBytes : 0;
   uint8_t* scratch = nullptr;
+  uint8_t* pool_scratch = nullptr;
   if (pre_bytes || bounds) {
-    scratch = (uint8_t*)pre_scratch(t->eng, s,
-                                    pre_bytes + (bounds ? sizeof(tlsgpu_record) * (size_t)n : 0));
+    const size_t sbytes = pre_bytes + (bounds ? sizeof(tlsgpu_record) * (size_t)n : 0);
+    if (g_pre_pool) {  // diagnostic only (DESIGN.md §4.1 pool scratch): stream-ordered pool
+      if (hipMallocAsync((void**)&scratch, sbytes, s) != hipSuccess) scratch = nullptr;
+      pool_scratch = scratch;
+    } else {
+      scratch = (uint8_t*)pre_scratch(t->eng, s, sbytes);
+    }
     if (!scratch) return fail(TLSGPU_ENOMEM, "batch scratch (%u records)", n);
   }
   if (bounds) {
@@ -475,6 +489,7 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   if ((have[TLSGPU_CHACHA20_POLY1305] || have[TLSGPU_CHACHA20_POLY1305_OLD]) &&
       launch_chacha(a, seal, raw, groups, s))
     return fail(TLSGPU_EHIP, "chacha launch: %s", hipGetErrorString(hipGetLastError()));
+  if (pool_scratch) HIPCHK(hipFreeAsync(pool_scratch, s));
   return TLSGPU_OK;
 }
 
