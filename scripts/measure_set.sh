@@ -1,7 +1,9 @@
 #!/bin/bash
 # Measurement set for a round (run on the GPU box via gpurun):
 #   bench lines: B (metric), B at S = 1 / 65,536 sessions and interleaved, C, D,
-#   the box's copy bandwidth; then PMC passes (scripts/pmc.sh) for B, C and D.
+#   the box's copy bandwidth, host-resident B (tlsgpu_open_host), the pinned
+#   PCIe rates, wire B (tlsgpu_open_wire); then PMC passes (scripts/pmc.sh) for
+#   B, C and D.
 # usage: scripts/measure_set.sh TAG [--no-pmc]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -22,7 +24,10 @@ run B_S1 --sessions 1 --no-cpu-baseline &&
 run B_S65536 --sessions 65536 --no-cpu-baseline &&
 run B_inter1024 --sessions 1024 --interleave --no-cpu-baseline &&
 run C --config C &&
-run D --config D || exit $?
+run D --config D &&
+run host_B --mode host --no-cpu-baseline --steps 8 --warmup 2 &&
+run pcie --mode pcie &&
+run wire_B --mode wire --no-cpu-baseline || exit $?
 [ "$2" = "--no-pmc" ] && exit 0
 for c in B C D; do
   bash scripts/pmc.sh $TAG/pmc$c --config $c || exit $?

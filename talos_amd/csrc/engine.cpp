@@ -422,9 +422,10 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
       impl != TLSGPU_GCM_TTABLE && (have[TLSGPU_AES_128_GCM] || have[TLSGPU_AES_256_GCM]);
   // per-stream scratch: [RecPre x n (queue kernels) | kCtlBytes control words |
   // checked descriptors x n].  Control words per key size k (0: AES-128, 1:
-  // AES-256): selection words at 16 k, per-workgroup record counters of the
-  // per-wave-session kernel at 1024 (k + 1).
-  constexpr size_t kCtlBytes = 4096;
+  // AES-256): per-workgroup record counters of the per-wave-session kernel at
+  // 1024 (k + 1), selection words (kSelSlots x 64 B) at 4096 + 1024 k.
+  constexpr size_t kCtlBytes = 8192;
+  static_assert(kSelSlots * kSelWords * 4 <= 1024, "selection words exceed their slot");
   const size_t pre_bytes = gcm_pre ? sizeof(RecPre) * (size_t)n + kCtlBytes : 0;
   uint8_t* scratch = nullptr;
   uint8_t* pool_scratch = nullptr;
@@ -458,7 +459,7 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
     // not send the AES-256 pass to the pack variant
     if (ctl && impl == TLSGPU_GCM_QUEUE) {
       const int k = rounds == 10 ? 0 : 1;
-      a.sel = reinterpret_cast<uint32_t*>(ctl + 16 * k);
+      a.sel = reinterpret_cast<uint32_t*>(ctl + 4096 + 1024 * k);
       a.wg_next = reinterpret_cast<uint32_t*>(ctl + 1024 * (k + 1));
     }
     int rc;

@@ -484,6 +484,23 @@ __device__ __forceinline__ uint32_t queue_take(uint32_t* q, uint32_t k, uint32_t
   return __builtin_amdgcn_readfirstlane(r);
 }
 
+// The prep pass's selection words, summed over the kSelSlots cache lines
+// (s_load: wave-uniform).
+struct SelSums {
+  uint32_t pack, runs, recs;
+};
+__device__ __forceinline__ SelSums sel_sums(const uint32_t* sel) {
+  cu32* f = as_const(sel);
+  SelSums t = {0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < kSelSlots; i++) {
+    t.pack |= f[kSelWords * i];
+    t.runs += f[kSelWords * i + 1];
+    t.recs += f[kSelWords * i + 2];
+  }
+  return t;
+}
+
 // NT threads, the first BSW waves bitsliced (0: a pure T-table queue kernel,
 // 16 waves of <= 128 VGPRs), T-table waves NB blocks wide.
 template <bool SEAL, int ROUNDS, int NT, int BSW, int NB, bool PACK = false>
@@ -493,9 +510,9 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
   // long-record loop SGPR spills), and the per-wave-session kernel replaces both
   // when session runs are short; the prep pass's selection words pick one
   if (a.sel) {
-    cu32* f = as_const(a.sel);
-    if (pws_selected(a.pws, f[1], f[2])) return;
-    if ((a.pack != 0 && f[0] != 0) != PACK) return;
+    const SelSums f = sel_sums(a.sel);
+    if (pws_selected(a.pws, f.runs, f.recs)) return;
+    if ((a.pack != 0 && f.pack != 0) != PACK) return;
   } else if (PACK) {
     return;
   }
@@ -664,18 +681,27 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
   }
 }
 
-// Per-record constants (RecPre) for the hybrid kernel, one thread per record,
-// T-table from LDS (1 KiB, Te1 = rotl8(Te0)).  Follows rec_consts (gcm_device.h).
+// Per-record constants (RecPre) for the queue kernels, one thread per record.
+// Follows rec_consts (gcm_device.h).  Te0 sits in LDS replicated over the 32
+// banks of ds_read_b32 (row x, copy = lane % 32: conflict-free, 32 KiB; Te1 =
+// rotl8(Te0)); the round keys come through s_load when the wave's records all
+// belong to one session (the common case: sessions form runs), else per lane.
+constexpr int kPrepThreads = 512;
 template <bool SEAL, int ROUNDS>
-__global__ __launch_bounds__(256) void gcm_prep_kernel(BatchArgs a, RecPre* __restrict__ pre) {
-  __shared__ uint32_t te[256];
-  te[threadIdx.x] = g_te0.v[threadIdx.x];
+__global__ __launch_bounds__(kPrepThreads) void gcm_prep_kernel(BatchArgs a,
+                                                                RecPre* __restrict__ pre) {
+  __shared__ uint32_t te[256 * 32];
+  __shared__ uint32_t cnt[3];  // packable flag, run starts, records of this key size
+  for (uint32_t q = threadIdx.x; q < 256 * 8; q += kPrepThreads) {
+    const uint32_t v = g_te0.v[q >> 3];
+    reinterpret_cast<uint4*>(te)[q] = make_uint4(v, v, v, v);
+  }
+  if (threadIdx.x < 3) cnt[threadIdx.x] = 0;
   __syncthreads();
-  const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t r = blockIdx.x * kPrepThreads + threadIdx.x;
+  const uint32_t l32 = threadIdx.x & 31;
   const tlsgpu_record* D = reinterpret_cast<const tlsgpu_record*>(a.descs);
-  // selection words (a.sel): records of this key size and session-run starts
-  // among them, one atomic per wave
-  bool mine = false, run_start = false;
+  bool mine = false, run_start = false, packable = false;
   tlsgpu_record d = {};
   const DevSession* S = nullptr;
   if (r < a.n) {
@@ -684,21 +710,34 @@ __global__ __launch_bounds__(256) void gcm_prep_kernel(BatchArgs a, RecPre* __re
       S = a.sessions + d.session;
       mine = is_gcm(S->kind) && (int)S->rounds == ROUNDS;
       run_start = mine && (r == 0 || D[r - 1].session != d.session);
+      packable = mine && pack_need<SEAL>(d.len_type, S->tag_len) <= kPackMaxNeed;
     }
   }
+  // selection words (a.sel, SelSums): summed per wave (ballot), per workgroup
+  // (LDS) and then added to one of kSelSlots cache lines — one global atomic
+  // per workgroup and counter, spread over 16 addresses (same-address atomics
+  // from every wave serialised at one L2 channel: 115 us of config D's step)
   if (a.sel) {
-    const uint64_t m = __ballot(mine), rs = __ballot(run_start);
+    const uint64_t m = __ballot(mine), rs = __ballot(run_start), pk = __ballot(packable);
     if ((threadIdx.x & 63) == 0 && m) {
-      atomicAdd(a.sel + 2, (uint32_t)__builtin_popcountll(m));
-      atomicAdd(a.sel + 1, (uint32_t)__builtin_popcountll(rs));
+      atomicAdd(&cnt[2], (uint32_t)__builtin_popcountll(m));
+      atomicAdd(&cnt[1], (uint32_t)__builtin_popcountll(rs));
+      if (pk) cnt[0] = 1u;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && cnt[2]) {
+      uint32_t* slot = a.sel + kSelWords * (blockIdx.x % kSelSlots);
+      atomicAdd(slot + 2, cnt[2]);
+      atomicAdd(slot + 1, cnt[1]);
+      if (cnt[0]) atomicOr(slot, 1u);
     }
   }
+  const uint32_t sid0 = __builtin_amdgcn_readfirstlane(mine ? d.session : 0xFFFFFFFFu);
+  const bool uniform = !__any(mine && d.session != sid0);
   if (!mine) return;
-  if (a.sel && pack_need<SEAL>(d.len_type, S->tag_len) <= kPackMaxNeed) a.sel[0] = 1u;
-  auto T0 = [&](uint32_t w, int b) { return te[(w >> (8 * b)) & 0xFF]; };
-  auto T1 = [&](uint32_t w, int b) { return rotl32(te[(w >> (8 * b)) & 0xFF], 8); };
-  auto SB = [&](uint32_t w, int b) { return (te[(w >> (8 * b)) & 0xFF] >> 8) & 0xFF; };
-  const uint32_t* rk = S->rk;
+  auto T0 = [&](uint32_t w, int b) { return te[(((w >> (8 * b)) & 0xFF) << 5) | l32]; };
+  auto T1 = [&](uint32_t w, int b) { return rotl32(T0(w, b), 8); };
+  auto SB = [&](uint32_t w, int b) { return (T0(w, b) >> 8) & 0xFF; };
   uint32_t j0[4];
   j0[0] = *reinterpret_cast<const uint32_t*>(S->fixed_nonce);
   j0[1] = j0[2] = 0;
@@ -711,40 +750,47 @@ __global__ __launch_bounds__(256) void gcm_prep_kernel(BatchArgs a, RecPre* __re
     j0[1] = load_u32_bytes(p);
     j0[2] = load_u32_bytes(p + 4);
   }
-  // E_K(J0)
-  uint32_t s[4] = {j0[0] ^ rk[0], j0[1] ^ rk[1], j0[2] ^ rk[2], j0[3] ^ rk[3]};
-  for (int rr = 1; rr < ROUNDS; rr++) {
-    uint32_t t[4];
+  auto body = [&](auto rk) {
+    // E_K(J0)
+    uint32_t s[4] = {j0[0] ^ rk[0], j0[1] ^ rk[1], j0[2] ^ rk[2], j0[3] ^ rk[3]};
+#pragma unroll
+    for (int rr = 1; rr < ROUNDS; rr++) {
+      uint32_t t[4];
+#pragma unroll
+      for (int c = 0; c < 4; c++)
+        t[c] = T0(s[c], 0) ^ T1(s[(c + 1) & 3], 1) ^
+               rotl32(T0(s[(c + 2) & 3], 2) ^ T1(s[(c + 3) & 3], 3), 16) ^ rk[4 * rr + c];
+#pragma unroll
+      for (int c = 0; c < 4; c++) s[c] = t[c];
+    }
+    RecPre o;
 #pragma unroll
     for (int c = 0; c < 4; c++)
-      t[c] = T0(s[c], 0) ^ T1(s[(c + 1) & 3], 1) ^
-             rotl32(T0(s[(c + 2) & 3], 2) ^ T1(s[(c + 3) & 3], 3), 16) ^ rk[4 * rr + c];
-#pragma unroll
-    for (int c = 0; c < 4; c++) s[c] = t[c];
-  }
-  RecPre o;
-#pragma unroll
-  for (int c = 0; c < 4; c++)
-    o.ek0[c] = (SB(s[c], 0) | (SB(s[(c + 1) & 3], 1) << 8) | (SB(s[(c + 2) & 3], 2) << 16) |
-                (SB(s[(c + 3) & 3], 3) << 24)) ^ rk[4 * ROUNDS + c];
-  // round-1 constants (ctr_setup) and round-2 constants (rec_consts)
-  const uint32_t s0 = j0[0] ^ rk[0], s1 = j0[1] ^ rk[1], s2 = j0[2] ^ rk[2];
-  uint32_t k1[4];
-  k1[0] = T0(s0, 0) ^ T1(s1, 1) ^ rotl32(T0(s2, 2), 16) ^ rk[4];
-  k1[1] = T0(s1, 0) ^ T1(s2, 1) ^ rotl32(T1(s0, 3), 16) ^ rk[5];
-  k1[2] = T0(s2, 0) ^ rotl32(T0(s0, 2) ^ T1(s1, 3), 16) ^ rk[6];
-  k1[3] = T1(s0, 1) ^ rotl32(T0(s1, 2) ^ T1(s2, 3), 16) ^ rk[7];
-  const uint32_t v0 = rk[3];
-  const uint32_t c2 = k1[2] ^ T1(v0, 1), c3 = k1[3] ^ T0(v0, 0);  // round-1 columns 2, 3
-  o.k1a = k1[0];
-  o.k1b = k1[1];
-  o.k2[0] = rotl32(T0(c2, 2) ^ T1(c3, 3), 16) ^ rk[8];
-  o.k2[1] = T1(c2, 1) ^ rotl32(T0(c3, 2), 16) ^ rk[9];
-  o.k2[2] = T0(c2, 0) ^ T1(c3, 1) ^ rk[10];
-  o.k2[3] = T0(c3, 0) ^ rotl32(T1(c2, 3), 16) ^ rk[11];
-  o.sb2[0] = SB(c2, 0) | (SB(c2, 1) << 8) | (SB(c2, 2) << 16) | (SB(c2, 3) << 24);
-  o.sb2[1] = SB(c3, 0) | (SB(c3, 1) << 8) | (SB(c3, 2) << 16) | (SB(c3, 3) << 24);
-  pre[r] = o;
+      o.ek0[c] = (SB(s[c], 0) | (SB(s[(c + 1) & 3], 1) << 8) | (SB(s[(c + 2) & 3], 2) << 16) |
+                  (SB(s[(c + 3) & 3], 3) << 24)) ^ rk[4 * ROUNDS + c];
+    // round-1 constants (ctr_setup) and round-2 constants (rec_consts)
+    const uint32_t s0 = j0[0] ^ rk[0], s1 = j0[1] ^ rk[1], s2 = j0[2] ^ rk[2];
+    uint32_t k1[4];
+    k1[0] = T0(s0, 0) ^ T1(s1, 1) ^ rotl32(T0(s2, 2), 16) ^ rk[4];
+    k1[1] = T0(s1, 0) ^ T1(s2, 1) ^ rotl32(T1(s0, 3), 16) ^ rk[5];
+    k1[2] = T0(s2, 0) ^ rotl32(T0(s0, 2) ^ T1(s1, 3), 16) ^ rk[6];
+    k1[3] = T1(s0, 1) ^ rotl32(T0(s1, 2) ^ T1(s2, 3), 16) ^ rk[7];
+    const uint32_t v0 = rk[3];
+    const uint32_t c2 = k1[2] ^ T1(v0, 1), c3 = k1[3] ^ T0(v0, 0);  // round-1 columns 2, 3
+    o.k1a = k1[0];
+    o.k1b = k1[1];
+    o.k2[0] = rotl32(T0(c2, 2) ^ T1(c3, 3), 16) ^ rk[8];
+    o.k2[1] = T1(c2, 1) ^ rotl32(T0(c3, 2), 16) ^ rk[9];
+    o.k2[2] = T0(c2, 0) ^ T1(c3, 1) ^ rk[10];
+    o.k2[3] = T0(c3, 0) ^ rotl32(T1(c2, 3), 16) ^ rk[11];
+    o.sb2[0] = SB(c2, 0) | (SB(c2, 1) << 8) | (SB(c2, 2) << 16) | (SB(c2, 3) << 24);
+    o.sb2[1] = SB(c3, 0) | (SB(c3, 1) << 8) | (SB(c3, 2) << 16) | (SB(c3, 3) << 24);
+    pre[r] = o;
+  };
+  if (uniform)
+    body(as_const(a.sessions[sid0].rk));  // wave-uniform: round keys in SGPRs
+  else
+    body(S->rk);
 }
 
 

@@ -167,8 +167,8 @@ __device__ __forceinline__ GhNib gh_nib(uint32_t lane, uint32_t base) {
 template <bool SEAL, int ROUNDS>
 __global__ __launch_bounds__(kPwThreads, 1) void gcm_pw_kernel(BatchArgs a,
                                                                const RecPre* __restrict__ pre) {
-  cu32* f = as_const(a.sel);
-  if (!pws_selected(a.pws, f[1], f[2])) return;  // the queue kernel runs this batch
+  const SelSums f = sel_sums(a.sel);
+  if (!pws_selected(a.pws, f.runs, f.recs)) return;  // the queue kernel runs this batch
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t laneoff = (lane & 31) * 4;

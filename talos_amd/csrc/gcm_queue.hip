@@ -11,7 +11,7 @@ namespace tg {
 
 int launch_gcm_prep(const BatchArgs& a, RecPre* pre, bool seal, int rounds, hipStream_t s) {
   if (a.n == 0) return 0;
-  const dim3 g((a.n + 255) / 256), b(256);
+  const dim3 g((a.n + kPrepThreads - 1) / kPrepThreads), b(kPrepThreads);
   if (rounds == 10) {
     if (seal) hipLaunchKernelGGL((gcm_prep_kernel<true, 10>), g, b, 0, s, a, pre);
     else hipLaunchKernelGGL((gcm_prep_kernel<false, 10>), g, b, 0, s, a, pre);

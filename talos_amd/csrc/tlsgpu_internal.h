@@ -191,6 +191,11 @@ struct BatchArgs {
 // replaces the queue kernel: a run shorter than the workgroup's wave count leaves
 // waves idle at the run barrier.
 constexpr uint32_t kPwsRun = 12;
+// Selection words of the prep pass per key size: kSelSlots slots of kSelWords
+// words (one 64-B line each) = {packable flag, session-run starts, records};
+// a workgroup adds into slot blockIdx % kSelSlots, readers sum the slots.
+constexpr int kSelSlots = 16;
+constexpr int kSelWords = 16;
 __host__ __device__ __forceinline__ bool pws_selected(uint32_t mode, uint32_t runs, uint32_t recs) {
   return mode == 2 || (mode == 0 && runs * kPwsRun > recs);
 }
