@@ -114,6 +114,25 @@ __device__ __forceinline__ WireWalk wire_walk(const tlsgpu_wire_stream& st, cons
   return r;
 }
 
+// Reserve k consecutive descriptor slots per lane with ONE atomic per wave on
+// `total` (an inclusive scan over the wave, lane 63 adds the wave's sum):
+// same-address atomics from every lane serialise at one L2 channel.  All 64
+// lanes must be active (inactive streams pass k = 0).
+__device__ __forceinline__ uint32_t wave_reserve(uint32_t* total, uint32_t k) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t incl = k;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d);
+    if (lane >= (uint32_t)d) incl += y;
+  }
+  const uint32_t sum = __shfl(incl, 63);
+  uint32_t base = 0;
+  if (lane == 63 && sum) base = atomicAdd(total, sum);
+  base = __shfl(base, 63);
+  return base + incl - k;
+}
+
 __global__ __launch_bounds__(256) void wire_frame_kernel(const tlsgpu_wire_stream* __restrict__ streams,
                                                          uint32_t n_streams, const uint8_t* wire,
                                                          const DevSession* __restrict__ sessions,
@@ -122,11 +141,17 @@ __global__ __launch_bounds__(256) void wire_frame_kernel(const tlsgpu_wire_strea
                                                          tlsgpu_wire_result* __restrict__ results,
                                                          uint32_t* total) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n_streams) return;
-  const tlsgpu_wire_stream st = streams[s];
+  const bool active = s < n_streams;
+  tlsgpu_wire_stream st = {};
+  WireWalk walk = {};
+  if (active) {
+    st = streams[s];
+    walk = wire_walk(st, wire + st.wire_off, 0xFFFFFFFFu, [](uint32_t, uint32_t, const Hdr&) {});
+  }
+  const uint32_t slot0 = wave_reserve(total, active ? walk.records : 0u);
+  if (!active) return;
+  const uint32_t first = walk.records ? slot0 : 0u;
   const uint8_t* w = wire + st.wire_off;
-  WireWalk walk = wire_walk(st, w, 0xFFFFFFFFu, [](uint32_t, uint32_t, const Hdr&) {});
-  uint32_t first = walk.records ? atomicAdd(total, walk.records) : 0u;
   uint32_t n = walk.records;
   if (first >= max_records) {
     n = 0;
@@ -217,15 +242,18 @@ __global__ __launch_bounds__(256) void wire_seal_frame_kernel(
     uint64_t wire_bytes, uint32_t max_records, tlsgpu_record* __restrict__ recs,
     tlsgpu_write_result* __restrict__ results, uint32_t* __restrict__ total) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_streams) return;
-  const tlsgpu_write_stream st = streams[i];
+  const bool active = i < n_streams;
+  tlsgpu_write_stream st = {};
+  if (active) st = streams[i];
   tlsgpu_write_result res = {};
   res.next_seq = st.seq;
-  const bool ok = st.session < n_sessions && sessions[st.session].kind != 0;
+  const bool ok = active && st.session < n_sessions && sessions[st.session].kind != 0;
   const uint32_t frag = st.max_fragment == 0 || st.max_fragment > kMaxPlain ? kMaxPlain
                                                                            : st.max_fragment;
   uint32_t nrec = ok ? (st.data_len + frag - 1) / frag : 0;  // len 0: nothing (:593-594)
-  const uint32_t first = nrec ? atomicAdd(total, nrec) : 0;
+  const uint32_t slot0 = wave_reserve(total, nrec);
+  if (!active) return;
+  const uint32_t first = nrec ? slot0 : 0u;
   if (first >= max_records) nrec = 0;
   else if (first + nrec > max_records) nrec = max_records - first;
   res.first = first;
