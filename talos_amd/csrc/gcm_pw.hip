@@ -17,20 +17,41 @@
 //     (one 256-B table per lane, L2-resident), the rem_4bit reduction is done
 //     on the VALU (rem * 0xE1 carry-less, gcm128.c:327-331);
 //   * waves pull single records from a per-workgroup counter in global memory.
-// LDS: 64 KiB AES + 12 x 8 KiB = 160 KiB, one 768-thread workgroup per CU.
+// LDS: 64 KiB AES + 16 x 4 KiB (TG_PW_HALF) or 12 x 8 KiB, one workgroup per CU.
+//
+// TG_PW_HALF (default): the table covers one 64-bit half only (4 KiB: the high
+// half's nibble p is the low half's nibble p times x^64, so its sum is
+// multiplied by x^64 on the VALU, mulx64), which fits 16 waves x 4 KiB + the
+// AES tables in LDS: a 1024-thread workgroup at <= 128 VGPRs, as the queue
+// kernel.  TG_PW_HALF=0: the round-2 form, 12 waves x 8 KiB.
+#ifndef TG_PW_HALF
+#define TG_PW_HALF 1
+#endif
+#if TG_PW_HALF
+#define TG_LDS_BYTES 131072
+#else
 #define TG_LDS_BYTES 163840
+#endif
 #include "gcm_hybrid.h"
 
 namespace tg {
 
+#if TG_PW_HALF
+constexpr int kPwThreads = 1024;
+constexpr uint32_t PW_TAB_BYTES = 4096;  // 16 values x 16 positions x 16 B
+#else
 constexpr int kPwThreads = 768;
+constexpr uint32_t PW_TAB_BYTES = 8192;  // 2 halves x 16 values x 16 positions x 16 B
+#endif
 constexpr int kPwWaves = kPwThreads / kWave;
 constexpr uint32_t PW_TAB_OFF = 65536;
-constexpr uint32_t PW_TAB_BYTES = 8192;  // 2 halves x 16 values x 16 positions x 16 B
 static_assert(PW_TAB_OFF + kPwWaves * PW_TAB_BYTES <= LDS_BYTES, "per-wave tables exceed LDS");
 
 #ifndef TG_PW_NB
 #define TG_PW_NB 2
+#endif
+#ifndef TG_PW_QGROUP  // nibble-plane groups of 4 lookups per batch (1, 2 or 4)
+#define TG_PW_QGROUP (TG_PW_HALF ? 2 : 4)
 #endif
 #ifndef TG_PW_SHOUP_BATCH
 #define TG_PW_SHOUP_BATCH 16
@@ -41,6 +62,27 @@ static_assert(PW_TAB_OFF + kPwWaves * PW_TAB_BYTES <= LDS_BYTES, "per-wave table
 __device__ __forceinline__ uint32_t rem4(uint32_t r) {
   const uint32_t a = xor3(r, r << 1, r << 2);
   return (r << 21) ^ (a << 26);
+}
+
+// Reverse the bits of every byte of w (GCM's bit order <-> integer bit order).
+__device__ __forceinline__ uint32_t rbyte(uint32_t w) {
+  return __builtin_bitreverse32(__builtin_amdgcn_perm(w, w, 0x00010203u));
+}
+
+// b * x^64 in GF(2^128) (LE words: bytes 8..15 of the result are bytes 0..7
+// of b; bytes 8..15 of b, times x^128 = x^7 + x^2 + x + 1, fold into bytes
+// 0..8: gcm128.c's reduction, 64 bits at once).
+__device__ __forceinline__ void mulx64(const uint32_t b[4], uint32_t r[4]) {
+  const uint32_t s0 = rbyte(b[2]), s1 = rbyte(b[3]);  // x^0..x^63 of the overflow, integer order
+  const uint32_t q0 = xor3(s0, s0 << 1, s0 << 2) ^ (s0 << 7);
+  const uint32_t q1 = xor3(s1, __builtin_amdgcn_alignbit(s1, s0, 31),
+                           __builtin_amdgcn_alignbit(s1, s0, 30)) ^
+                      __builtin_amdgcn_alignbit(s1, s0, 25);
+  const uint32_t q2 = xor3(s1 >> 31, s1 >> 30, s1 >> 25);  // x^64..x^70
+  r[0] = rbyte(q0);
+  r[1] = rbyte(q1);
+  r[2] = b[0] ^ rbyte(q2);
+  r[3] = b[1];
 }
 
 struct GhNib {
@@ -56,7 +98,7 @@ struct GhNib {
   // Lanes of a ds_read_b128 lane group have distinct m, so distinct positions,
   // so distinct quad-banks: conflict-free.
   __device__ __forceinline__ void mul64(const uint32_t x[4], uint32_t o[4]) const {
-    uint32_t acc[4] = {0, 0, 0, 0};
+    uint32_t acc[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
 #pragma unroll
     for (int h = 0; h < 2; h++) {  // 16 lookups in flight per half
       const uint32_t lo = x[2 * h], hi = x[2 * h + 1];
@@ -65,23 +107,33 @@ struct GhNib {
       const uint32_t yhi = __builtin_amdgcn_alignbit(a, b, s);
       const uint32_t pl[4] = {ylo & 0x0F0F0F0Fu, (ylo >> 4) & 0x0F0F0F0Fu, yhi & 0x0F0F0F0Fu,
                               (yhi >> 4) & 0x0F0F0F0Fu};
-      uint4 v[16];
+      const uint32_t hb = TG_PW_HALF ? base : base + 4096u * h;
+      const int d = TG_PW_HALF ? h : 0;
 #pragma unroll
-      for (int q = 0; q < 4; q++)
+      for (int q0 = 0; q0 < 4; q0 += TG_PW_QGROUP) {  // 4 * TG_PW_QGROUP lookups in flight
+        uint4 v[4 * TG_PW_QGROUP];
 #pragma unroll
-        for (int bb = 0; bb < 4; bb++)
-          v[4 * q + bb] = lds_u128(base + 4096u * h +
-                                   __builtin_amdgcn_perm(pl[q], cq[q],
-                                                         0x0C0C0000u | ((4u + bb) << 8) | bb));
+        for (int q = 0; q < TG_PW_QGROUP; q++)
 #pragma unroll
-      for (int k = 0; k < 16; k += 2) {
-        acc[0] = xor3(acc[0], v[k].x, v[k + 1].x);
-        acc[1] = xor3(acc[1], v[k].y, v[k + 1].y);
-        acc[2] = xor3(acc[2], v[k].z, v[k + 1].z);
-        acc[3] = xor3(acc[3], v[k].w, v[k + 1].w);
+          for (int bb = 0; bb < 4; bb++)
+            v[4 * q + bb] = lds_u128(hb + __builtin_amdgcn_perm(pl[q0 + q], cq[q0 + q],
+                                                                0x0C0C0000u | ((4u + bb) << 8) | bb));
+#pragma unroll
+        for (int k = 0; k < 4 * TG_PW_QGROUP; k += 2) {
+          acc[d][0] = xor3(acc[d][0], v[k].x, v[k + 1].x);
+          acc[d][1] = xor3(acc[d][1], v[k].y, v[k + 1].y);
+          acc[d][2] = xor3(acc[d][2], v[k].z, v[k + 1].z);
+          acc[d][3] = xor3(acc[d][3], v[k].w, v[k + 1].w);
+        }
       }
     }
-    o[0] = acc[0]; o[1] = acc[1]; o[2] = acc[2]; o[3] = acc[3];
+    if (TG_PW_HALF) {
+      uint32_t t[4];
+      mulx64(acc[1], t);
+      o[0] = acc[0][0] ^ t[0]; o[1] = acc[0][1] ^ t[1]; o[2] = acc[0][2] ^ t[2]; o[3] = acc[0][3] ^ t[3];
+    } else {
+      o[0] = acc[0][0]; o[1] = acc[0][1]; o[2] = acc[0][2]; o[3] = acc[0][3];
+    }
   }
 
   // Z = X * H^e (Shoup 4-bit, gcm128.c:333-393), BE words, table from HBM
@@ -118,24 +170,31 @@ struct GhNib {
 
   // This wave's table for session tables `t` (from basis[q] = H^64 * x^q, LE
   // words; bit t of the byte at position j is x^(8j + 7 - t), load_session_tables).
-  // Lane l builds position p = l % 16 of half h = (l / 16) % 2, values
-  // 8g .. 8g + 7 with g = l / 32.
+  // Half form: lane l builds position p = l % 16, values 4g .. 4g + 3 with
+  // g = l / 16.  Full form: position p = l % 16 of half h = (l / 16) % 2,
+  // values 8g .. 8g + 7 with g = l / 32.
   __device__ __forceinline__ void build(uint32_t lane) const {
+#if TG_PW_HALF
+    const uint32_t p = lane & 15, h = 0, g = lane >> 4;
+    constexpr int kVals = 4;
+#else
     const uint32_t p = lane & 15, h = (lane >> 4) & 1, g = lane >> 5;
+    constexpr int kVals = 8;
+#endif
     const uint32_t i = 16 * h + p, j = i >> 1, sh = 4 * (i & 1);
     uint4 B[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) B[t] = gload16(&tab->basis[8 * j + 7 - sh - t][0]);
-    const uint32_t m3 = g ? 0xFFFFFFFFu : 0u;
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const uint32_t m0 = (u & 1) ? 0xFFFFFFFFu : 0u, m1 = (u & 2) ? 0xFFFFFFFFu : 0u;
-      const uint32_t m2 = (u & 4) ? 0xFFFFFFFFu : 0u;
+    for (int u = 0; u < kVals; u++) {
+      const uint32_t v = kVals * g + u;
+      const uint32_t m0 = (v & 1) ? 0xFFFFFFFFu : 0u, m1 = (v & 2) ? 0xFFFFFFFFu : 0u;
+      const uint32_t m2 = (v & 4) ? 0xFFFFFFFFu : 0u, m3 = (v & 8) ? 0xFFFFFFFFu : 0u;
       const uint4 e = make_uint4((B[0].x & m0) ^ (B[1].x & m1) ^ (B[2].x & m2) ^ (B[3].x & m3),
                                  (B[0].y & m0) ^ (B[1].y & m1) ^ (B[2].y & m2) ^ (B[3].y & m3),
                                  (B[0].z & m0) ^ (B[1].z & m1) ^ (B[2].z & m2) ^ (B[3].z & m3),
                                  (B[0].w & m0) ^ (B[1].w & m1) ^ (B[2].w & m2) ^ (B[3].w & m3));
-      *reinterpret_cast<uint4*>(s_lds + base + 4096u * h + (8u * g + u) * 256u + p * 16u) = e;
+      *reinterpret_cast<uint4*>(s_lds + base + 4096u * h + v * 256u + p * 16u) = e;
     }
     // the wave's own later lookups read what its lanes just wrote
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
