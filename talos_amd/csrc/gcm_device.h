@@ -18,7 +18,13 @@ constexpr int kWaves = kThreads / kWave;
 constexpr uint32_t AES_OFF = 0;
 constexpr uint32_t KT_OFF = 65536;
 constexpr uint32_t SH_OFF = 131072;
-constexpr uint32_t R4_OFF = SH_OFF + kPowMax * 256;
+// Shoup tables: entry (e, v) of H^e (e = 1..65, nibble v) at
+// SH_OFF + ((e-1)/16) * 4 KiB + v * 256 + ((e-1) % 16) * 16 (sh_base), i.e. the
+// power picks the 16-B column: the lanes of a ds_read_b128 group (distinct lane
+// % 16) need powers with distinct (e-1) % 16 in the per-lane chain weights, so
+// their lookups are conflict-free whatever the nibbles.
+constexpr uint32_t SH_BYTES = ((kPowMax + 15) / 16) * 4096;
+constexpr uint32_t R4_OFF = SH_OFF + SH_BYTES;
 constexpr uint32_t Q_OFF = R4_OFF + 64;      // hybrid kernel: per-run record queue
 constexpr uint32_t DBG_OFF = Q_OFF + 16;     // hybrid kernel: phase counters (diagnostic)
 constexpr uint32_t PLAN_OFF = DBG_OFF + 32 * 8;  // queue kernel: per-run pack plan
@@ -374,11 +380,25 @@ __device__ __forceinline__ void mul_k2(const uint32_t xa[4], const uint32_t xb[4
   ob[0] = acc[1].x; ob[1] = acc[1].y; ob[2] = acc[1].z; ob[3] = acc[1].w;
 }
 
+// LDS address of the Shoup table of H^e (e = 1..65); entry v at + v * 256.
+__device__ __forceinline__ uint32_t sh_base(uint32_t e) {
+  const uint32_t i = e - 1;
+  return SH_OFF + (i >> 4) * 4096u + (i & 15u) * 16u;
+}
+
+// rem_4bit[r] >> 32 (gcm128.c:327-331) on the VALU: (r * 0xE1, carry-less) << 21,
+// 0xE1 = x^0 + x^5 + x^6 + x^7, so r*0xE1 = r ^ ((r ^ r<<1 ^ r<<2) << 5).  (A
+// 16-entry LDS table read with a random index costs 3-4-way bank conflicts.)
+__device__ __forceinline__ uint32_t rem4(uint32_t r) {
+  const uint32_t a = xor3(r, r << 1, r << 2);
+  return (r << 21) ^ (a << 26);
+}
+
 // z = x * H^e (Shoup 4-bit, gcm128.c:333-393), all in big-endian words.
 __device__ __forceinline__ void mul_shoup(const uint32_t X[4], uint32_t e, uint32_t Z[4]) {
-  const uint32_t base = SH_OFF + (e - 1) * 256;
+  const uint32_t base = sh_base(e);
   uint32_t n0 = X[3] & 0xF;
-  uint4 m = lds_u128(base + n0 * 16);
+  uint4 m = lds_u128(base + n0 * 256);
   uint32_t z0 = m.x, z1 = m.y, z2 = m.z, z3 = m.w;
 #pragma unroll
   for (int k = 1; k < 32; k++) {
@@ -387,8 +407,8 @@ __device__ __forceinline__ void mul_shoup(const uint32_t X[4], uint32_t e, uint3
     z3 = __builtin_amdgcn_alignbit(z2, z3, 4);
     z2 = __builtin_amdgcn_alignbit(z1, z2, 4);
     z1 = __builtin_amdgcn_alignbit(z0, z1, 4);
-    z0 = (z0 >> 4) ^ lds_u32(R4_OFF + rem * 4);
-    uint4 t = lds_u128(base + nib * 16);
+    z0 = (z0 >> 4) ^ rem4(rem);
+    uint4 t = lds_u128(base + nib * 256);
     z0 ^= t.x; z1 ^= t.y; z2 ^= t.z; z3 ^= t.w;
   }
   Z[0] = z0; Z[1] = z1; Z[2] = z2; Z[3] = z3;
@@ -405,10 +425,10 @@ __device__ __forceinline__ void GhLane::shoup(const uint32_t X[4], uint32_t e, u
 __device__ __forceinline__ void mul_shoup2(const uint32_t A[4], uint32_t ea, uint32_t ZA[4],
                                            const uint32_t B[4], uint32_t eb, uint32_t ZB[4]) {
   // empty chains (e == 0) read the H^1 table and are masked to zero at the end
-  const uint32_t base_a = SH_OFF + (ea ? ea - 1 : 0) * 256, base_b = SH_OFF + (eb ? eb - 1 : 0) * 256;
+  const uint32_t base_a = sh_base(ea ? ea : 1), base_b = sh_base(eb ? eb : 1);
   const uint32_t ma = ea ? 0xFFFFFFFFu : 0u, mb = eb ? 0xFFFFFFFFu : 0u;
-  uint4 m = lds_u128(base_a + (A[3] & 0xF) * 16);
-  uint4 n = lds_u128(base_b + (B[3] & 0xF) * 16);
+  uint4 m = lds_u128(base_a + (A[3] & 0xF) * 256);
+  uint4 n = lds_u128(base_b + (B[3] & 0xF) * 256);
   uint32_t a0 = m.x, a1 = m.y, a2 = m.z, a3 = m.w;
   uint32_t b0 = n.x, b1 = n.y, b2 = n.z, b3 = n.w;
 #pragma unroll
@@ -416,8 +436,8 @@ __device__ __forceinline__ void mul_shoup2(const uint32_t A[4], uint32_t ea, uin
     const uint32_t na = (A[3 - k / 8] >> (4 * (k % 8))) & 0xF;
     const uint32_t nb = (B[3 - k / 8] >> (4 * (k % 8))) & 0xF;
     const uint32_t ra = a3 & 0xF, rb = b3 & 0xF;
-    const uint4 ta = lds_u128(base_a + na * 16), tb = lds_u128(base_b + nb * 16);
-    const uint32_t qa = lds_u32(R4_OFF + ra * 4), qb = lds_u32(R4_OFF + rb * 4);
+    const uint4 ta = lds_u128(base_a + na * 256), tb = lds_u128(base_b + nb * 256);
+    const uint32_t qa = rem4(ra), qb = rem4(rb);
     a3 = __builtin_amdgcn_alignbit(a2, a3, 4);
     a2 = __builtin_amdgcn_alignbit(a1, a2, 4);
     a1 = __builtin_amdgcn_alignbit(a0, a1, 4);
@@ -1146,8 +1166,8 @@ __device__ void load_session_tables(const DevGcmTables* __restrict__ tab) {
     }
   }
   const uint4* sh = reinterpret_cast<const uint4*>(&tab->shoup[0][0][0]);
-  for (uint32_t k = threadIdx.x; k < kPowMax * 16; k += NT)
-    *reinterpret_cast<uint4*>(s_lds + SH_OFF + k * 16) = sh[k];
+  for (uint32_t k = threadIdx.x; k < kPowMax * 16; k += NT)  // k = 16 (e - 1) + v
+    *reinterpret_cast<uint4*>(s_lds + sh_base(1 + (k >> 4)) + (k & 15u) * 256u) = sh[k];
 }
 
 // Bitsliced round-key masks from the round-key words (SGPRs): s_bfe_i32

@@ -20,7 +20,7 @@
 //                           at step k (its state pre-rotated by m bytes) so the
 //                           16 lanes of every ds_read_b128 group hit 16
 //                           different slots: conflict-free GHASH lookups;
-//       SHOUP [128K, +16.6K): 4-bit tables of H^1..H^65 for the per-lane final
+//       SHOUP [128K, +20K): 4-bit tables of H^1..H^65 (column = power) for the per-lane final
 //                           multiply; REM4: 16-entry reduction table;
 //   * GHASH: lane l runs a Horner chain x <- x*H^64 ^ E_j over the extended
 //     block sequence E = [AAD', C_0..C_{nb-1}, lengths] (j = l mod 64), then

@@ -57,13 +57,6 @@ static_assert(PW_TAB_OFF + kPwWaves * PW_TAB_BYTES <= LDS_BYTES, "per-wave table
 #define TG_PW_SHOUP_BATCH 16
 #endif
 
-// rem_4bit[r] >> 32 (gcm128.c:327-331) on the VALU: (r * 0xE1, carry-less) << 21,
-// 0xE1 = x^0 + x^5 + x^6 + x^7, so r*0xE1 = r ^ ((r ^ r<<1 ^ r<<2) << 5).
-__device__ __forceinline__ uint32_t rem4(uint32_t r) {
-  const uint32_t a = xor3(r, r << 1, r << 2);
-  return (r << 21) ^ (a << 26);
-}
-
 // Reverse the bits of every byte of w (GCM's bit order <-> integer bit order).
 __device__ __forceinline__ uint32_t rbyte(uint32_t w) {
   return __builtin_bitreverse32(__builtin_amdgcn_perm(w, w, 0x00010203u));
