@@ -353,7 +353,7 @@ extern "C" int tlsgpu_debug_phase_stats(tlsgpu_engine* e, unsigned long long* ou
 
 static uint32_t g_hy_flags = []() {
   const char* v = getenv("TLSGPU_HY_FLAGS");
-  return v ? (uint32_t)strtoul(v, nullptr, 0) & 7u : 0u;
+  return v ? (uint32_t)strtoul(v, nullptr, 0) & 15u : 0u;
 }();
 
 // Queue kernel: records with n >= this take the packed bitsliced path

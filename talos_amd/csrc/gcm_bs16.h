@@ -197,4 +197,52 @@ __device__ __forceinline__ void gcm_record_bs16(const RecCtx& rc, const RecPre* 
   pc.lap(15, lane);
 }
 
+// The queue kernel's bitsliced wave role (hy_b16_record): a
+// 16-B-aligned record of at most 1024 blocks.  Its full 64-block steps take
+// the bitsliced keystream with a lean consume loop (whole-wave 16-B loads and
+// stores, no partial-block masking: the general loop of gcm_record_bs16 spills
+// in the queue kernel), the rest (< 64 blocks) the T-table gcm_blocks path.
+template <bool SEAL, int ROUNDS>
+__device__ __forceinline__ void gcm_record_bs16f(const RecCtx& rc, const RecPre* pre,
+                                                 const DevSession* __restrict__ S,
+                                                 int32_t* status_slot, uint32_t lane,
+                                                 uint32_t laneoff, const GhLane& gl) {
+  cu32* rk = as_const(S->rk);
+  const uint32_t steps = rc.n >> 10;  // full 64-block steps, <= 16
+  const Prefetch<2> pf = l2_prefetch<2>(rc.src, steps << 10, lane);
+  uint32_t st[64];
+  bs16_keystream<ROUNDS>(st, pre, 2u + lane, rk);
+  const uint32_t rkl[4] = {rk[4 * ROUNDS], rk[4 * ROUNDS + 1], rk[4 * ROUNDS + 2], rk[4 * ROUNDS + 3]};
+  uint32_t x[4] = {0, 0, 0, 0};
+  if (lane == 63) {  // AAD' at j = -1 (TLS: the 13-byte AAD)
+    x[0] = bswap32(rc.aad_be[0]); x[1] = bswap32(rc.aad_be[1]);
+    x[2] = bswap32(rc.aad_be[2]); x[3] = bswap32(rc.aad_be[3]);
+  }
+  const uint4* src = reinterpret_cast<const uint4*>(rc.src) + lane;
+  uint4* dst = reinterpret_cast<uint4*>(rc.dst) + lane;
+  uint4 cur = src[0];
+  prefetch_done(pf);
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    if ((uint32_t)j < steps) {
+      uint4 nxt = cur;
+      if (j + 1 < 16 && (uint32_t)(j + 1) < steps) nxt = src[64 * (j + 1)];
+      const uint32_t c[4] = {cur.x, cur.y, cur.z, cur.w};
+      const uint32_t o[4] = {xor3(c[0], st[j], rkl[0]), xor3(c[1], st[32 + j], rkl[1]),
+                             xor3(c[2], st[16 + j], rkl[2]), xor3(c[3], st[48 + j], rkl[3])};
+      dst[64 * j] = make_uint4(o[0], o[1], o[2], o[3]);
+      uint32_t xk[4];
+      mul_k(x, xk, gl);
+      const uint32_t* g = SEAL ? o : c;
+      x[0] = xk[0] ^ g[0]; x[1] = xk[1] ^ g[1]; x[2] = xk[2] ^ g[2]; x[3] = xk[3] ^ g[3];
+      cur = nxt;
+    }
+  }
+  const RecConsts rcc = rec_consts_of(pre);
+  uint32_t start = steps << 6;
+  const CtrConst none = {};
+  gcm_blocks<SEAL, ROUNDS, true>(rc, S, rcc, none, x, start, lane, laneoff, gl);
+  gcm_finish<SEAL>(rc, x, rcc.ek0, S, status_slot, lane, gl);
+}
+
 }  // namespace tg

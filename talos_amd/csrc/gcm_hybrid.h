@@ -317,6 +317,30 @@ __device__ __forceinline__ void hy_tt_record(const BatchArgs& a, const RecPre* _
   gcm_record_x4<SEAL, ROUNDS, NB>(rc, S, rcc, a.status + r, lane, laneoff, gl, a.dbg);
 }
 
+// Packed bitsliced wave role: a record of a_min..16384
+// bytes, 16-B aligned, with more than `reserve` records of its session run
+// still unclaimed runs through gcm_record_bs16 (AES-CTR on the VALU, GHASH on
+// the shared LDS table); anything else through the T-table path.  The reserve
+// keeps the run's last records on T-table waves, so the run-end barrier does
+// not wait for a bitsliced record started late.
+template <bool SEAL, int ROUNDS>
+__device__ __forceinline__ bool hy_b16_record(const BatchArgs& a, const RecPre* __restrict__ pre,
+                                              uint32_t r, uint32_t left,
+                                              const DevSession* __restrict__ S, uint32_t lane,
+                                              uint32_t laneoff, const GhLane& gl) {
+  const tlsgpu_record* D = reinterpret_cast<const tlsgpu_record*>(a.descs);
+  const tlsgpu_record d = load_desc(D + r);
+  if (left <= a.bs_reserve) return false;
+  RecCtx rc;
+  if (!parse_tls<SEAL>(d, S, a.in, a.out, a.status + r, lane, rc)) return true;
+  if (rc.n >= a.bs16_min && rc.n >= 1024u && rc.n <= 16384u &&
+      ((((uintptr_t)rc.src) | ((uintptr_t)rc.dst)) & 15) == 0) {
+    gcm_record_bs16f<SEAL, ROUNDS>(rc, pre + r, S, a.status + r, lane, laneoff, gl);
+    return true;
+  }
+  return false;  // the caller's T-table path (one call site of gcm_record_x4: inlined)
+}
+
 // ---------------------------------------------------------------------------
 // Short-record packs.  A record's GHASH sequence is
 // [AAD, C_0..C_{nb-1}, lengths] (gcm128.c:826-881,1356-1500): nb + 2 elements.
@@ -502,8 +526,10 @@ __device__ __forceinline__ SelSums sel_sums(const uint32_t* sel) {
 }
 
 // NT threads, the first BSW waves bitsliced (0: a pure T-table queue kernel,
-// 16 waves of <= 128 VGPRs), T-table waves NB blocks wide.
-template <bool SEAL, int ROUNDS, int NT, int BSW, int NB, bool PACK = false>
+// 16 waves of <= 128 VGPRs), T-table waves NB blocks wide; B16W > 0: the first
+// B16W waves take the packed bitsliced role (hy_b16_record, one per SIMD for
+// B16W = 4: waves go to the SIMDs in turn).
+template <bool SEAL, int ROUNDS, int NT, int BSW, int NB, bool PACK = false, int B16W = 0>
 __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
                                                        const RecPre* __restrict__ pre) {
   // pack and no-pack variants are separate kernels (the pack code costs the
@@ -523,6 +549,8 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
   const tlsgpu_record* D = reinterpret_cast<const tlsgpu_record*>(a.descs);
   const bool bs_role = wave < (uint32_t)BSW;
   if (BSW && !bs_role) __builtin_amdgcn_s_setprio(1);
+  const bool b16_role = B16W > 0 && wave < (uint32_t)B16W;
+  if (B16W > 0 && !b16_role && !(a.hy_flags & 8u)) __builtin_amdgcn_s_setprio(1);
   uint32_t* q = reinterpret_cast<uint32_t*>(s_lds + Q_OFF);
 
   fill_aes_lds<NT>();
@@ -637,7 +665,11 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
           }
         } else {
           uint32_t r;
-          if (has_short) {
+          if (B16W > 0 && b16_role) {
+            r = queue_take(q, 1, lane);
+            if (r >= run_end) break;
+            if (hy_b16_record<SEAL, ROUNDS>(a, pre, r, run_end - r, S, lane, laneoff, gl)) continue;
+          } else if (has_short) {
             // claim the pack the plan starts at the queue head (k = 0: a long
             // record alone); the CAS window is two LDS operations
             uint32_t k = 0;

@@ -26,6 +26,11 @@ int launch_gcm_queue(const BatchArgs& a, const RecPre* pre, bool seal, int round
                      hipStream_t s) {
   if (a.n == 0) return 0;
   const dim3 g(groups), b(1024);
+#ifdef TG_EXPERIMENTAL
+  if (a.bs16_min != 0 && a.sel) {  // no-pack variant with bitsliced waves (gcm_queue_b16.hip)
+    if (launch_gcm_queue_b16(a, pre, seal, rounds, groups, s)) return -1;
+  } else
+#endif
   if (rounds == 10) {
     if (seal) hipLaunchKernelGGL((gcm_hy_kernel<true, 10, 1024, 0, TG_QUEUE_NB>), g, b, 0, s, a, pre);
     else hipLaunchKernelGGL((gcm_hy_kernel<false, 10, 1024, 0, TG_QUEUE_NB>), g, b, 0, s, a, pre);

@@ -172,8 +172,9 @@ struct BatchArgs {
                                     // 1 = no bitsliced pairs, 2 = T-table waves idle,
                                     // 4 = bitsliced waves idle
   unsigned long long* dbg;          // phase timing (PhaseClock), normally null
-  uint32_t bs16_min;                // queue kernel: records of n >= this (<= 16384, 16-B
-                                    // aligned) take the packed bitsliced path; 0 = never
+  uint32_t bs16_min;                // queue kernel: non-zero = the no-pack variant runs with
+                                    // 4 packed bitsliced waves, which take records of n >= this
+                                    // (<= 16384, 16-B aligned; gcm_queue_b16.hip); 0 = never
   uint32_t pack;                    // queue kernel: short records of one session share a
                                     // wave (gcm_pack); 0 = off
   uint32_t* sel;                    // queue impl: 4 selection words of this key size, filled
@@ -220,6 +221,8 @@ int launch_gcm(const BatchArgs& a, bool seal, bool raw, int rounds, int groups,
 int launch_gcm_prep(const BatchArgs& a, RecPre* pre, bool seal, int rounds, hipStream_t s);
 int launch_gcm_queue(const BatchArgs& a, const RecPre* pre, bool seal, int rounds, int groups,
                      hipStream_t s);
+int launch_gcm_queue_b16(const BatchArgs& a, const RecPre* pre, bool seal, int rounds, int groups,
+                         hipStream_t s);
 int launch_gcm_pw(const BatchArgs& a, const RecPre* pre, bool seal, int rounds, int groups,
                   hipStream_t s);
 int launch_gcm_stream(const DevSession* sessions, const DevGcmTables* tables, uint32_t session,
