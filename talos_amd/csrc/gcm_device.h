@@ -15,8 +15,13 @@ static __device__ const WordTable g_te0 = kTe0;
 
 constexpr int kThreads = 1024;
 constexpr int kWaves = kThreads / kWave;
-constexpr uint32_t AES_OFF = 0;
-constexpr uint32_t KT_OFF = 65536;
+// The GHASH byte-position table sits at LDS offset 0 and the AES T-tables at
+// 64 KiB: a table address is then a single v_perm with no base add — the
+// KT lookups' base is 0, and the T-table base 0x10000 rides in byte 2 of the
+// lane's `laneoff` operand, which taddr's selector copies (aes_laneoff).
+constexpr uint32_t KT_OFF = 0;
+constexpr uint32_t AES_OFF = 0x10000;
+static_assert(AES_OFF == 0x10000, "taddr takes the T-table base from byte 2 of laneoff");
 constexpr uint32_t SH_OFF = 131072;
 // Shoup tables: entry (e, v) of H^e (e = 1..65, nibble v) at
 // SH_OFF + ((e-1)/16) * 4 KiB + v * 256 + ((e-1) % 16) * 16 (sh_base), i.e. the
@@ -52,10 +57,13 @@ __device__ __forceinline__ uint4 lds_u128(uint32_t off) {
   return *reinterpret_cast<const uint4*>(s_lds + off);
 }
 
-// address of Te0[byte r of w] for this lane: [0, 0, byte, lane bank]
+// The lane's T-table operand: its bank offset (lane % 32) * 4 in byte 0 and
+// the table base AES_OFF >> 16 in byte 2.
+__device__ __forceinline__ uint32_t aes_laneoff(uint32_t lane) { return ((lane & 31) * 4) | AES_OFF; }
+// address of Te0[byte r of w] for this lane: [0, AES_OFF >> 16, byte, lane bank]
 template <int R>
 __device__ __forceinline__ uint32_t taddr(uint32_t w, uint32_t laneoff) {
-  return __builtin_amdgcn_perm(w, laneoff, 0x0C0C0000u | ((4u + R) << 8));
+  return __builtin_amdgcn_perm(w, laneoff, 0x0C020000u | ((4u + R) << 8));
 }
 __device__ __forceinline__ uint32_t rotl16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
 // three-input XOR in one VALU op: v_bitop3_b32 with truth table 0x96 (gfx950
@@ -66,8 +74,8 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return d;
 }
 
-#define TE0(w, r) lds_u32(AES_OFF + taddr<r>((w), laneoff))
-#define TE1(w, r) lds_u32(AES_OFF + 128 + taddr<r>((w), laneoff))
+#define TE0(w, r) lds_u32(taddr<r>((w), laneoff))
+#define TE1(w, r) lds_u32(128 + taddr<r>((w), laneoff))
 
 // One full AES round on little-endian columns (ShiftRows: row r of output
 // column c comes from input column c+r).  kr_c = rotr16(k_c) is folded into the

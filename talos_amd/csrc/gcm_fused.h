@@ -317,7 +317,7 @@ template <bool SEAL, int ROUNDS>
 __global__ __launch_bounds__(kFuThreads, 1) void gcm_fused_kernel(BatchArgs a,
                                                                  const RecPre* __restrict__ pre) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t laneoff = (lane & 31) * 4;
+  const uint32_t laneoff = aes_laneoff(lane);
   const GhLane gl = gh_lane(lane);
   const tlsgpu_record* D = reinterpret_cast<const tlsgpu_record*>(a.descs);
   uint32_t* q = reinterpret_cast<uint32_t*>(s_lds + Q_OFF);

@@ -544,7 +544,7 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
   }
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t laneoff = (lane & 31) * 4;
+  const uint32_t laneoff = aes_laneoff(lane);
   const GhLane gl = gh_lane(lane);
   const tlsgpu_record* D = reinterpret_cast<const tlsgpu_record*>(a.descs);
   const bool bs_role = wave < (uint32_t)BSW;

@@ -33,7 +33,7 @@ template <bool SEAL, bool RAW, int ROUNDS>
 __global__ __launch_bounds__(kThreads, 1) void gcm_batch_kernel(BatchArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t laneoff = (lane & 31) * 4;
+  const uint32_t laneoff = aes_laneoff(lane);
   const GhLane gl = gh_lane(lane);
 
   fill_aes_lds<kThreads>();
@@ -120,7 +120,7 @@ template <bool SEAL, int ROUNDS>
 __global__ __launch_bounds__(kThreads, 1) void gcm_raw_kernel(BatchArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t laneoff = (lane & 31) * 4;
+  const uint32_t laneoff = aes_laneoff(lane);
   const GhLane gl = gh_lane(lane);
   const uint32_t r = blockIdx.x;
   const RawJob* J = reinterpret_cast<const RawJob*>(a.descs) + r;

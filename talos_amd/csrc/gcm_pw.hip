@@ -30,7 +30,8 @@
 #if TG_PW_HALF
 #define TG_LDS_BYTES 131072
 #else
-#define TG_LDS_BYTES 163840
+// 12 x 8 KiB tables + the T-tables at 64 KiB (gcm_device.h AES_OFF) exceed the LDS
+#error "TG_PW_HALF=0 (12 waves x 8 KiB tables) no longer fits the LDS plan"
 #endif
 #include "gcm_hybrid.h"
 
@@ -44,7 +45,10 @@ constexpr int kPwThreads = 768;
 constexpr uint32_t PW_TAB_BYTES = 8192;  // 2 halves x 16 values x 16 positions x 16 B
 #endif
 constexpr int kPwWaves = kPwThreads / kWave;
-constexpr uint32_t PW_TAB_OFF = 65536;
+// per-wave tables at 0 .. 64 KiB, below the T-tables (AES_OFF): a lookup address
+// is the table's [0, 0, wave * 16 + nibble, position * 16], one v_perm
+constexpr uint32_t PW_TAB_OFF = 0;
+static_assert(PW_TAB_OFF + kPwWaves * PW_TAB_BYTES <= AES_OFF, "per-wave tables overlap the T-tables");
 static_assert(PW_TAB_OFF + kPwWaves * PW_TAB_BYTES <= LDS_BYTES, "per-wave tables exceed LDS");
 
 #ifndef TG_PW_NB
@@ -80,6 +84,8 @@ __device__ __forceinline__ void mulx64(const uint32_t b[4], uint32_t r[4]) {
 
 struct GhNib {
   uint32_t base;     // LDS byte offset of this wave's table
+  uint32_t wb;       // (base >> 8) in every byte: the table's 256-B row index, ORed
+                     // into the nibble planes so the address needs no base add
   uint32_t sw;       // m >= 8 (m = lane % 16): swap the words of each 64-bit half
   uint32_t s;        // then rotate each half right by 4 * (m & 7) bits
   uint32_t cq[4];    // cq[pl].byte[b] = ((k + m) & 15) * 16, k = 8(pl>>1) + 2b + (pl&1)
@@ -98,9 +104,9 @@ struct GhNib {
       const uint32_t a = sw ? hi : lo, b = sw ? lo : hi;
       const uint32_t ylo = __builtin_amdgcn_alignbit(b, a, s);
       const uint32_t yhi = __builtin_amdgcn_alignbit(a, b, s);
-      const uint32_t pl[4] = {ylo & 0x0F0F0F0Fu, (ylo >> 4) & 0x0F0F0F0Fu, yhi & 0x0F0F0F0Fu,
-                              (yhi >> 4) & 0x0F0F0F0Fu};
-      const uint32_t hb = TG_PW_HALF ? base : base + 4096u * h;
+      const uint32_t pl[4] = {(ylo & 0x0F0F0F0Fu) | wb, ((ylo >> 4) & 0x0F0F0F0Fu) | wb,
+                              (yhi & 0x0F0F0F0Fu) | wb, ((yhi >> 4) & 0x0F0F0F0Fu) | wb};
+      const uint32_t hb = 0;
       const int d = TG_PW_HALF ? h : 0;
 #pragma unroll
       for (int q0 = 0; q0 < 4; q0 += TG_PW_QGROUP) {  // 4 * TG_PW_QGROUP lookups in flight
@@ -200,6 +206,7 @@ __device__ __forceinline__ GhNib gh_nib(uint32_t lane, uint32_t base) {
   GhNib g;
   const uint32_t m = lane & 15;
   g.base = base;
+  g.wb = (base >> 8) * 0x01010101u;
   g.sw = m >> 3;
   g.s = 4 * (m & 7);
 #pragma unroll
@@ -223,7 +230,7 @@ __global__ __launch_bounds__(kPwThreads, 1) void gcm_pw_kernel(BatchArgs a,
   if (!pws_selected(a.pws, f.runs, f.recs)) return;  // the queue kernel runs this batch
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t laneoff = (lane & 31) * 4;
+  const uint32_t laneoff = aes_laneoff(lane);
   const tlsgpu_record* D = reinterpret_cast<const tlsgpu_record*>(a.descs);
   fill_aes_lds<kPwThreads, false>();
   __syncthreads();

@@ -2,18 +2,19 @@
 // the record-layer half of ssl3_get_record (ssl/s3_pkt.c:279-495) for the AEAD
 // suites; the cipher half is the batch open kernels (tls1_enc(s, 0)).
 //
-//   wire_frame_kernel   one lane per stream: walks the 5-byte headers
+//   wire_frame_kernel   one wave per stream: walks the 5-byte headers
 //                       (s3_pkt.c:304-341), applies the version / length checks
 //                       (:319-341, :376), reserves a contiguous range of record
-//                       slots (one atomic per stream) and writes the in-place
+//                       slots (one atomic per workgroup) and writes the in-place
 //                       open descriptors (t1_enc.c:951-955);
-//   wire_finish_kernel  one lane per stream: maps the open statuses to the
+//   wire_finish_kernel  one wave per stream: maps the open statuses to the
 //                       reference's alerts in record order (:385-390 decryption
 //                       failed, :450-462 bad_record_mac, :465-469 record
 //                       overflow) and marks the records after the first failure
 //                       as not delivered.
-// Header walks are a dependent chain of small reads per stream, so the
-// parallelism is across streams (connections), as a server's batch has it.
+// Header walks are a dependent chain of small reads per stream: the parallelism
+// is across streams (connections), as a server's batch has it, and each round
+// trip covers many headers (wire_walk).
 #include "tlsgpu_internal.h"
 
 namespace tg {
@@ -47,71 +48,232 @@ __device__ __forceinline__ Hdr read_hdr(const uint8_t* h) {
 }
 
 // The header walk is a chain of dependent reads (each header gives the next
-// one's offset): one memory round trip per record.  It covers up to kSpec
-// headers per round trip by speculating that the next records have the last
-// record's length (a bulk sender's stream is runs of equal-size records): the
-// speculative headers are loaded together, and header k is used only if the
-// real walk lands exactly on it; a misprediction restarts from the real offset.
-constexpr int kSpec = 8;
+// one's offset), so one wave walks one stream and covers many headers per
+// memory round trip in two ways at once:
+//   * a 16 KiB window of the stream at the walk position, loaded by the whole
+//     wave (16 coalesced 1 KiB loads) into LDS: the headers of short, varying
+//     records (Zipf mixes: ~10 per window) are then LDS reads;
+//   * 64 speculative headers, lane k at pos + k * (last record's size): a bulk
+//     sender's runs of equal-size records (16 KiB fragments) need one round
+//     trip per 64 records.
+// A header neither covers starts the next round trip at the walk position.
+constexpr uint32_t kWin = 16384;   // LDS window per wave (bytes)
+constexpr int kFrameWaves = 4;     // streams (waves) per 256-thread workgroup
 
-// Visits the complete records of stream `st` that pass the header checks, in
-// order, at most `limit`, calling visit(index, offset, header) for each.
-template <class Visit>
-__device__ __forceinline__ WireWalk wire_walk(const tlsgpu_wire_stream& st, const uint8_t* w,
-                                              uint32_t limit, Visit&& visit) {
-  WireWalk r = {0, 0, 0};
-  const uint32_t rbuf = st.rbuf_len ? st.rbuf_len : kDefaultRbuf;
-  uint32_t pos = 0, stride = 0;
-  bool stop = false;
-  while (!stop && r.records < limit && pos + kHdr <= st.wire_len) {
-    const uint32_t base = pos, sb = stride;
-    Hdr hs[kSpec];
+// Stream bytes [lo, lo + kWin) into `win`, lo = p rounded down to the
+// 16-B-aligned address; bytes outside [0, len) read as zero (never used: the
+// walk only reads headers inside the stream).
+__device__ __forceinline__ int32_t win_load(const uint8_t* w, uint32_t len, uint32_t p, uint8_t* win,
+                                            uint32_t lane) {
+  const uint32_t sh = (uint32_t)((uintptr_t)(w + p) & 15u);
+  const int32_t lo = (int32_t)p - (int32_t)sh;
+  const uint8_t* A = w + p - sh;
+  uint4 v[kWin / 1024];
 #pragma unroll
-    for (int k = 0; k < kSpec; k++) {  // unconditional loads (clamped into the stream):
-      // a header past the stream end is never used (the walk stops first)
-      const uint32_t p = min(base + (uint32_t)k * sb, st.wire_len - kHdr);
-      hs[k] = read_hdr(w + p);
-    }
-#pragma unroll
-    for (int k = 0; k < kSpec; k++) {
-      if (k > 0 && (sb == 0 || pos != base + (uint32_t)k * sb)) break;  // mispredicted
-      if (r.records >= limit || pos + kHdr > st.wire_len) {
-        stop = true;
-        break;
-      }
-      const Hdr h = hs[k];
-      if (!(st.flags & TLSGPU_WIRE_FIRST_PACKET) && h.ver != st.version) {
-        r.alert = kAlertProtocolVersion;  // s3_pkt.c:319-329
-        stop = true;
-        break;
-      }
-      if ((h.ver >> 8) != 3) {  // SSL3_VERSION_MAJOR, :331-335 (goto err: no alert)
-        r.alert = -1;
-        stop = true;
-        break;
-      }
-      if (h.len > rbuf - kHdr) {  // :337-341
-        r.alert = kAlertRecordOverflow;
-        stop = true;
-        break;
-      }
-      if (pos + kHdr + h.len > st.wire_len) {  // fragment not complete yet
-        stop = true;
-        break;
-      }
-      if (h.len > kMaxEncrypted) {  // :376-380
-        r.alert = kAlertRecordOverflow;
-        stop = true;
-        break;
-      }
-      visit(r.records, pos, h);
-      r.records++;
-      pos += kHdr + h.len;
-      r.consumed = pos;
-      stride = kHdr + h.len;
+  for (int j = 0; j < (int)(kWin / 1024); j++) {
+    const int32_t o = lo + (int32_t)(1024 * j + 16 * lane);
+    const uint8_t* src = A + 1024 * j + 16 * lane;
+    v[j] = make_uint4(0, 0, 0, 0);
+    if (o >= 0 && o + 16 <= (int32_t)len) {
+      v[j] = gload16(src);
+    } else if (o < (int32_t)len && o + 16 > 0) {  // the stream's first / last piece
+      uint32_t q[4] = {0, 0, 0, 0};
+      for (int b = 0; b < 16; b++)
+        if (o + b >= 0 && o + b < (int32_t)len) q[b >> 2] |= (uint32_t)gld<uint8_t>(src)[b] << (8 * (b & 3));
+      v[j] = make_uint4(q[0], q[1], q[2], q[3]);
     }
   }
+#pragma unroll
+  for (int j = 0; j < (int)(kWin / 1024); j++) *reinterpret_cast<uint4*>(win + 1024 * j + 16 * lane) = v[j];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return lo;
+}
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Visits the complete records of stream `st` that pass the header checks, in
+// order, at most `limit`, calling visit(index, offset, header) for each
+// (wave-uniform arguments).  Whole wave, `win` = the wave's kWin LDS bytes.
+template <class Visit>
+__device__ __forceinline__ WireWalk wire_walk(const tlsgpu_wire_stream& st, const uint8_t* w,
+                                              uint32_t limit, uint8_t* win, uint32_t lane,
+                                              Visit&& visit) {
+  WireWalk r = {0, 0, 0};
+  const uint32_t rbuf = st.rbuf_len ? st.rbuf_len : kDefaultRbuf;
+  const uint32_t len = st.wire_len;
+  uint32_t pos = 0, stride = 0;
+  int32_t lo = 0;
+  bool have_win = false;
+  uint32_t cbase = 0, cstride = 0, cnext = 64;  // speculative headers: cnext = next usable lane
+  Hdr cand = {0, 0, 0};
+  while (r.records < limit && pos + kHdr <= len) {
+    Hdr h;
+    if (cnext < 64 && pos == cbase + cnext * cstride) {
+      h.type = uni(__builtin_amdgcn_readlane(cand.type, cnext));
+      h.ver = uni(__builtin_amdgcn_readlane(cand.ver, cnext));
+      h.len = uni(__builtin_amdgcn_readlane(cand.len, cnext));
+      cnext++;
+    } else if (have_win && (int32_t)pos >= lo && (int32_t)(pos + kHdr) <= lo + (int32_t)kWin) {
+      const uint8_t* q = win + ((int32_t)pos - lo);
+      h.type = q[0];
+      h.ver = ((uint32_t)q[1] << 8) | q[2];
+      h.len = ((uint32_t)q[3] << 8) | q[4];
+      h.type = uni(h.type); h.ver = uni(h.ver); h.len = uni(h.len);
+      cnext = 64;
+    } else {  // one round trip: the window at pos and 64 headers at pos + k * stride
+      cbase = pos;
+      cstride = stride;
+      cnext = stride ? 0u : 64u;
+      if (stride) cand = read_hdr(w + min(pos + lane * stride, len - kHdr));
+      lo = win_load(w, len, pos, win, lane);
+      have_win = true;
+      continue;
+    }
+    if (!(st.flags & TLSGPU_WIRE_FIRST_PACKET) && h.ver != st.version) {
+      r.alert = kAlertProtocolVersion;  // s3_pkt.c:319-329
+      break;
+    }
+    if ((h.ver >> 8) != 3) {  // SSL3_VERSION_MAJOR, :331-335 (goto err: no alert)
+      r.alert = -1;
+      break;
+    }
+    if (h.len > rbuf - kHdr) {  // :337-341
+      r.alert = kAlertRecordOverflow;
+      break;
+    }
+    if (pos + kHdr + h.len > len) break;  // fragment not complete yet
+    if (h.len > kMaxEncrypted) {  // :376-380
+      r.alert = kAlertRecordOverflow;
+      break;
+    }
+    visit(r.records, pos, h);
+    r.records++;
+    pos += kHdr + h.len;
+    r.consumed = pos;
+    stride = kHdr + h.len;
+  }
   return r;
+}
+
+// One wave per stream (kFrameWaves streams per workgroup): walk, reserve the
+// stream's descriptor range (one atomic per workgroup), walk again (the window
+// loads now hit the cache) writing the in-place open descriptors.
+__global__ __launch_bounds__(64 * kFrameWaves) void wire_frame_kernel(
+    const tlsgpu_wire_stream* __restrict__ streams, uint32_t n_streams, const uint8_t* wire,
+    const DevSession* __restrict__ sessions, uint32_t n_sessions, uint32_t max_records,
+    tlsgpu_record* __restrict__ recs, tlsgpu_wire_result* __restrict__ results, uint32_t* total) {
+  __shared__ __attribute__((aligned(16))) uint8_t wins[kFrameWaves][kWin];
+  __shared__ uint32_t cnt[kFrameWaves], base_slot;
+  const uint32_t lane = threadIdx.x & 63, wave = uni(threadIdx.x >> 6);
+  const uint32_t s = blockIdx.x * kFrameWaves + wave;
+  const bool active = s < n_streams;
+  tlsgpu_wire_stream st = {};
+  WireWalk walk = {};
+  if (active) {
+    st = streams[s];
+    walk = wire_walk(st, wire + st.wire_off, 0xFFFFFFFFu, wins[wave], lane,
+                     [](uint32_t, uint32_t, const Hdr&) {});
+  }
+  if (lane == 0) cnt[wave] = active ? walk.records : 0u;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t sum = 0;
+    for (int k = 0; k < kFrameWaves; k++) sum += cnt[k];
+    base_slot = sum ? atomicAdd(total, sum) : 0u;
+  }
+  __syncthreads();
+  if (!active) return;
+  uint32_t slot0 = base_slot;
+  for (uint32_t k = 0; k < wave; k++) slot0 += cnt[k];
+  slot0 = uni(slot0);
+  const uint32_t first = walk.records ? slot0 : 0u;
+  const uint8_t* w = wire + st.wire_off;
+  uint32_t n = walk.records;
+  if (first >= max_records) {
+    n = 0;
+  } else if (first + n > max_records) {
+    n = max_records - first;
+  }
+  // explicit nonce length of the session's AEAD (GCM 8, ChaCha 0); an unknown
+  // session still gets descriptors, which the open kernels leave PUBLIC_INVALID
+  uint32_t eiv = 0;
+  if (st.session < n_sessions) {
+    const uint32_t kind = sessions[st.session].kind;
+    eiv = (kind == TLSGPU_AES_128_GCM || kind == TLSGPU_AES_256_GCM) ? 8u : 0u;
+  }
+  // descriptors gathered 64 at a time in the lanes, stored by the whole wave
+  tlsgpu_record d = {};
+  uint32_t held = 0;
+  auto flush = [&](uint32_t upto) {
+    if (lane < held) recs[first + upto - held + lane] = d;
+    held = 0;
+  };
+  const WireWalk w2 = wire_walk(st, w, n, wins[wave], lane, [&](uint32_t i, uint32_t pos, const Hdr& h) {
+    if (lane == held) {
+      d.in_off = st.wire_off + pos + kHdr;
+      d.out_off = d.in_off + eiv;
+      d.seq = st.seq + i;
+      d.session = st.session;
+      d.len_type = (h.type << 24) | h.len;
+    }
+    if (++held == 64) flush(i + 1);
+  });
+  flush(w2.records);
+  if (n != walk.records) {  // truncated at a record boundary: no alert reached
+    walk = w2;
+    walk.alert = 0;
+  }
+  if (lane == 0) {
+    tlsgpu_wire_result r;
+    r.first = n ? first : 0u;
+    r.records = n;
+    r.delivered = n;
+    r.consumed = walk.consumed;
+    r.alert = walk.alert;
+    r.alert_record = n;
+    r.reserved[0] = r.reserved[1] = 0;
+    results[s] = r;
+  }
+}
+
+// One wave per stream: the statuses of 64 records per load, the first failing
+// record found with a ballot (s3_pkt.c alert order: the first failure wins,
+// later records are not delivered).
+__global__ __launch_bounds__(256) void wire_finish_kernel(uint32_t n_streams,
+                                                          tlsgpu_wire_result* __restrict__ results,
+                                                          int32_t* __restrict__ status) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t s = blockIdx.x * 4 + uni(threadIdx.x >> 6);
+  if (s >= n_streams) return;
+  tlsgpu_wire_result r = results[s];
+  bool dead = false;
+  for (uint32_t i0 = 0; i0 < r.records; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    const bool in = i < r.records;
+    int32_t* sp = status + r.first + i;
+    if (dead) {
+      if (in) *sp = TLSGPU_REC_SKIPPED;
+      continue;
+    }
+    const int32_t st = in ? *sp : 0;
+    const int32_t alert = !in ? 0
+                          : st == TLSGPU_REC_BAD_MAC        ? kAlertBadRecordMac
+                          : st == TLSGPU_REC_PUBLIC_INVALID ? kAlertDecryptionFailed
+                          : st > (int32_t)kMaxPlain         ? kAlertRecordOverflow
+                                                            : 0;
+    const uint64_t bad = __ballot(alert != 0);
+    if (!bad) continue;
+    const uint32_t fl = (uint32_t)__builtin_ctzll(bad);  // first failing lane
+    if (lane == fl && alert == kAlertRecordOverflow) *sp = TLSGPU_REC_OVERFLOW;
+    if (in && lane > fl) *sp = TLSGPU_REC_SKIPPED;
+    dead = true;
+    r.alert = __shfl(alert, (int)fl);
+    r.alert_record = i0 + fl;
+    r.delivered = i0 + fl;
+  }
+  if (lane == 0) results[s] = r;
 }
 
 // Reserve k consecutive descriptor slots per lane with ONE atomic per wave on
@@ -131,105 +293,6 @@ __device__ __forceinline__ uint32_t wave_reserve(uint32_t* total, uint32_t k) {
   if (lane == 63 && sum) base = atomicAdd(total, sum);
   base = __shfl(base, 63);
   return base + incl - k;
-}
-
-__global__ __launch_bounds__(256) void wire_frame_kernel(const tlsgpu_wire_stream* __restrict__ streams,
-                                                         uint32_t n_streams, const uint8_t* wire,
-                                                         const DevSession* __restrict__ sessions,
-                                                         uint32_t n_sessions, uint32_t max_records,
-                                                         tlsgpu_record* __restrict__ recs,
-                                                         tlsgpu_wire_result* __restrict__ results,
-                                                         uint32_t* total) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = s < n_streams;
-  tlsgpu_wire_stream st = {};
-  WireWalk walk = {};
-  if (active) {
-    st = streams[s];
-    walk = wire_walk(st, wire + st.wire_off, 0xFFFFFFFFu, [](uint32_t, uint32_t, const Hdr&) {});
-  }
-  const uint32_t slot0 = wave_reserve(total, active ? walk.records : 0u);
-  if (!active) return;
-  const uint32_t first = walk.records ? slot0 : 0u;
-  const uint8_t* w = wire + st.wire_off;
-  uint32_t n = walk.records;
-  if (first >= max_records) {
-    n = 0;
-  } else if (first + n > max_records) {
-    n = max_records - first;
-  }
-  // explicit nonce length of the session's AEAD (GCM 8, ChaCha 0); an unknown
-  // session still gets descriptors, which the open kernels leave PUBLIC_INVALID
-  uint32_t eiv = 0;
-  if (st.session < n_sessions) {
-    const uint32_t kind = sessions[st.session].kind;
-    eiv = (kind == TLSGPU_AES_128_GCM || kind == TLSGPU_AES_256_GCM) ? 8u : 0u;
-  }
-  // second walk (headers now cache-resident) writes the in-place descriptors
-  const WireWalk w2 = wire_walk(st, w, n, [&](uint32_t i, uint32_t pos, const Hdr& h) {
-    tlsgpu_record d;
-    d.in_off = st.wire_off + pos + kHdr;
-    d.out_off = d.in_off + eiv;
-    d.seq = st.seq + i;
-    d.session = st.session;
-    d.len_type = (h.type << 24) | h.len;
-    recs[first + i] = d;
-  });
-  if (n != walk.records) {  // truncated at a record boundary: no alert reached
-    walk = w2;
-    walk.alert = 0;
-  }
-  tlsgpu_wire_result r;
-  r.first = n ? first : 0u;
-  r.records = n;
-  r.delivered = n;
-  r.consumed = walk.consumed;
-  r.alert = walk.alert;
-  r.alert_record = n;
-  r.reserved[0] = r.reserved[1] = 0;
-  results[s] = r;
-}
-
-__global__ __launch_bounds__(256) void wire_finish_kernel(uint32_t n_streams,
-                                                          tlsgpu_wire_result* __restrict__ results,
-                                                          int32_t* __restrict__ status) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n_streams) return;
-  tlsgpu_wire_result r = results[s];
-  bool dead = false;
-  // statuses in groups of 8 loaded together (independent loads, one round trip)
-  for (uint32_t i0 = 0; i0 < r.records; i0 += 8) {
-    int32_t sv[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) sv[k] = i0 + k < r.records ? status[r.first + i0 + k] : 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const uint32_t i = i0 + k;
-      if (i >= r.records) break;
-      int32_t* sp = status + r.first + i;
-      if (dead) {
-        *sp = TLSGPU_REC_SKIPPED;
-        continue;
-      }
-      const int32_t st = sv[k];
-      int32_t alert = 0;
-      if (st == TLSGPU_REC_BAD_MAC) {
-        alert = kAlertBadRecordMac;
-      } else if (st == TLSGPU_REC_PUBLIC_INVALID) {
-        alert = kAlertDecryptionFailed;
-      } else if (st > (int32_t)kMaxPlain) {
-        alert = kAlertRecordOverflow;
-        *sp = TLSGPU_REC_OVERFLOW;
-      }
-      if (alert) {
-        dead = true;
-        r.alert = alert;
-        r.alert_record = i;
-        r.delivered = i;
-      }
-    }
-  }
-  results[s] = r;
 }
 
 // Write-side framing (ssl3_write_bytes / do_ssl3_write, s3_pkt.c:501-762), one
@@ -304,8 +367,8 @@ int launch_wire_frame(const tlsgpu_wire_stream* streams, uint32_t n_streams, con
                       tlsgpu_record* recs, tlsgpu_wire_result* results, uint32_t* total,
                       hipStream_t s) {
   if (n_streams == 0) return 0;
-  // 64-lane groups: the scattered header loads of one wave per CU, not four
-  hipLaunchKernelGGL(wire_frame_kernel, dim3((n_streams + 63) / 64), dim3(64), 0, s, streams,
+  hipLaunchKernelGGL(wire_frame_kernel, dim3((n_streams + kFrameWaves - 1) / kFrameWaves),
+                     dim3(64 * kFrameWaves), 0, s, streams,
                      n_streams, wire, sessions, n_sessions, max_records, recs, results, total);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -313,7 +376,7 @@ int launch_wire_frame(const tlsgpu_wire_stream* streams, uint32_t n_streams, con
 int launch_wire_finish(uint32_t n_streams, tlsgpu_wire_result* results, int32_t* status,
                        hipStream_t s) {
   if (n_streams == 0) return 0;
-  hipLaunchKernelGGL(wire_finish_kernel, dim3((n_streams + 63) / 64), dim3(64), 0, s, n_streams,
+  hipLaunchKernelGGL(wire_finish_kernel, dim3((n_streams + 3) / 4), dim3(256), 0, s, n_streams,
                      results, status);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
