@@ -94,12 +94,15 @@ __device__ __forceinline__ int32_t win_load(const uint8_t* w, uint32_t len, uint
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // Visits the complete records of stream `st` that pass the header checks, in
-// order, at most `limit`, calling visit(index, offset, header) for each
-// (wave-uniform arguments).  Whole wave, `win` = the wave's kWin LDS bytes.
-template <class Visit>
+// order, at most `limit`: visit(index, offset, header) for one record at a time
+// (wave-uniform arguments), bulk(index, k0, m, base, stride, header) for m
+// records accepted at once from the speculative headers — lane k in
+// [k0, k0 + m) holds record index + k - k0 at base + k * stride.  Whole wave,
+// `win` = the wave's kWin LDS bytes.
+template <class Visit, class Bulk>
 __device__ __forceinline__ WireWalk wire_walk(const tlsgpu_wire_stream& st, const uint8_t* w,
                                               uint32_t limit, uint8_t* win, uint32_t lane,
-                                              Visit&& visit) {
+                                              Visit&& visit, Bulk&& bulk) {
   WireWalk r = {0, 0, 0};
   const uint32_t rbuf = st.rbuf_len ? st.rbuf_len : kDefaultRbuf;
   const uint32_t len = st.wire_len;
@@ -111,6 +114,25 @@ __device__ __forceinline__ WireWalk wire_walk(const tlsgpu_wire_stream& st, cons
   while (r.records < limit && pos + kHdr <= len) {
     Hdr h;
     if (cnext < 64 && pos == cbase + cnext * cstride) {
+      // lanes k >= cnext whose header passes every check below and repeats the
+      // stride: records k = cnext .. cnext + m - 1 are accepted together
+      const uint32_t ck = cbase + lane * cstride;
+      const bool ok = lane >= cnext && ck + kHdr <= len &&
+                      ((st.flags & TLSGPU_WIRE_FIRST_PACKET) || cand.ver == st.version) &&
+                      (cand.ver >> 8) == 3 && cand.len <= rbuf - kHdr &&
+                      ck + kHdr + cand.len <= len && cand.len <= kMaxEncrypted &&
+                      cand.len + kHdr == cstride && r.records + (lane - cnext) < limit;
+      const uint64_t run = ~__ballot(ok) >> cnext;  // bit j: lane cnext + j fails
+      const uint32_t m = run ? (uint32_t)__builtin_ctzll(run) : 64u - cnext;
+      if (m != 0) {
+        bulk(r.records, cnext, m, cbase, cstride, cand);
+        r.records += m;
+        pos += m * cstride;
+        r.consumed = pos;
+        stride = cstride;
+        cnext += m;
+        continue;
+      }
       h.type = uni(__builtin_amdgcn_readlane(cand.type, cnext));
       h.ver = uni(__builtin_amdgcn_readlane(cand.ver, cnext));
       h.len = uni(__builtin_amdgcn_readlane(cand.len, cnext));
@@ -174,7 +196,8 @@ __global__ __launch_bounds__(64 * kFrameWaves) void wire_frame_kernel(
   if (active) {
     st = streams[s];
     walk = wire_walk(st, wire + st.wire_off, 0xFFFFFFFFu, wins[wave], lane,
-                     [](uint32_t, uint32_t, const Hdr&) {});
+                     [](uint32_t, uint32_t, const Hdr&) {},
+                     [](uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, const Hdr&) {});
   }
   if (lane == 0) cnt[wave] = active ? walk.records : 0u;
   __syncthreads();
@@ -219,6 +242,17 @@ __global__ __launch_bounds__(64 * kFrameWaves) void wire_frame_kernel(
       d.len_type = (h.type << 24) | h.len;
     }
     if (++held == 64) flush(i + 1);
+  }, [&](uint32_t i, uint32_t k0, uint32_t m, uint32_t base, uint32_t stride, const Hdr& h) {
+    flush(i);  // the held records end at index i
+    if (lane >= k0 && lane < k0 + m) {
+      tlsgpu_record e;
+      e.in_off = st.wire_off + base + lane * stride + kHdr;
+      e.out_off = e.in_off + eiv;
+      e.seq = st.seq + i + (lane - k0);
+      e.session = st.session;
+      e.len_type = (h.type << 24) | h.len;
+      recs[first + i + (lane - k0)] = e;
+    }
   });
   flush(w2.records);
   if (n != walk.records) {  // truncated at a record boundary: no alert reached

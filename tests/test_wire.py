@@ -190,6 +190,13 @@ def test_open_wire_matches_ssl3_get_record(ta, engine, oracle, kind):
     table = ta.SessionTable(engine, 1)
     table.install(0, [params])
     got = run_wire(ta, engine, table, streams, max_records=256)
+    check_against_model(oracle, osess, kind, streams, got)
+    table.close()
+
+
+def check_against_model(oracle, osess, kind, streams, got):
+    """Every stream's result, descriptors, statuses and opened bytes equal the
+    ssl3_get_record model (model_stream)."""
     eiv = 8 if kind in (po.AES_128_GCM, po.AES_256_GCM) else 0
     total = 0
     for i, s in enumerate(streams):
@@ -219,6 +226,56 @@ def test_open_wire_matches_ssl3_get_record(ta, engine, oracle, kind):
                 assert got["wire"][frag_off + eiv:frag_off + eiv + n] == bytes(n), (i, k)
             pos += 5 + ln
     assert got["total"] == total
+
+
+def test_open_wire_long_runs(ta, engine, oracle):
+    """Streams longer than the framing kernel's 16 KiB window and its 64
+    speculative headers: equal-length runs accepted in bulk, runs broken by a
+    different length, a failing header or a tampered record inside a run, and
+    16 KiB records (the finish kernel's 64-record status chunks included)."""
+    rnd = random.Random(77)
+    kind = po.AES_128_GCM
+    key = bytes(rnd.randrange(256) for _ in range(16))
+    fiv = bytes(rnd.randrange(256) for _ in range(4))
+    params = ta.SessionParams(kind, key, fiv)
+    osess = oracle.tls_session(kind, key, fiv)
+
+    def recs(seq0, lens, version=TLS12):
+        out = []
+        for i, n in enumerate(lens):
+            body = oracle.tls_seal(osess, seq0 + i, 23, bytes(rnd.randrange(256) for _ in range(n)))
+            out.append(header(23, version, len(body)) + body)
+        return out
+
+    def stream(parts, seq0):
+        return dict(wire=b"".join(parts), seq=seq0, version=TLS12, first=False, rbuf=0, session=0)
+
+    S = []
+    lens = [100] * 150 + [7, 3000, 1] + [1400] * 70 + [0] * 5 + [rnd.randrange(0, 2000) for _ in range(40)]
+    S.append(stream(recs(10, lens), 10))
+    parts = recs(500, [300] * 140)  # wrong version at record 100, inside a run
+    parts[100] = recs(600, [300], version=0x0301)[0]
+    S.append(stream(parts, 500))
+    parts = recs(1000, [64] * 200)  # tampered record 130: bad_record_mac, 131.. skipped
+    b = bytearray(parts[130])
+    b[20] ^= 1
+    parts[130] = bytes(b)
+    S.append(stream(parts, 1000))
+    S.append(stream(recs(2000, [16384] * 20 + [16000]), 2000))
+    parts = recs(3000, [200] * 90)  # record 70 claims more than rbuf: overflow at its header
+    parts[70] = header(23, TLS12, 16708) + parts[70][5:]
+    S.append(stream(parts, 3000))
+    S.append(stream(recs(4000, [50] * 100) + [recs(4100, [900])[0][:300]], 4000))  # incomplete tail
+    table = ta.SessionTable(engine, 1)
+    table.install(0, [params])
+    got = run_wire(ta, engine, table, S, max_records=1024)
+    check_against_model(oracle, osess, kind, S, got)
+    # capacity cut inside a bulk run: every stream is framed up to what fits
+    got = run_wire(ta, engine, table, S[:1], max_records=90)
+    r = got["results"][0]
+    assert int(r["records"]) == 90 and int(r["alert"]) == 0 and got["total"] == len(lens)
+    assert int(r["consumed"]) == sum(5 + 8 + n + 16 for n in lens[:90])
+    assert all(int(x) >= 0 for x in got["status"][:90])
     table.close()
 
 
