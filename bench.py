@@ -53,18 +53,22 @@ def algo_bytes_per_record(kind_name: str, length: int, op: str) -> int:
     return rd + wr
 
 
-def main_kernel(kind_name: str, op: str, short_records: bool = False) -> str:
-    """Name of the step's dominant kernel as rocprofv3 lists it (the queue kernel's
-    pack variant runs when the batch has records of <= 62 blocks)."""
+def main_kernel(kind_name: str, op: str, short_records: bool = False, short_runs: bool = False) -> str:
+    """Name of the step's dominant kernel as rocprofv3 lists it: the queue kernel's
+    pack variant runs when the batch has records of <= 62 blocks,
+    the per-wave-session kernel when session runs average < 12 records (§4.1d)."""
     import talos_amd as ta
     if "gcm" not in kind_name:   # the LDS-staged TLS kernel (DESIGN.md §4.5); C = seal + open
-        return "tg::chacha_tls_kernel<" if op == "seal+open" else \
+        return "tg::chacha_tls_kernel" if op == "seal+open" else \
             f"tg::chacha_tls_kernel<{'true' if op == 'seal' else 'false'}>"
     rounds = 10 if "128" in kind_name else 14
     seal = "true" if op != "open" else "false"
     impl = ta.get_gcm_impl()
+    pws = os.environ.get("TLSGPU_PWS", "")
+    if impl == "queue" and (pws == "1" or (pws != "0" and short_runs)):
+        return f"tg::gcm_pw_kernel<{seal}, {rounds}>"
     pack = ", true" if short_records and os.environ.get("TLSGPU_PACK", "1") != "0" else ", false"
-    return {"queue": f"tg::gcm_hy_kernel<{seal}, {rounds}, 1024, 0, 2{pack}>",
+    return {"queue": f"tg::gcm_hy_kernel<{seal}, {rounds}, 1024, 0, 2{pack}, 0>",
             "hybrid": f"tg::gcm_hy_kernel<{seal}, {rounds}, 512, 4, 4, false>",
             "bitslice": f"tg::gcm_hy_kernel<{seal}, {rounds}, 512, 8, 4, false>",
             "fused": f"tg::gcm_fused_kernel<{seal}, {rounds}>",
@@ -261,7 +265,10 @@ def main():
     algo = sum(algo_bytes_per_record(kind_name, int(l), op) for l in
                ([rec_len] * wl.n if lengths is None else lengths.tolist()))
     achieved = algo / per_launch_s / 1e9
-    traffic, traffic_src = load_traffic(args.config, main_kernel(kind_name, op, CONFIGS[args.config][3] is None))
+    # session runs of the batch (prep-pass selection, tlsgpu_internal.h pws_selected)
+    runs = per_gpu if args.interleave and sessions > 1 else min(sessions, per_gpu)
+    kernel = main_kernel(kind_name, op, CONFIGS[args.config][3] is None, runs * 12 > per_gpu)
+    traffic, traffic_src = load_traffic(args.config, kernel)
 
     line = {
         "metric": METRIC if args.config == "B" else
@@ -289,7 +296,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "algorithmic_bytes_per_launch": algo,
-                     "kernel": main_kernel(kind_name, op, CONFIGS[args.config][3] is None), "traffic_source": traffic_src,
+                     "kernel": kernel, "traffic_source": traffic_src,
                      "timing": "HIP events around each whole step on the engine stream "
                                "(prep pass + status memset + main kernel)"},
     }

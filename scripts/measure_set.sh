@@ -2,7 +2,7 @@
 # Measurement set for a round (run on the GPU box via gpurun):
 #   bench lines: B (metric), B at S = 1 / 65,536 sessions and interleaved, C, D,
 #   the box's copy bandwidth, host-resident B (tlsgpu_open_host), the pinned
-#   PCIe rates, wire B (tlsgpu_open_wire); then PMC passes (scripts/pmc.sh) for
+#   PCIe rates, wire B / C / D (tlsgpu_open_wire); then PMC passes (scripts/pmc.sh) for
 #   B, C and D.
 # usage: scripts/measure_set.sh TAG [--no-pmc]
 set -o pipefail
@@ -27,7 +27,9 @@ run C --config C &&
 run D --config D &&
 run host_B --mode host --no-cpu-baseline --steps 8 --warmup 2 &&
 run pcie --mode pcie &&
-run wire_B --mode wire --no-cpu-baseline || exit $?
+run wire_B --mode wire --no-cpu-baseline &&
+run wire_C --mode wire --config C --no-cpu-baseline &&
+run wire_D --mode wire --config D --no-cpu-baseline || exit $?
 [ "$2" = "--no-pmc" ] && exit 0
 for c in B C D; do
   bash scripts/pmc.sh $TAG/pmc$c --config $c || exit $?
