@@ -16,19 +16,9 @@
 namespace tg {
 
 // v_bitop3_b32: D bit = imm[(a<<2)|(b<<1)|c] (0xF0 = a, 0xCC = b, 0xAA = c).
-#define bop3(a, b, c, imm)                                                            \
-  ({                                                                                 \
-    uint32_t _d;                                                                     \
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:" #imm : "=v"(_d) : "v"(a), "v"(b), "v"(c)); \
-    _d;                                                                              \
-  })
-// same with a wave-uniform third operand in an SGPR (round-key words)
-#define bop3s(a, b, c, imm)                                                           \
-  ({                                                                                 \
-    uint32_t _d;                                                                     \
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:" #imm : "=v"(_d) : "v"(a), "v"(b), "s"(c)); \
-    _d;                                                                              \
-  })
+#define bop3(a, b, c, imm) __builtin_amdgcn_bitop3_b32((a), (b), (c), (imm))
+// same with a wave-uniform third operand (round-key words: may stay in an SGPR)
+#define bop3s(a, b, c, imm) __builtin_amdgcn_bitop3_b32((a), (b), (c), (imm))
 
 }  // namespace tg
 

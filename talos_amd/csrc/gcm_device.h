@@ -67,11 +67,17 @@ __device__ __forceinline__ uint32_t taddr(uint32_t w, uint32_t laneoff) {
 }
 __device__ __forceinline__ uint32_t rotl16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
 // three-input XOR in one VALU op: v_bitop3_b32 with truth table 0x96 (gfx950
-// has no v_xor3_b32; hipcc does not form bitop3 from these ^ chains)
+// has no v_xor3_b32; hipcc does not form bitop3 from these ^ chains).  The
+// builtin, not inline asm: a wave-uniform operand (round-key word) stays in
+// its SGPR instead of being copied to a VGPR first, and the scheduler sees it.
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#ifdef TG_XOR3_ASM  // opaque to the scheduler: gcm_pw.hip (the builtin's schedule spills there)
   uint32_t d;
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
   return d;
+#else
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#endif
 }
 
 #define TE0(w, r) lds_u32(taddr<r>((w), laneoff))

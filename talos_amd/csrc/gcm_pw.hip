@@ -33,6 +33,7 @@
 // 12 x 8 KiB tables + the T-tables at 64 KiB (gcm_device.h AES_OFF) exceed the LDS
 #error "TG_PW_HALF=0 (12 waves x 8 KiB tables) no longer fits the LDS plan"
 #endif
+#define TG_XOR3_ASM  // xor3 as inline asm here: the builtin's freer schedule spills this kernel
 #include "gcm_hybrid.h"
 
 namespace tg {
