@@ -180,24 +180,36 @@ __device__ __forceinline__ WireWalk wire_walk(const tlsgpu_wire_stream& st, cons
 }
 
 // One wave per stream (kFrameWaves streams per workgroup): walk, reserve the
-// stream's descriptor range (one atomic per workgroup), walk again (the window
-// loads now hit the cache) writing the in-place open descriptors.
+// stream's descriptor range (one atomic per workgroup), then write the in-place
+// open descriptors from the walk's LDS list of (offset, type|length) — or, for
+// a stream of more than kList records, walk again (the window loads now hit
+// the cache) writing them.
+constexpr uint32_t kList = 1024;  // records per stream remembered by the first walk
 __global__ __launch_bounds__(64 * kFrameWaves) void wire_frame_kernel(
     const tlsgpu_wire_stream* __restrict__ streams, uint32_t n_streams, const uint8_t* wire,
     const DevSession* __restrict__ sessions, uint32_t n_sessions, uint32_t max_records,
     tlsgpu_record* __restrict__ recs, tlsgpu_wire_result* __restrict__ results, uint32_t* total) {
   __shared__ __attribute__((aligned(16))) uint8_t wins[kFrameWaves][kWin];
+  __shared__ uint2 lists[kFrameWaves][kList];  // {offset, type << 24 | length}
   __shared__ uint32_t cnt[kFrameWaves], base_slot;
   const uint32_t lane = threadIdx.x & 63, wave = uni(threadIdx.x >> 6);
   const uint32_t s = blockIdx.x * kFrameWaves + wave;
   const bool active = s < n_streams;
+  uint2* list = lists[wave];
   tlsgpu_wire_stream st = {};
   WireWalk walk = {};
   if (active) {
     st = streams[s];
     walk = wire_walk(st, wire + st.wire_off, 0xFFFFFFFFu, wins[wave], lane,
-                     [](uint32_t, uint32_t, const Hdr&) {},
-                     [](uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, const Hdr&) {});
+                     [&](uint32_t i, uint32_t pos, const Hdr& h) {
+                       if (lane == 0 && i < kList) list[i] = make_uint2(pos, (h.type << 24) | h.len);
+                     },
+                     [&](uint32_t i, uint32_t k0, uint32_t m, uint32_t base, uint32_t stride,
+                         const Hdr& h) {
+                       const uint32_t j = i + lane - k0;
+                       if (lane >= k0 && lane < k0 + m && j < kList)
+                         list[j] = make_uint2(base + lane * stride, (h.type << 24) | h.len);
+                     });
   }
   if (lane == 0) cnt[wave] = active ? walk.records : 0u;
   __syncthreads();
@@ -226,38 +238,63 @@ __global__ __launch_bounds__(64 * kFrameWaves) void wire_frame_kernel(
     const uint32_t kind = sessions[st.session].kind;
     eiv = (kind == TLSGPU_AES_128_GCM || kind == TLSGPU_AES_256_GCM) ? 8u : 0u;
   }
-  // descriptors gathered 64 at a time in the lanes, stored by the whole wave
-  tlsgpu_record d = {};
-  uint32_t held = 0;
-  auto flush = [&](uint32_t upto) {
-    if (lane < held) recs[first + upto - held + lane] = d;
-    held = 0;
-  };
-  const WireWalk w2 = wire_walk(st, w, n, wins[wave], lane, [&](uint32_t i, uint32_t pos, const Hdr& h) {
-    if (lane == held) {
-      d.in_off = st.wire_off + pos + kHdr;
-      d.out_off = d.in_off + eiv;
-      d.seq = st.seq + i;
-      d.session = st.session;
-      d.len_type = (h.type << 24) | h.len;
+  if (walk.records <= kList) {  // descriptors from the list, 64 per wave store
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      if (i < n) {
+        const uint2 e = list[i];
+        tlsgpu_record d;
+        d.in_off = st.wire_off + e.x + kHdr;
+        d.out_off = d.in_off + eiv;
+        d.seq = st.seq + i;
+        d.session = st.session;
+        d.len_type = e.y;
+        recs[first + i] = d;
+      }
     }
-    if (++held == 64) flush(i + 1);
-  }, [&](uint32_t i, uint32_t k0, uint32_t m, uint32_t base, uint32_t stride, const Hdr& h) {
-    flush(i);  // the held records end at index i
-    if (lane >= k0 && lane < k0 + m) {
-      tlsgpu_record e;
-      e.in_off = st.wire_off + base + lane * stride + kHdr;
-      e.out_off = e.in_off + eiv;
-      e.seq = st.seq + i + (lane - k0);
-      e.session = st.session;
-      e.len_type = (h.type << 24) | h.len;
-      recs[first + i + (lane - k0)] = e;
+    if (n != walk.records) {  // truncated at a record boundary: no alert reached
+      const uint2 e = n ? list[n - 1] : make_uint2(0, 0);
+      walk.records = n;
+      walk.consumed = n ? e.x + kHdr + (e.y & 0xFFFFFFu) : 0u;
+      walk.alert = 0;
     }
-  });
-  flush(w2.records);
-  if (n != walk.records) {  // truncated at a record boundary: no alert reached
-    walk = w2;
-    walk.alert = 0;
+  } else {
+    // descriptors gathered 64 at a time in the lanes, stored by the whole wave
+    tlsgpu_record d = {};
+    uint32_t held = 0;
+    auto flush = [&](uint32_t upto) {
+      if (lane < held) recs[first + upto - held + lane] = d;
+      held = 0;
+    };
+    const WireWalk w2 = wire_walk(st, w, n, wins[wave], lane, [&](uint32_t i, uint32_t pos, const Hdr& h) {
+      if (lane == held) {
+        d.in_off = st.wire_off + pos + kHdr;
+        d.out_off = d.in_off + eiv;
+        d.seq = st.seq + i;
+        d.session = st.session;
+        d.len_type = (h.type << 24) | h.len;
+      }
+      if (++held == 64) flush(i + 1);
+    }, [&](uint32_t i, uint32_t k0, uint32_t m, uint32_t base, uint32_t stride, const Hdr& h) {
+      flush(i);  // the held records end at index i
+      if (lane >= k0 && lane < k0 + m) {
+        tlsgpu_record e;
+        e.in_off = st.wire_off + base + lane * stride + kHdr;
+        e.out_off = e.in_off + eiv;
+        e.seq = st.seq + i + (lane - k0);
+        e.session = st.session;
+        e.len_type = (h.type << 24) | h.len;
+        recs[first + i + (lane - k0)] = e;
+      }
+    });
+    flush(w2.records);
+    if (n != walk.records) {  // truncated at a record boundary: no alert reached
+      walk = w2;
+      walk.alert = 0;
+    }
   }
   if (lane == 0) {
     tlsgpu_wire_result r;

@@ -266,9 +266,12 @@ def test_open_wire_long_runs(ta, engine, oracle):
     parts[70] = header(23, TLS12, 16708) + parts[70][5:]
     S.append(stream(parts, 3000))
     S.append(stream(recs(4000, [50] * 100) + [recs(4100, [900])[0][:300]], 4000))  # incomplete tail
+    # more records than the framing kernel's per-stream list (kList = 1024): second walk
+    long_lens = [rnd.randrange(0, 40) for _ in range(1100)]
+    S.append(stream(recs(6000, long_lens), 6000))
     table = ta.SessionTable(engine, 1)
     table.install(0, [params])
-    got = run_wire(ta, engine, table, S, max_records=1024)
+    got = run_wire(ta, engine, table, S, max_records=4096)
     check_against_model(oracle, osess, kind, S, got)
     # capacity cut inside a bulk run: every stream is framed up to what fits
     got = run_wire(ta, engine, table, S[:1], max_records=90)
@@ -276,6 +279,12 @@ def test_open_wire_long_runs(ta, engine, oracle):
     assert int(r["records"]) == 90 and int(r["alert"]) == 0 and got["total"] == len(lens)
     assert int(r["consumed"]) == sum(5 + 8 + n + 16 for n in lens[:90])
     assert all(int(x) >= 0 for x in got["status"][:90])
+    # capacity cut in the second-walk path
+    got = run_wire(ta, engine, table, S[-1:], max_records=1050)
+    r = got["results"][0]
+    assert int(r["records"]) == 1050 and int(r["alert"]) == 0 and got["total"] == len(long_lens)
+    assert int(r["consumed"]) == sum(5 + 8 + n + 16 for n in long_lens[:1050])
+    assert all(int(x) >= 0 for x in got["status"][:1050])
     table.close()
 
 
