@@ -45,12 +45,12 @@ CONFIGS = {
 }
 
 
-def algo_bytes_per_record(kind_name: str, length: int, op: str) -> int:
+def algo_bytes_per_record(kind_name: str, length: int, op: str, read_only: bool = False) -> int:
     """read explicit nonce + ct + tag + 32-B descriptor, write pt + status."""
     eiv = 8 if "gcm" in kind_name else 0
     rd = eiv + length + 16 + 32
     wr = length + 4
-    return rd + wr
+    return rd if read_only else rd + wr
 
 
 def main_kernel(kind_name: str, op: str, short_records: bool = False, short_runs: bool = False) -> str:
@@ -265,6 +265,8 @@ def main():
     algo = sum(algo_bytes_per_record(kind_name, int(l), op) for l in
                ([rec_len] * wl.n if lengths is None else lengths.tolist()))
     achieved = algo / per_launch_s / 1e9
+    algo_rd = sum(algo_bytes_per_record(kind_name, int(l), op, True) for l in
+                  ([rec_len] * wl.n if lengths is None else lengths.tolist()))
     # session runs of the batch (prep-pass selection, tlsgpu_internal.h pws_selected)
     runs = per_gpu if args.interleave and sessions > 1 else min(sessions, per_gpu)
     kernel = main_kernel(kind_name, op, CONFIGS[args.config][3] is None, runs * 12 > per_gpu)
@@ -296,6 +298,9 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "algorithmic_bytes_per_launch": algo,
+                     # north_star prices the "HBM-read roofline": the read half alone
+                     "read_achieved": round(algo_rd / per_launch_s / 1e9, 1),
+                     "read_frac": round(algo_rd / per_launch_s / 1e9 / HBM_PEAK_GBS, 4),
                      "kernel": kernel, "traffic_source": traffic_src,
                      "timing": "HIP events around each whole step on the engine stream "
                                "(prep pass + status memset + main kernel)"},
