@@ -53,7 +53,8 @@ def algo_bytes_per_record(kind_name: str, length: int, op: str, read_only: bool 
     return rd if read_only else rd + wr
 
 
-def main_kernel(kind_name: str, op: str, short_records: bool = False, short_runs: bool = False) -> str:
+def main_kernel(kind_name: str, op: str, short_records: bool = False, short_runs: bool = False,
+                records: int = 1 << 30) -> str:
     """Name of the step's dominant kernel as rocprofv3 lists it: the queue kernel's
     pack variant runs when the batch has records of <= 62 blocks,
     the per-wave-session kernel when session runs average < 12 records (§4.1d)."""
@@ -64,6 +65,9 @@ def main_kernel(kind_name: str, op: str, short_records: bool = False, short_runs
     rounds = 10 if "128" in kind_name else 14
     seal = "true" if op != "open" else "false"
     impl = ta.get_gcm_impl()
+    if impl == "split" or (impl == "auto" and records <= 512):  # small batch: <= 2 records per CU
+        return f"tg::gcm_raw_kernel<{seal}, {rounds}, true>"
+    impl = "queue" if impl == "auto" else impl
     pws = os.environ.get("TLSGPU_PWS", "")
     if impl == "queue" and (pws == "1" or (pws != "0" and short_runs)):
         return f"tg::gcm_pw_kernel<{seal}, {rounds}>"
@@ -269,7 +273,7 @@ def main():
                   ([rec_len] * wl.n if lengths is None else lengths.tolist()))
     # session runs of the batch (prep-pass selection, tlsgpu_internal.h pws_selected)
     runs = per_gpu if args.interleave and sessions > 1 else min(sessions, per_gpu)
-    kernel = main_kernel(kind_name, op, CONFIGS[args.config][3] is None, runs * 12 > per_gpu)
+    kernel = main_kernel(kind_name, op, CONFIGS[args.config][3] is None, runs * 12 > per_gpu, wl.n)
     traffic, traffic_src = load_traffic(args.config, kernel)
 
     line = {

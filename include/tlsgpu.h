@@ -280,7 +280,12 @@ uint64_t tlsgpu_seal_wire_size(int aead, uint32_t data_len, uint32_t max_fragmen
     uint32_t tag_len);
 
 /* GCM TLS batch kernel selection (process-wide; results are identical).
- * TLSGPU_GCM_QUEUE (default): a prep pass computes every record's E_K(J0) and
+ * TLSGPU_GCM_AUTO (default): TLSGPU_GCM_SPLIT for batches of at most two
+ * records per CU of the device, TLSGPU_GCM_QUEUE for larger ones.
+ * TLSGPU_GCM_SPLIT: one record per 16-wave workgroup, the record's blocks split
+ * over the waves (latency: a 16 KiB record in ~20 us instead of one wave's
+ * serial pass).
+ * TLSGPU_GCM_QUEUE: a prep pass computes every record's E_K(J0) and
  * round-1/2 constants, then 16 T-table waves per CU (AES rounds as LDS
  * lookups) pull records from a per-session-run queue.  Records of <= 62
  * blocks share a wave in packs (environment TLSGPU_PACK=0 turns packs off).
@@ -290,11 +295,12 @@ uint64_t tlsgpu_seal_wire_size(int aead, uint32_t data_len, uint32_t max_fragmen
  * TLSGPU_GCM_BITSLICE: 8 bitsliced waves per CU.
  * TLSGPU_GCM_FUSED: 8 waves per CU, each running a bitsliced record pair with
  * a T-table record interleaved into its AES rounds.
- * The environment variable TLSGPU_GCM_IMPL=queue|ttable|hybrid|bitslice|fused
- * sets the initial value.  The per-call EVP path always uses TTABLE. */
+ * The environment variable TLSGPU_GCM_IMPL=auto|split|queue|ttable|hybrid|bitslice|fused
+ * sets the initial value.  The per-call EVP path always uses the split kernel
+ * on its raw jobs. */
 enum tlsgpu_gcm_impl {
   TLSGPU_GCM_BITSLICE = 0, TLSGPU_GCM_TTABLE = 1, TLSGPU_GCM_HYBRID = 2, TLSGPU_GCM_QUEUE = 3,
-  TLSGPU_GCM_FUSED = 4
+  TLSGPU_GCM_FUSED = 4, TLSGPU_GCM_SPLIT = 5, TLSGPU_GCM_AUTO = 6
 };
 int tlsgpu_set_gcm_impl(int impl);
 int tlsgpu_get_gcm_impl(void);

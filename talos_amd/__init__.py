@@ -343,13 +343,14 @@ class SessionTable:
             self.handle = None
 
 
-GCM_BITSLICE, GCM_TTABLE, GCM_HYBRID, GCM_QUEUE, GCM_FUSED = 0, 1, 2, 3, 4
+GCM_BITSLICE, GCM_TTABLE, GCM_HYBRID, GCM_QUEUE, GCM_FUSED, GCM_SPLIT, GCM_AUTO = 0, 1, 2, 3, 4, 5, 6
 _GCM_IMPLS = {"bitslice": GCM_BITSLICE, "ttable": GCM_TTABLE, "hybrid": GCM_HYBRID,
-              "queue": GCM_QUEUE, "fused": GCM_FUSED}
+              "queue": GCM_QUEUE, "fused": GCM_FUSED, "split": GCM_SPLIT, "auto": GCM_AUTO}
 
 
 def set_gcm_impl(impl: int | str) -> None:
-    """Select the GCM TLS batch kernel (tlsgpu_set_gcm_impl): queue|ttable|hybrid|bitslice|fused."""
+    """Select the GCM TLS batch kernel (tlsgpu_set_gcm_impl):
+    auto|split|queue|ttable|hybrid|bitslice|fused."""
     if isinstance(impl, str):
         impl = _GCM_IMPLS[impl]
     _check(load_library().tlsgpu_set_gcm_impl(impl), "tlsgpu_set_gcm_impl")

@@ -269,7 +269,9 @@ static int initial_gcm_impl() {
   if (v && strcmp(v, "bitslice") == 0) return TLSGPU_GCM_BITSLICE;
   if (v && strcmp(v, "hybrid") == 0) return TLSGPU_GCM_HYBRID;
   if (v && strcmp(v, "fused") == 0) return TLSGPU_GCM_FUSED;
-  return TLSGPU_GCM_QUEUE;
+  if (v && strcmp(v, "queue") == 0) return TLSGPU_GCM_QUEUE;
+  if (v && strcmp(v, "split") == 0) return TLSGPU_GCM_SPLIT;
+  return TLSGPU_GCM_AUTO;
 }
 // The bitsliced / hybrid / fused GCM variants measured slower than the queue
 // kernel; they are compiled only with `make EXPERIMENTAL=1`
@@ -280,13 +282,14 @@ static constexpr bool kExperimental = true;
 static constexpr bool kExperimental = false;
 #endif
 static bool impl_built(int impl) {
-  return impl == TLSGPU_GCM_QUEUE || impl == TLSGPU_GCM_TTABLE || kExperimental;
+  return impl == TLSGPU_GCM_QUEUE || impl == TLSGPU_GCM_TTABLE || impl == TLSGPU_GCM_SPLIT ||
+         impl == TLSGPU_GCM_AUTO || kExperimental;
 }
 static std::atomic<int> g_gcm_impl{impl_built(initial_gcm_impl()) ? initial_gcm_impl()
-                                                                 : (int)TLSGPU_GCM_QUEUE};
+                                                                 : (int)TLSGPU_GCM_AUTO};
 
 extern "C" int tlsgpu_set_gcm_impl(int impl) {
-  if (impl < TLSGPU_GCM_BITSLICE || impl > TLSGPU_GCM_FUSED)
+  if (impl < TLSGPU_GCM_BITSLICE || impl > TLSGPU_GCM_AUTO)
     return fail(TLSGPU_EINVAL, "unknown gcm impl %d", impl);
   if (!impl_built(impl))
     return fail(TLSGPU_EINVAL, "gcm impl %d not built (make EXPERIMENTAL=1)", impl);
@@ -408,7 +411,14 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   a.pack = g_pack;
   a.pws = g_pws;
   int groups = groups_for(t->eng, n, &a.records_per_group);
-  if (raw) {
+  const int sel_impl = g_gcm_impl.load();
+  // small TLS batches (at most two records per CU): one record per workgroup,
+  // its blocks split over the 16 waves, instead of one wave per record
+  // (measured crossover, 16 KiB records: split 47 vs 77 us at 512 records,
+  // 93 vs 81 us at 1,024)
+  const bool split = !raw && (sel_impl == TLSGPU_GCM_SPLIT ||
+                              (sel_impl == TLSGPU_GCM_AUTO && n <= 2u * (uint32_t)t->eng->num_cus));
+  if (raw || split) {
     // raw EVP jobs: latency, not throughput — one workgroup per job, so a
     // batch of jobs on different contexts runs side by side instead of one
     // session run (table rebuild) after another inside one workgroup
@@ -417,9 +427,11 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   }
   // records whose session is empty/invalid keep this status
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)d_status, (int)TLSGPU_REC_PUBLIC_INVALID, n, s));
-  const int impl = raw ? TLSGPU_GCM_TTABLE : g_gcm_impl.load();
-  const bool gcm_pre =
-      impl != TLSGPU_GCM_TTABLE && (have[TLSGPU_AES_128_GCM] || have[TLSGPU_AES_256_GCM]);
+  const int impl = raw ? TLSGPU_GCM_TTABLE
+                       : split ? TLSGPU_GCM_SPLIT
+                       : sel_impl == TLSGPU_GCM_AUTO ? TLSGPU_GCM_QUEUE : sel_impl;
+  const bool gcm_pre = impl != TLSGPU_GCM_TTABLE && impl != TLSGPU_GCM_SPLIT &&
+                       (have[TLSGPU_AES_128_GCM] || have[TLSGPU_AES_256_GCM]);
   // per-stream scratch: [RecPre x n (queue kernels) | kCtlBytes control words |
   // checked descriptors x n].  Control words per key size k (0: AES-128, 1:
   // AES-256): per-workgroup record counters of the per-wave-session kernel at
@@ -465,6 +477,8 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
     int rc;
     if (impl == TLSGPU_GCM_TTABLE) {
       rc = launch_gcm(a, seal, raw, rounds, groups, s);
+    } else if (impl == TLSGPU_GCM_SPLIT) {
+      rc = launch_gcm_split(a, seal, rounds, s);
     } else {
       rc = launch_gcm_prep(a, pre, seal, rounds, s);
       if (rc == 0) {

@@ -106,17 +106,19 @@ __global__ __launch_bounds__(kThreads, 1) void gcm_batch_kernel(BatchArgs a) {
   }
 }
 
-// Raw EVP jobs (EVP_AEAD_CTX_seal/open, any nonce / AAD length): one job per
-// workgroup and the job's blocks split over the 16 waves, for latency — a
-// synchronous EVP call waits for its one job, and a coalesced batch runs its
-// jobs side by side on as many CUs.  Wave w takes the 64-aligned block range
+// Raw EVP jobs (EVP_AEAD_CTX_seal/open, any nonce / AAD length; TLS = false)
+// or the records of a small TLS batch (TLS = true: tlsgpu_record descriptors,
+// parse_tls): one job per workgroup and the job's blocks split over the 16
+// waves, for latency — a synchronous EVP call waits for its one job, a small
+// batch leaves most CUs idle with one wave per record, and a coalesced batch
+// runs its jobs side by side on as many CUs.  Wave w takes the 64-aligned block range
 // [64 * spw * w, 64 * spw * (w + 1)); its lane chains are the record's chains
 // restricted to that range, so their weights are H^(nb + 1 - jlast) as in the
 // one-wave form: the last range closes with the lengths block as usual, the
 // others raise their chains by (H^64)^q with q extra Horner steps and finish
 // with one Shoup multiply.  The 16 partial GHASH values meet in LDS and wave 0
 // forms / checks the tag (and zero-fills on failure) after the barrier.
-template <bool SEAL, int ROUNDS>
+template <bool SEAL, int ROUNDS, bool TLS = false>
 __global__ __launch_bounds__(kThreads, 1) void gcm_raw_kernel(BatchArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -124,7 +126,8 @@ __global__ __launch_bounds__(kThreads, 1) void gcm_raw_kernel(BatchArgs a) {
   const GhLane gl = gh_lane(lane);
   const uint32_t r = blockIdx.x;
   const RawJob* J = reinterpret_cast<const RawJob*>(a.descs) + r;
-  const uint32_t sid = __builtin_amdgcn_readfirstlane(J->session);
+  const tlsgpu_record* D = reinterpret_cast<const tlsgpu_record*>(a.descs) + r;
+  const uint32_t sid = __builtin_amdgcn_readfirstlane(TLS ? as_const(D)[6] : J->session);
   const bool in_range = sid < a.n_sessions;
   const DevSession* __restrict__ S = a.sessions + (in_range ? sid : 0);
   const uint32_t kind = as_const(&S->kind)[0];
@@ -133,7 +136,13 @@ __global__ __launch_bounds__(kThreads, 1) void gcm_raw_kernel(BatchArgs a) {
   load_session_tables<kThreads>(a.gcm_tables + sid);
   __syncthreads();
   RecCtx rc;
-  parse_raw<SEAL>(*J, S, rc);
+  if (TLS) {
+    // every wave parses (same descriptor): a publicly invalid record returns
+    // from all of them before the barrier below
+    if (!parse_tls<SEAL>(load_desc(D), S, a.in, a.out, a.status + r, lane, rc)) return;
+  } else {
+    parse_raw<SEAL>(*J, S, rc);
+  }
   cu32* rk = as_const(S->rk);
   const uint32_t nb = (rc.n + 15) >> 4;
   const uint32_t nsteps = (nb + kWave - 1) / kWave;
@@ -193,10 +202,16 @@ __global__ __launch_bounds__(kThreads, 1) void gcm_raw_kernel(BatchArgs a) {
   gcm_tag<SEAL>(rc, t, ek0, S, a.status + r, lane);
 }
 
-template <bool SEAL, int ROUNDS>
+template <bool SEAL, int ROUNDS, bool TLS = false>
 static int launch_raw(const BatchArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((gcm_raw_kernel<SEAL, ROUNDS>), dim3(a.n), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL((gcm_raw_kernel<SEAL, ROUNDS, TLS>), dim3(a.n), dim3(kThreads), 0, s, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_gcm_split(const BatchArgs& a, bool seal, int rounds, hipStream_t s) {
+  if (a.n == 0) return 0;
+  if (rounds == 10) return seal ? launch_raw<true, 10, true>(a, s) : launch_raw<false, 10, true>(a, s);
+  return seal ? launch_raw<true, 14, true>(a, s) : launch_raw<false, 14, true>(a, s);
 }
 
 template <bool SEAL, bool RAW, int ROUNDS>

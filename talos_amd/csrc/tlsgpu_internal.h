@@ -218,6 +218,7 @@ static_assert(sizeof(RecPre) == 48, "RecPre layout");
 namespace tg {
 int launch_gcm(const BatchArgs& a, bool seal, bool raw, int rounds, int groups,
                hipStream_t s);
+int launch_gcm_split(const BatchArgs& a, bool seal, int rounds, hipStream_t s);
 int launch_gcm_prep(const BatchArgs& a, RecPre* pre, bool seal, int rounds, hipStream_t s);
 int launch_gcm_queue(const BatchArgs& a, const RecPre* pre, bool seal, int rounds, int groups,
                      hipStream_t s);

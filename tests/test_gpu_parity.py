@@ -247,7 +247,7 @@ def gcm_impl(ta):
     ta.set_gcm_impl(prev)
 
 
-@pytest.mark.parametrize("impl", ["queue", "ttable", "hybrid", "bitslice", "fused"])
+@pytest.mark.parametrize("impl", ["auto", "split", "queue", "ttable", "hybrid", "bitslice", "fused"])
 @pytest.mark.parametrize("name", ["aes-128-gcm", "aes-256-gcm"])
 def test_batch_gcm_impls_all_lengths(ta, engine, oracle, gcm_impl, impl, name):
     gcm_impl(impl)
