@@ -62,3 +62,21 @@ def test_engine_create_fails_loudly_without_gpu(lib):
     import talos_amd as ta
     with pytest.raises(ta.TlsGpuError):
         ta.Engine(0)
+
+
+def test_gcm_impl_selection_without_gpu(lib):
+    """tlsgpu_set/get_gcm_impl (include/tlsgpu.h): the default build selects
+    auto (split for small batches, queue above) and accepts split / queue /
+    ttable; the slower experimental kernels are refused unless built."""
+    import talos_amd as ta
+    prev = ta.get_gcm_impl()
+    try:
+        for name in ("auto", "split", "queue", "ttable"):
+            ta.set_gcm_impl(name)
+            assert ta.get_gcm_impl() == name
+        assert lib.tlsgpu_set_gcm_impl(99) != 0  # unknown impl: an error code, selection kept
+        assert ta.get_gcm_impl() == "ttable"
+    finally:
+        ta.set_gcm_impl(prev)
+    if not os.environ.get("TLSGPU_GCM_IMPL"):
+        assert prev == "auto"
