@@ -575,6 +575,19 @@ __device__ __forceinline__ uint32_t gcm_close_chain(const RecCtx& rc, uint32_t (
   return jlast == -2 ? 0u : (uint32_t)((int32_t)nb + 1 - jlast);
 }
 
+// Zero n bytes at d (the plaintext of a record whose tag failed,
+// evp_aead.c:137-143): the whole wave, 16-B stores for the aligned bulk (a
+// byte loop made a tampered 16 KiB record's wave 256 store rounds long).
+__device__ __forceinline__ void zero_fill_wave(uint8_t* d, uint64_t n, uint32_t lane) {
+  const uint64_t head = min(n, (uint64_t)((16u - ((uintptr_t)d & 15u)) & 15u));
+  if (lane < head) d[lane] = 0;
+  uint4* b = reinterpret_cast<uint4*>(d + head);
+  const uint64_t nb = (n - head) >> 4;
+  for (uint64_t k = lane; k < nb; k += kWave) b[k] = make_uint4(0, 0, 0, 0);
+  const uint64_t done = head + 16 * nb;
+  if (lane < n - done) d[done + lane] = 0;
+}
+
 // Sum the weighted lane values across the wave, form the tag (GHASH ^ E_K(J0))
 // and check it (open, constant time over the tag bytes, zero-fill on failure:
 // e_aes.c:1492-1506, evp_aead.c:137-143) or write it (seal, e_aes.c:1452-1456).
@@ -604,7 +617,7 @@ __device__ __forceinline__ void gcm_tag(const RecCtx& rc, uint32_t (&y)[4], cons
     if (lane < tag_len) diff = rc.tag_byte ^ tbyte;
     bool bad = __any(diff != 0);  // constant-time in the data: every lane compares
     if (bad) {
-      for (uint64_t o = lane; o < rc.zero_len; o += kWave) rc.dst[o] = 0;
+      zero_fill_wave(rc.dst, rc.zero_len, lane);
     }
     if (lane == 0) *status_slot = bad ? TLSGPU_REC_BAD_MAC : rc.ok_status;
   }
