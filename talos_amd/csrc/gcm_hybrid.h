@@ -700,7 +700,21 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
             r = queue_take(q, 1, lane);
             if (r >= run_end) break;
           }
+#ifndef TG_NO_TAIL_PRIO
+          // the run's last claims finish last: issue priority by claim order
+          // over the final records, so the run's tail ends together instead of
+          // one straggler per SIMD running alone before the barrier
+          const uint32_t left = run_end - r;
+          if (!BSW && !PACK && left <= 3 * kWaves) {
+            if (left <= kWaves) __builtin_amdgcn_s_setprio(3);
+            else if (left <= 2 * kWaves) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(1);
+          }
+#endif
           hy_tt_record<SEAL, ROUNDS, NB>(a, pre, r, S, lane, laneoff, gl);
+#ifndef TG_NO_TAIL_PRIO
+          if (!BSW && !PACK) __builtin_amdgcn_s_setprio(0);
+#endif
         }
       }
     }
