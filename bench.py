@@ -38,11 +38,15 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 GIB = float(1 << 30)
 
 CONFIGS = {
-    # name: (kind, records per GPU, sessions, record_len or None(zipf), seed, op)
+    # name: (kind, records per GPU, sessions per GPU, record_len or None(zipf), seed, op)
     "B": ("aes-128-gcm", 65536, 1024, 16384, 0x5EED0001, "open"),
     "C": ("chacha20-poly1305", 1 << 20, 4096, 1400, 0x5EED0002, "seal+open"),
     "D": ("aes-256-gcm", 1 << 18, 1024, None, 0x5EED0003, "open"),
+    # configs[4]: ONE batch of 512 Ki x 16 KiB records (8,192 sessions) split
+    # across 8 GPUs; GPU r opens shard r (records [64 Ki r, 64 Ki (r + 1)))
+    "E": ("aes-128-gcm", 65536, 1024, 16384, 0x5EED0004, "open"),
 }
+E_GPUS = 8   # config E's batch is defined over 8 shards
 
 
 def algo_bytes_per_record(kind_name: str, length: int, op: str, read_only: bool = False) -> int:
@@ -193,6 +197,10 @@ def main():
         return pcie_mode(args, eng)
     cp = ControlPlane(world)   # gloo control plane: barrier + max over ranks only
 
+    # N > 1 GPUs run BASELINE configs[4] (config E) unless a config is named:
+    # the headline metric's multi-GPU line
+    if world > 1 and args.config == "B" and not args.records and not args.sessions:
+        args.config = "E"
     kind_name, per_gpu, sessions, rec_len, seed, op = CONFIGS[args.config]
     if args.records:
         per_gpu = args.records
@@ -200,16 +208,21 @@ def main():
     if args.sessions:
         sessions = min(args.sessions, per_gpu)
     kind = ta.AEAD_NAMES[kind_name]
-    # weak scaling: the global batch has world * per_gpu records; rank r owns a
-    # contiguous equal-byte slice, no data-path collective
-    glob = (np.full(world * per_gpu, rec_len, dtype=np.int64) if rec_len else
-            zipf_lengths(world * per_gpu, seed))
-    lo, hi = shard_by_bytes(glob, world, rank)
+    # weak scaling: ONE global batch of shards x per_gpu records (config E: 8
+    # shards whatever N is, GPU r opens shard r; the others: N shards); rank r
+    # owns a contiguous equal-byte slice, no data-path
+    # collective.  Every rank builds its slice with global record indices
+    # (talos_amd.workload), so shard r is the same bytes at any N and
+    # tests/golden/batch_digests.json E_shard<r> pins it.
+    shards = max(E_GPUS, world) if args.config == "E" else world
+    glob = (np.full(shards * per_gpu, rec_len, dtype=np.int64) if rec_len else
+            zipf_lengths(shards * per_gpu, seed))
+    lo, hi = shard_by_bytes(glob, shards, rank)
     lengths = None if rec_len else glob[lo:hi]
-    wl = Workload(eng, kind, hi - lo, max(1, sessions * (hi - lo) // per_gpu),
-                  seed ^ (rank * 0x100000001), lengths=lengths, record_len=rec_len or 0,
-                  index0=lo, tamper_every=1024 if op == "open" and args.mode != "wire" else 0,
-                  interleave=args.interleave)
+    wl = Workload(eng, kind, shards * per_gpu, shards * sessions, seed, lengths=lengths,
+                  record_len=rec_len or 0,
+                  tamper_every=1024 if op == "open" and args.mode != "wire" else 0,
+                  interleave=args.interleave, shard=(lo, hi))
     total_len = int(wl.lengths.sum())
     if args.mode == "host":
         return host_mode(args, eng, wl, kind_name, total_len)
@@ -277,7 +290,7 @@ def main():
     traffic, traffic_src = load_traffic(args.config, kernel)
 
     line = {
-        "metric": METRIC if args.config == "B" else
+        "metric": METRIC if args.config in ("B", "E") else
         f"GiB/s device-resident {kind_name} TLS record {op} (config {args.config})",
         "value": round(value, 3),
         "unit": "GiB/s",
@@ -292,9 +305,13 @@ def main():
         "dtype": "u8",
         "data": "synthetic (counter-SplitMix64 plaintexts sealed on device; 1/1024 tampered)"
         if op == "open" else "synthetic (counter-SplitMix64 plaintexts)",
-        "config": {"workload": f"{kind_name} TLS 1.2 record {op}, "
+        "config": {"workload": (f"config {args.config}: " if args.config in ("B", "E") else "") +
+                               f"{kind_name} TLS 1.2 record {op}, "
                                f"{'16 KiB' if rec_len == 16384 else (str(rec_len) + ' B' if rec_len else 'Zipf 64 B-16 KiB')}"
-                               f" records, {per_gpu} records/GPU, device-resident",
+                               f" records, {per_gpu} records/GPU, device-resident" +
+                               (f"; shards 0..{world - 1} of one {shards * per_gpu}-record batch "
+                                f"(seed {seed:#x}, {shards * sessions} sessions)"
+                                if args.config == "E" else ""),
                    "records_per_gpu": per_gpu, "sessions_per_gpu": sessions,
                    "session_order": "interleaved" if args.interleave else "grouped",
                    "gcm_impl": ta.get_gcm_impl() if "gcm" in kind_name else None,

@@ -152,9 +152,12 @@ int tlsgpu_seal_batch(tlsgpu_sessions *t, const tlsgpu_record *d_recs, uint32_t 
  * of chunk k-1 on their own streams overlap the kernels of chunk k) when
  * the records' in_off and out_off ascend with the record index; otherwise it
  * runs the batch as one chunk.  Synchronous: returns when h_out and h_status
- * are final.  Bytes of h_out outside the records' plaintext spans are
- * unspecified afterwards (in place: the headers, explicit nonces and tags are
- * written back unchanged). */
+ * are final, and also on every error — no copy into or out of the caller's
+ * buffers is still running once it has returned.  Bytes of h_out between the
+ * records' plaintext spans (from the first span to the last, or all of
+ * out_bytes when the layout does not ascend) come back as zeros out of place;
+ * in place, the headers, explicit nonces and tags are written back unchanged.
+ * Bytes outside that range are not touched. */
 int tlsgpu_open_host(tlsgpu_sessions *t, const tlsgpu_record *h_recs, uint32_t n,
     const uint8_t *h_in, size_t in_bytes, uint8_t *h_out, size_t out_bytes, int32_t *h_status);
 /* The write direction: plaintext records in host memory (h_in) sealed into
@@ -181,6 +184,64 @@ int tlsgpu_set_plaintext_hooks(tlsgpu_engine *e, tlsgpu_plaintext_hook on_read,
  * 2; copies in and out have a stream each), chunks of about `chunk_bytes`
  * input bytes (default 32 MiB). */
 int tlsgpu_host_pipeline(tlsgpu_engine *e, unsigned streams, size_t chunk_bytes);
+
+/* ---------------------------------------------------------------------------
+ * Multi-GPU batch split (BASELINE configs[4]).  Records are
+ * independent, so a batch splits into contiguous slices of about equal bytes,
+ * one per GPU, with no collective and no xGMI traffic.  A group is one engine
+ * per listed device (the same device may be listed twice: two engines, two
+ * streams) and one host worker thread per engine; session tables are
+ * replicated on every member.  This is what a caller of the per-record
+ * tls1_enc (ssl/t1_enc.c:911,964) that batches — a record layer with
+ * read-ahead over many connections — binds to use every GPU of the node. */
+typedef struct tlsgpu_group tlsgpu_group;
+typedef struct tlsgpu_group_sessions tlsgpu_group_sessions;
+
+/* devices == NULL or n == 0: every visible GPU. */
+int tlsgpu_group_create(const int *devices, uint32_t n, tlsgpu_group **out);
+void tlsgpu_group_destroy(tlsgpu_group *g);
+uint32_t tlsgpu_group_size(const tlsgpu_group *g);
+tlsgpu_engine *tlsgpu_group_engine(tlsgpu_group *g, uint32_t member);
+/* One session table per member, same capacity; install writes every member. */
+int tlsgpu_group_sessions_create(tlsgpu_group *g, uint32_t capacity, tlsgpu_group_sessions **out);
+void tlsgpu_group_sessions_destroy(tlsgpu_group_sessions *gs);
+tlsgpu_sessions *tlsgpu_group_sessions_member(tlsgpu_group_sessions *gs, uint32_t member);
+int tlsgpu_group_sessions_install(tlsgpu_group_sessions *gs, uint32_t first, uint32_t n,
+    const tlsgpu_session_params *params);
+
+/* Byte-balanced contiguous split of n records into `parts` slices: cuts[0] = 0
+ * <= cuts[1] <= ... <= cuts[parts] = n, slice k = records [cuts[k], cuts[k+1]).
+ * Cut k is the first record boundary whose prefix of record lengths (len_type
+ * bits 0-23) reaches k/parts of the total (integer arithmetic; equal lengths
+ * give equal counts).  Host only, no GPU call. */
+int tlsgpu_split_by_bytes(const tlsgpu_record *recs, uint32_t n, uint32_t parts, uint32_t *cuts);
+
+/* Host-resident batch over the group: slice k (tlsgpu_split_by_bytes) runs as
+ * tlsgpu_open_host / tlsgpu_seal_host on member k, all members at once, each
+ * from its own worker thread (its own PCIe link and HBM).  Same buffers,
+ * offsets, statuses and synchronous contract as the single-GPU calls; the
+ * first member error is returned after every member has finished. */
+int tlsgpu_group_open_host(tlsgpu_group_sessions *gs, const tlsgpu_record *h_recs, uint32_t n,
+    const uint8_t *h_in, size_t in_bytes, uint8_t *h_out, size_t out_bytes, int32_t *h_status);
+int tlsgpu_group_seal_host(tlsgpu_group_sessions *gs, const tlsgpu_record *h_recs, uint32_t n,
+    const uint8_t *h_in, size_t in_bytes, uint8_t *h_out, size_t out_bytes, int32_t *h_status);
+
+/* Device-resident batch over the group (per-GPU pools): shards[k] is member
+ * k's slice, already in that member's HBM.  Launched on every member's engine
+ * stream; asynchronous — tlsgpu_group_sync waits for all members. */
+typedef struct tlsgpu_shard {
+	const tlsgpu_record *d_recs;
+	uint32_t n;
+	uint32_t reserved;
+	const uint8_t *d_in;
+	size_t in_bytes;
+	uint8_t *d_out;
+	size_t out_bytes;
+	int32_t *d_status;
+} tlsgpu_shard;
+int tlsgpu_group_open_batch(tlsgpu_group_sessions *gs, const tlsgpu_shard *shards);
+int tlsgpu_group_seal_batch(tlsgpu_group_sessions *gs, const tlsgpu_shard *shards);
+int tlsgpu_group_sync(tlsgpu_group *g);
 
 /* ---------------------------------------------------------------------------
  * Wire-record framing: ssl3_get_record (ssl/s3_pkt.c:279-495)
@@ -322,6 +383,15 @@ int tlsgpu_evp_batch_stats(uint64_t *batches, uint64_t *jobs);
  * not), process-wide since load.  Lets a caller that interposed the library
  * under an unchanged libssl check that every TLS record went through it. */
 int tlsgpu_evp_call_stats(uint64_t *seal_calls, uint64_t *open_calls);
+/* The EVP surface's GPUs.  TLSGPU_DEVICES=a,b,... (a device may repeat: two
+ * engines on one GPU) or TLSGPU_DEVICE=d pin them; by default every visible
+ * GPU.  EVP_AEAD_CTX_init gives new contexts (and EVP_CIPHER contexts their
+ * first key) to these devices in turn; each device has its own engine, call
+ * streams and, with batching on, its own coalescing queue and session pool
+ * (pool_sessions each).  tlsgpu_evp_device_stats(k, ...): device ordinal,
+ * contexts created and EVP calls run on the k-th of them. */
+uint32_t tlsgpu_evp_device_count(void);
+int tlsgpu_evp_device_stats(uint32_t k, int *device, uint64_t *contexts, uint64_t *calls);
 /* GPU programs run by the EVP_aes_{128,256}_gcm EVP_CIPHER objects
  * (include/tlsgpu_evp.h), process-wide since load. */
 int tlsgpu_evp_cipher_stats(uint64_t *programs);

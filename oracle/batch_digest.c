@@ -16,9 +16,15 @@
  * numbers with near-carry starts, counter-SplitMix64 plaintexts, tamper rule),
  * so the GPU test regenerates the same batch on the device and compares.
  *
- * usage: batch_digest AEAD N_RECORDS N_SESSIONS SEED TAMPER_EVERY LEN|@lengths.u32 [interleave]
+ * usage: batch_digest AEAD N_RECORDS N_SESSIONS SEED TAMPER_EVERY LEN|@lengths.u32
+ *                     [interleave] [range=LO:HI]
  *   AEAD: aes-128-gcm | aes-256-gcm | chacha20-poly1305 | chacha20-poly1305-old
  *   interleave: records dealt to sessions round-robin (workload.py session_plan)
+ *   range=LO:HI: digest only records [LO, HI) of the N-record batch — one GPU's
+ *     shard of a batch split across GPUs (config E).  Sessions,
+ *     sequence numbers, plaintexts and the tamper rule stay those of the whole
+ *     batch (global record index), as talos_amd.workload.Workload(shard=) builds
+ *     them on each GPU.
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -64,13 +70,29 @@ hex(const unsigned char *d, char *out)
 int
 main(int argc, char **argv)
 {
-	if (argc != 7 && argc != 8) {
-		fprintf(stderr, "usage: %s AEAD N S SEED TAMPER_EVERY LEN|@file [interleave]\n", argv[0]);
+	if (argc < 7 || argc > 9) {
+		fprintf(stderr, "usage: %s AEAD N S SEED TAMPER_EVERY LEN|@file [interleave] [range=LO:HI]\n",
+		    argv[0]);
 		return 2;
 	}
-	const int interleave = argc == 8 && !strcmp(argv[7], "interleave");
+	int interleave = 0;
+	long lo = 0, hi = -1;
+	for (int a = 7; a < argc; a++) {
+		if (!strcmp(argv[a], "interleave"))
+			interleave = 1;
+		else if (sscanf(argv[a], "range=%ld:%ld", &lo, &hi) != 2) {
+			fprintf(stderr, "bad argument %s\n", argv[a]);
+			return 2;
+		}
+	}
 	const char *name = argv[1];
 	long n = atol(argv[2]), S = atol(argv[3]);
+	if (hi < 0)
+		hi = n;
+	if (lo < 0 || lo > hi || hi > n) {
+		fprintf(stderr, "range %ld:%ld outside [0, %ld]\n", lo, hi, n);
+		return 2;
+	}
 	uint64_t seed = strtoull(argv[4], NULL, 0);
 	long tamper = atol(argv[5]);
 	const EVP_AEAD *aead;
@@ -124,7 +146,7 @@ main(int argc, char **argv)
 	long per = n / S > 0 ? n / S : 1;
 	const int eiv = gcm ? 8 : 0;
 	size_t maxlen = 0;
-	for (long i = 0; i < n; i++)
+	for (long i = lo; i < hi; i++)
 		if (lens[i] > maxlen)
 			maxlen = lens[i];
 	unsigned char *pt = malloc(maxlen + 1), *body = malloc(maxlen + 64), *back = malloc(maxlen + 1);
@@ -132,7 +154,7 @@ main(int argc, char **argv)
 	SHA256_Init(&hs);
 	SHA256_Init(&ho);
 	long bad = 0;
-	for (long r = 0; r < n; r++) {
+	for (long r = lo; r < hi; r++) {
 		long s = interleave ? r % S : (r / per < S - 1 ? r / per : S - 1);
 		uint64_t seq = seq0[s] + (uint64_t)(interleave ? r / S : r % per);
 		size_t len = lens[r];
@@ -187,11 +209,11 @@ main(int argc, char **argv)
 	hex(d1, h1);
 	hex(d2, h2);
 	long long payload = 0;
-	for (long i = 0; i < n; i++)
+	for (long i = lo; i < hi; i++)
 		payload += lens[i];
 	printf("{\"aead\": \"%s\", \"records\": %ld, \"sessions\": %ld, \"seed\": %llu, "
-	    "\"tamper_every\": %ld, \"interleave\": %s, \"payload_bytes\": %lld, \"bad_record_mac\": %ld, "
-	    "\"sealed_sha256\": \"%s\", \"opened_sha256\": \"%s\"}\n", name, n, S,
-	    (unsigned long long)seed, tamper, interleave ? "true" : "false", payload, bad, h1, h2);
+	    "\"tamper_every\": %ld, \"interleave\": %s, \"range\": [%ld, %ld], \"payload_bytes\": %lld, "
+	    "\"bad_record_mac\": %ld, \"sealed_sha256\": \"%s\", \"opened_sha256\": \"%s\"}\n", name, n,
+	    S, (unsigned long long)seed, tamper, interleave ? "true" : "false", lo, hi, payload, bad, h1, h2);
 	return 0;
 }

@@ -147,6 +147,9 @@ def load_library(path: str = LIBPATH) -> C.CDLL:
         "tlsgpu_evp_set_batching": (i32, [C.c_uint, C.c_uint, C.c_uint]),
         "tlsgpu_evp_batch_stats": (i32, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "tlsgpu_evp_call_stats": (i32, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+        "tlsgpu_evp_device_count": (u32, []),
+        "tlsgpu_evp_device_stats": (i32, [u32, C.POINTER(i32), C.POINTER(C.c_uint64),
+                                          C.POINTER(C.c_uint64)]),
         "tlsgpu_malloc": (i32, [vp, C.c_size_t, C.POINTER(vp)]),
         "tlsgpu_free": (i32, [vp, vp]),
         "tlsgpu_host_alloc": (i32, [vp, C.c_size_t, C.POINTER(vp)]),
@@ -160,6 +163,20 @@ def load_library(path: str = LIBPATH) -> C.CDLL:
         "tlsgpu_event_destroy": (i32, [vp, vp]),
         "tlsgpu_event_record": (i32, [vp, vp, vp]),
         "tlsgpu_event_elapsed_ms": (i32, [vp, vp, vp, C.POINTER(C.c_float)]),
+        "tlsgpu_group_create": (i32, [C.POINTER(i32), u32, C.POINTER(vp)]),
+        "tlsgpu_group_destroy": (None, [vp]),
+        "tlsgpu_group_size": (u32, [vp]),
+        "tlsgpu_group_engine": (vp, [vp, u32]),
+        "tlsgpu_group_sessions_create": (i32, [vp, u32, C.POINTER(vp)]),
+        "tlsgpu_group_sessions_destroy": (None, [vp]),
+        "tlsgpu_group_sessions_member": (vp, [vp, u32]),
+        "tlsgpu_group_sessions_install": (i32, [vp, u32, u32, vp]),
+        "tlsgpu_split_by_bytes": (i32, [vp, u32, u32, C.POINTER(u32)]),
+        "tlsgpu_group_open_host": (i32, [vp, vp, u32, vp, C.c_size_t, vp, C.c_size_t, vp]),
+        "tlsgpu_group_seal_host": (i32, [vp, vp, u32, vp, C.c_size_t, vp, C.c_size_t, vp]),
+        "tlsgpu_group_open_batch": (i32, [vp, vp]),
+        "tlsgpu_group_seal_batch": (i32, [vp, vp]),
+        "tlsgpu_group_sync": (i32, [vp]),
         "EVP_aead_aes_128_gcm": (vp, []),
         "EVP_aead_aes_256_gcm": (vp, []),
         "EVP_aead_chacha20_poly1305": (vp, []),
@@ -455,6 +472,89 @@ def seal_batch(table: SessionTable, d_recs: int, n: int, d_in: int, in_bytes: in
                                        d_status, stream), "tlsgpu_seal_batch")
 
 
+# ---------------------------------------------------------------------------
+# Multi-GPU batch split (include/tlsgpu.h tlsgpu_group_*)
+
+SHARD_DTYPE = np.dtype([("d_recs", "<u8"), ("n", "<u4"), ("reserved", "<u4"), ("d_in", "<u8"),
+                        ("in_bytes", "<u8"), ("d_out", "<u8"), ("out_bytes", "<u8"),
+                        ("d_status", "<u8")])
+assert SHARD_DTYPE.itemsize == 56
+
+
+def split_by_bytes(recs: np.ndarray, parts: int) -> list[int]:
+    """Byte-balanced contiguous cuts of a RECORD_DTYPE array (tlsgpu_split_by_bytes,
+    host only)."""
+    recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)
+    cuts = (C.c_uint32 * (parts + 1))()
+    _check(load_library().tlsgpu_split_by_bytes(recs.ctypes.data if len(recs) else None,
+                                                 len(recs), parts, cuts),
+           "tlsgpu_split_by_bytes")
+    return list(cuts)
+
+
+class Group:
+    """One engine per listed device, one worker thread per engine
+    (tlsgpu_group_create; devices=None: every visible GPU)."""
+
+    def __init__(self, devices: list[int] | None = None):
+        self.lib = load_library()
+        h = C.c_void_p()
+        arr = (C.c_int * len(devices))(*devices) if devices else None
+        _check(self.lib.tlsgpu_group_create(arr, len(devices) if devices else 0, C.byref(h)),
+               "tlsgpu_group_create")
+        self.handle = h
+
+    @property
+    def size(self) -> int:
+        return int(self.lib.tlsgpu_group_size(self.handle))
+
+    def sync(self) -> None:
+        _check(self.lib.tlsgpu_group_sync(self.handle), "tlsgpu_group_sync")
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.tlsgpu_group_destroy(self.handle)
+            self.handle = None
+
+
+class GroupSessionTable:
+    """Session table replicated on every group member (tlsgpu_group_sessions_*)."""
+
+    def __init__(self, group: Group, capacity: int):
+        self.group = group
+        self.lib = group.lib
+        h = C.c_void_p()
+        _check(self.lib.tlsgpu_group_sessions_create(group.handle, capacity, C.byref(h)),
+               "tlsgpu_group_sessions_create")
+        self.handle = h
+
+    def install(self, first: int, params: list[SessionParams]) -> None:
+        arr = (_SessionParams * len(params))(*[p.to_c() for p in params])
+        _check(self.lib.tlsgpu_group_sessions_install(self.handle, first, len(params), arr),
+               "tlsgpu_group_sessions_install")
+
+    def open_host(self, h_recs: int, n: int, h_in: int, in_bytes: int, h_out: int,
+                  out_bytes: int, h_status: int) -> None:
+        _check(self.lib.tlsgpu_group_open_host(self.handle, h_recs, n, h_in, in_bytes, h_out,
+                                               out_bytes, h_status), "tlsgpu_group_open_host")
+
+    def seal_host(self, h_recs: int, n: int, h_in: int, in_bytes: int, h_out: int,
+                  out_bytes: int, h_status: int) -> None:
+        _check(self.lib.tlsgpu_group_seal_host(self.handle, h_recs, n, h_in, in_bytes, h_out,
+                                               out_bytes, h_status), "tlsgpu_group_seal_host")
+
+    def batch(self, shards: np.ndarray, seal: bool) -> None:
+        """shards: SHARD_DTYPE, one per member (device pointers on that member)."""
+        shards = np.ascontiguousarray(shards, dtype=SHARD_DTYPE)
+        fn = self.lib.tlsgpu_group_seal_batch if seal else self.lib.tlsgpu_group_open_batch
+        _check(fn(self.handle, shards.ctypes.data), "tlsgpu_group_batch")
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.tlsgpu_group_sessions_destroy(self.handle)
+            self.handle = None
+
+
 class _EvpCtx(C.Structure):
     _fields_ = [("aead", C.c_void_p), ("aead_state", C.c_void_p)]
 
@@ -501,6 +601,18 @@ def evp_set_batching(window_us: int, max_jobs: int = 0, pool_sessions: int = 0) 
     """Turn on / retune the EVP coalescing queue (tlsgpu_evp_set_batching)."""
     _check(load_library().tlsgpu_evp_set_batching(window_us, max_jobs, pool_sessions),
            "tlsgpu_evp_set_batching")
+
+
+def evp_device_stats() -> list[tuple[int, int, int]]:
+    """(device ordinal, contexts, calls) of each GPU the EVP surface uses."""
+    lib = load_library()
+    out = []
+    for k in range(lib.tlsgpu_evp_device_count()):
+        d, c, n = C.c_int(0), C.c_uint64(0), C.c_uint64(0)
+        _check(lib.tlsgpu_evp_device_stats(k, C.byref(d), C.byref(c), C.byref(n)),
+               "tlsgpu_evp_device_stats")
+        out.append((d.value, c.value, n.value))
+    return out
 
 
 def evp_batch_stats() -> tuple[int, int]:

@@ -432,13 +432,15 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
                        : sel_impl == TLSGPU_GCM_AUTO ? TLSGPU_GCM_QUEUE : sel_impl;
   const bool gcm_pre = impl != TLSGPU_GCM_TTABLE && impl != TLSGPU_GCM_SPLIT &&
                        (have[TLSGPU_AES_128_GCM] || have[TLSGPU_AES_256_GCM]);
-  // per-stream scratch: [RecPre x n (queue kernels) | kCtlBytes control words |
+  // per-stream scratch: [RecPre x n (queue kernels) | ctl_bytes control words |
   // checked descriptors x n].  Control words per key size k (0: AES-128, 1:
-  // AES-256): per-workgroup record counters of the per-wave-session kernel at
-  // 1024 (k + 1), selection words (kSelSlots x 64 B) at 4096 + 1024 k.
-  constexpr size_t kCtlBytes = 8192;
+  // AES-256): selection words (kSelSlots x 64 B) at 1024 k, then one uint32
+  // record counter per workgroup of the per-wave-session kernel at
+  // 2048 + k * cnt_bytes, sized from the grid (any CU count).
   static_assert(kSelSlots * kSelWords * 4 <= 1024, "selection words exceed their slot");
-  const size_t pre_bytes = gcm_pre ? sizeof(RecPre) * (size_t)n + kCtlBytes : 0;
+  const size_t cnt_bytes = ((size_t)groups * 4 + 255) & ~(size_t)255;
+  const size_t ctl_bytes = 2048 + 2 * cnt_bytes;
+  const size_t pre_bytes = gcm_pre ? sizeof(RecPre) * (size_t)n + ctl_bytes : 0;
   uint8_t* scratch = nullptr;
   uint8_t* pool_scratch = nullptr;
   if (pre_bytes || bounds) {
@@ -463,7 +465,7 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   if (gcm_pre) {
     pre = reinterpret_cast<RecPre*>(scratch);
     ctl = reinterpret_cast<uint8_t*>(pre + n);
-    if (impl == TLSGPU_GCM_QUEUE) HIPCHK(hipMemsetAsync(ctl, 0, kCtlBytes, s));
+    if (impl == TLSGPU_GCM_QUEUE) HIPCHK(hipMemsetAsync(ctl, 0, ctl_bytes, s));
   }
   for (int rounds : {10, 14}) {
     if (!have[rounds == 10 ? TLSGPU_AES_128_GCM : TLSGPU_AES_256_GCM]) continue;
@@ -471,8 +473,8 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
     // not send the AES-256 pass to the pack variant
     if (ctl && impl == TLSGPU_GCM_QUEUE) {
       const int k = rounds == 10 ? 0 : 1;
-      a.sel = reinterpret_cast<uint32_t*>(ctl + 4096 + 1024 * k);
-      a.wg_next = reinterpret_cast<uint32_t*>(ctl + 1024 * (k + 1));
+      a.sel = reinterpret_cast<uint32_t*>(ctl + 1024 * k);
+      a.wg_next = reinterpret_cast<uint32_t*>(ctl + 2048 + cnt_bytes * k);
     }
     int rc;
     if (impl == TLSGPU_GCM_TTABLE) {
@@ -550,6 +552,13 @@ extern "C" int tlsgpu_host_pipeline(tlsgpu_engine* e, unsigned streams, size_t c
   if (chunk_bytes) e->host.chunk_bytes = chunk_bytes;
   return TLSGPU_OK;
 }
+
+// Test hook (TLSGPU_TEST_HOST_FAIL_CHUNK=k): the host pipeline fails right
+// after queueing chunk k's copy in, with earlier chunks still in flight.
+static const long g_host_fail_chunk = [] {
+  const char* v = getenv("TLSGPU_TEST_HOST_FAIL_CHUNK");
+  return v && *v ? strtol(v, nullptr, 10) : -1L;
+}();
 
 // The host-resident pipeline for both directions (tlsgpu_open_host /
 // tlsgpu_seal_host).  Open: in = record fragments, out = plaintext; seal: in =
@@ -640,43 +649,62 @@ static int host_batch(tlsgpu_sessions* t, bool seal, const tlsgpu_record* h_recs
   }
   hipStream_t s_in = hp.streams[0], s_out = hp.streams[1];
   const size_t ncomp = hp.streams.size() - 2;
-  // all descriptors in one copy ahead of the first chunk, all statuses in one after the last
-  HIPCHK(hipMemcpyAsync(hp.d_recs, h_recs, sizeof(tlsgpu_record) * (size_t)n,
-                        hipMemcpyHostToDevice, s_in));
-  for (size_t k = 0; k < nchunks; k++) {
-    const uint32_t a = cuts[k], b = cuts[k + 1];
-    hipStream_t hs = hp.streams[2 + k % ncomp];
-    hipEvent_t ev_in = hp.events[2 * k], ev_done = hp.events[2 * k + 1];
-    uint64_t ilo = UINT64_MAX, ihi = 0, olo = UINT64_MAX, ohi = 0;
-    for (uint32_t i = a; i < b; i++) {
-      uint64_t l, h;
-      span_in(h_recs[i], &l, &h);
-      ilo = std::min(ilo, l);
-      ihi = std::max(ihi, h);
-      span_out(h_recs[i], &l, &h);
-      olo = std::min(olo, l);
-      ohi = std::max(ohi, h);
+  // Everything below is asynchronous on the pipeline streams; whatever fails,
+  // the streams are drained before returning, so no copy into or out of the
+  // caller's buffers is still running once the call has returned.
+  auto issue = [&]() -> int {
+    // all descriptors in one copy ahead of the first chunk, all statuses in one after the last
+    HIPCHK(hipMemcpyAsync(hp.d_recs, h_recs, sizeof(tlsgpu_record) * (size_t)n,
+                          hipMemcpyHostToDevice, s_in));
+    for (size_t k = 0; k < nchunks; k++) {
+      const uint32_t a = cuts[k], b = cuts[k + 1];
+      hipStream_t hs = hp.streams[2 + k % ncomp];
+      hipEvent_t ev_in = hp.events[2 * k], ev_done = hp.events[2 * k + 1];
+      uint64_t ilo = UINT64_MAX, ihi = 0, olo = UINT64_MAX, ohi = 0;
+      for (uint32_t i = a; i < b; i++) {
+        uint64_t l, h;
+        span_in(h_recs[i], &l, &h);
+        ilo = std::min(ilo, l);
+        ihi = std::max(ihi, h);
+        span_out(h_recs[i], &l, &h);
+        olo = std::min(olo, l);
+        ohi = std::max(ohi, h);
+      }
+      if (!ascending) {  // one chunk: the whole buffers
+        ilo = 0; ihi = in_bytes; olo = 0; ohi = out_bytes;
+      }
+      // copy in (DMA engine 1) -> kernels (compute stream) -> copy out (DMA engine 2)
+      if (ihi > ilo)
+        HIPCHK(hipMemcpyAsync(d_in + ilo, h_in + ilo, ihi - ilo, hipMemcpyHostToDevice, s_in));
+      if ((long)k == g_host_fail_chunk)  // test hook: a failure with earlier chunks in flight
+        return fail(TLSGPU_EHIP, "injected host pipeline failure at chunk %zu", k);
+      HIPCHK(hipEventRecord(ev_in, s_in));
+      HIPCHK(hipStreamWaitEvent(hs, ev_in, 0));
+      // out of place, the HBM mirror is reused across calls: clear the range
+      // copied back, so bytes between the records' output spans come back as
+      // zeros, never as an earlier call's plaintext (in place, the whole range
+      // was just copied in from h_in)
+      if (!in_place && ohi > olo) HIPCHK(hipMemsetAsync(d_out + olo, 0, ohi - olo, hs));
+      const Bounds bd = {in_bytes, out_bytes};
+      const int rc = run_batch(t, hp.d_recs + a, b - a, d_in, d_out, hp.d_status + a, hs, seal,
+                               false, &bd);
+      if (rc != TLSGPU_OK) return rc;
+      HIPCHK(hipEventRecord(ev_done, hs));
+      HIPCHK(hipStreamWaitEvent(s_out, ev_done, 0));
+      if (ohi > olo)
+        HIPCHK(hipMemcpyAsync(h_out + olo, d_out + olo, ohi - olo, hipMemcpyDeviceToHost, s_out));
     }
-    if (!ascending) {  // one chunk: the whole buffers
-      ilo = 0; ihi = in_bytes; olo = 0; ohi = out_bytes;
-    }
-    // copy in (DMA engine 1) -> kernels (compute stream) -> copy out (DMA engine 2)
-    if (ihi > ilo)
-      HIPCHK(hipMemcpyAsync(d_in + ilo, h_in + ilo, ihi - ilo, hipMemcpyHostToDevice, s_in));
-    HIPCHK(hipEventRecord(ev_in, s_in));
-    HIPCHK(hipStreamWaitEvent(hs, ev_in, 0));
-    const Bounds bd = {in_bytes, out_bytes};
-    const int rc = run_batch(t, hp.d_recs + a, b - a, d_in, d_out, hp.d_status + a, hs, seal, false,
-                             &bd);
-    if (rc != TLSGPU_OK) return rc;
-    HIPCHK(hipEventRecord(ev_done, hs));
-    HIPCHK(hipStreamWaitEvent(s_out, ev_done, 0));
-    if (ohi > olo)
-      HIPCHK(hipMemcpyAsync(h_out + olo, d_out + olo, ohi - olo, hipMemcpyDeviceToHost, s_out));
+    HIPCHK(hipMemcpyAsync(h_status, hp.d_status, sizeof(int32_t) * (size_t)n,
+                          hipMemcpyDeviceToHost, s_out));
+    return TLSGPU_OK;
+  };
+  int rc = issue();
+  for (hipStream_t hs : hp.streams) {  // drain on success and on every failure
+    const hipError_t e = hipStreamSynchronize(hs);
+    if (e != hipSuccess && rc == TLSGPU_OK)
+      rc = fail(TLSGPU_EHIP, "host pipeline sync: %s", hipGetErrorString(e));
   }
-  HIPCHK(hipMemcpyAsync(h_status, hp.d_status, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost,
-                        s_out));
-  for (hipStream_t hs : hp.streams) HIPCHK(hipStreamSynchronize(hs));
+  if (rc != TLSGPU_OK) return rc;
   if (!seal && hp.on_read) {  // tls_processing_ssl_read (s3_pkt.c.patch:39-52 placement)
     for (uint32_t i = 0; i < n; i++)
       if (h_status[i] >= 0)
@@ -916,24 +944,71 @@ extern "C" size_t EVP_AEAD_nonce_length(const EVP_AEAD* a) { return a->nonce_len
 extern "C" size_t EVP_AEAD_max_overhead(const EVP_AEAD* a) { return a->overhead; }
 extern "C" size_t EVP_AEAD_max_tag_len(const EVP_AEAD* a) { return a->max_tag_len; }
 
-// Process-wide engine for the per-call path (device from TLSGPU_DEVICE, default 0).
+// Process-wide engines of the per-call path, one per GPU the EVP surface uses:
+// TLSGPU_DEVICE=d pins it to device d; otherwise every visible GPU takes new
+// contexts in turn (EVP_AEAD_CTX_init round-robin), so an unchanged server's
+// connections spread over the node's GPUs — one SSL per thread
+// in the reference's worker model, one context per connection direction.
+constexpr int kMaxEvpDevices = 16;
 static std::mutex g_mu;
-static tlsgpu_engine* g_engine = nullptr;
+static std::vector<int> g_evp_devices;  // device ordinals, filled once
+static tlsgpu_engine* g_engines[kMaxEvpDevices] = {};
+static std::atomic<uint32_t> g_evp_rr{0};
+static std::atomic<uint64_t> g_evp_dev_calls[kMaxEvpDevices];  // per EVP device
+static std::atomic<uint64_t> g_evp_dev_ctx[kMaxEvpDevices];
 
-static tlsgpu_engine* default_engine() {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (!g_engine) {
+static const std::vector<int>& evp_devices_locked() {
+  if (g_evp_devices.empty()) {
     const char* d = getenv("TLSGPU_DEVICE");
-    if (tlsgpu_engine_create(d ? atoi(d) : 0, &g_engine) != TLSGPU_OK) g_engine = nullptr;
+    const char* list = getenv("TLSGPU_DEVICES");  // e.g. "0,1,2,3"; a device may repeat
+    int count = 0;
+    if (list && *list) {
+      for (const char* c = list; *c && g_evp_devices.size() < (size_t)kMaxEvpDevices;) {
+        char* end = nullptr;
+        const long v = strtol(c, &end, 10);
+        if (end == c) break;
+        g_evp_devices.push_back((int)v);
+        c = *end == ',' ? end + 1 : end;
+      }
+    }
+    if (!g_evp_devices.empty()) {
+    } else if (d && *d) {
+      g_evp_devices.push_back(atoi(d));
+    } else if (hipGetDeviceCount(&count) == hipSuccess && count > 0) {
+      for (int i = 0; i < count && i < kMaxEvpDevices; i++) g_evp_devices.push_back(i);
+    } else {
+      g_evp_devices.push_back(0);
+    }
   }
-  return g_engine;
+  return g_evp_devices;
 }
 
+// Engine of the k-th EVP device (created on first use), or nullptr.
+static tlsgpu_engine* evp_engine(size_t k) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  const auto& devs = evp_devices_locked();
+  if (k >= devs.size()) return nullptr;
+  if (!g_engines[k] && tlsgpu_engine_create(devs[k], &g_engines[k]) != TLSGPU_OK)
+    g_engines[k] = nullptr;
+  return g_engines[k];
+}
+
+static size_t evp_device_count() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return evp_devices_locked().size();
+}
+
+// The next device index for a new context (round-robin over the EVP devices).
+static size_t evp_pick() { return g_evp_rr.fetch_add(1) % evp_device_count(); }
+
+struct EvpBatcher;
 struct AeadState {
   tlsgpu_sessions* sess;  // the shared EVP pool table (slot >= 0) or a private one
   int slot;               // session id in sess
   int kind;
   unsigned tag_len;
+  EvpBatcher* batcher;    // the queue of the context's device (pooled contexts)
+  uint32_t evp_dev;       // index of the context's device among the EVP devices
 };
 
 // ---------------------------------------------------------------------------
@@ -1004,9 +1079,13 @@ struct EvpBatcher {
   void dispatch_loop();
   void complete_loop();
   void submit(EvpSlot* s);
+  bool submit_work(EvpSlot* s);
   void release(EvpSlot* s);
 };
-static EvpBatcher* g_batcher = nullptr;
+// one coalescing queue per EVP device (index as evp_engine); g_batcher_on once
+// tlsgpu_evp_set_batching has created them
+static EvpBatcher* g_batchers[kMaxEvpDevices] = {};
+static bool g_batcher_on = false;
 static std::mutex g_batcher_mu;
 
 static inline void futex_wait(std::atomic<uint32_t>* w, uint32_t v) {
@@ -1026,10 +1105,13 @@ static inline void futex_wake_all(std::atomic<uint32_t>* w) {
 // tools/hip_latency); each thread waits on its own event, i.e. on its own
 // work and what was queued before it on that stream.
 constexpr int kCallStreams = 4;
-static hipStream_t g_call_streams[kCallStreams];
-static std::once_flag g_call_streams_once;
+constexpr int kMaxDev = 64;  // device ordinals a thread may stage for
+static hipStream_t g_call_streams[kMaxDev][kCallStreams];
+static std::once_flag g_call_streams_once[kMaxDev];
+static bool g_call_streams_ok[kMaxDev];
 static std::atomic<uint32_t> g_call_thread_seq{0};
 
+// One per (thread, device): buffers, stream and event belong to that device.
 struct Staging {
   int device = -1;
   hipStream_t stream = nullptr;
@@ -1043,15 +1125,18 @@ struct Staging {
     if (done) (void)hipEventDestroy(done);
   }
   bool ensure(int dev, size_t bytes) {
-    if (hipSetDevice(dev) != hipSuccess) return false;
+    if (dev < 0 || dev >= kMaxDev || hipSetDevice(dev) != hipSuccess) return false;
     if (!stream) {
-      bool ok = true;
-      std::call_once(g_call_streams_once, [&] {
-        for (hipStream_t& cs : g_call_streams)
+      std::call_once(g_call_streams_once[dev], [dev] {
+        bool ok = true;
+        for (hipStream_t& cs : g_call_streams[dev])
           ok &= hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) == hipSuccess;
+        g_call_streams_ok[dev] = ok;
       });
-      if (!ok || hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess) return false;
-      stream = g_call_streams[g_call_thread_seq.fetch_add(1) % kCallStreams];
+      if (!g_call_streams_ok[dev] ||
+          hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess)
+        return false;
+      stream = g_call_streams[dev][g_call_thread_seq.fetch_add(1) % kCallStreams];
     }
     device = dev;
     if (cap >= bytes) return true;
@@ -1066,7 +1151,21 @@ struct Staging {
     return true;
   }
 };
-static thread_local Staging t_stage;
+struct StagingSet {
+  Staging* by_dev[kMaxDev] = {};
+  ~StagingSet() {
+    for (Staging* st : by_dev) delete st;
+  }
+};
+static thread_local StagingSet t_stages;
+
+// This thread's staging for device `dev` (nullptr on a bad ordinal / no memory).
+static Staging* stage_for(int dev) {
+  if (dev < 0 || dev >= kMaxDev) return nullptr;
+  Staging*& st = t_stages.by_dev[dev];
+  if (!st) st = new (std::nothrow) Staging();
+  return st;
+}
 
 extern "C" int EVP_AEAD_CTX_init(EVP_AEAD_CTX* ctx, const EVP_AEAD* aead, const unsigned char* key,
                                  size_t key_len, size_t tag_len, ENGINE* impl) {
@@ -1084,19 +1183,24 @@ extern "C" int EVP_AEAD_CTX_init(EVP_AEAD_CTX* ctx, const EVP_AEAD* aead, const 
             gcm ? R_TAG_TOO_LARGE : R_TOO_LARGE);
     return 0;
   }
-  tlsgpu_engine* e = default_engine();
+  const size_t dk = evp_pick();  // this context's GPU (round-robin over the EVP devices)
+  tlsgpu_engine* e = evp_engine(dk);
   if (!e) return 0;
   auto* st = new (std::nothrow) AeadState();
   if (!st) return 0;
   st->kind = aead->kind;
   st->tag_len = (unsigned)tag_len;
   st->slot = -1;
+  st->batcher = nullptr;
+  st->evp_dev = (uint32_t)dk;
   {
     std::lock_guard<std::mutex> lk(g_batcher_mu);
-    if (g_batcher && !g_batcher->free_sessions.empty()) {
-      st->slot = g_batcher->free_sessions.back();
-      g_batcher->free_sessions.pop_back();
-      st->sess = g_batcher->pool;
+    EvpBatcher* b = g_batchers[dk];
+    if (b && !b->free_sessions.empty()) {
+      st->slot = b->free_sessions.back();
+      b->free_sessions.pop_back();
+      st->sess = b->pool;
+      st->batcher = b;
     }
   }
   if (st->slot < 0) {
@@ -1119,13 +1223,14 @@ extern "C" int EVP_AEAD_CTX_init(EVP_AEAD_CTX* ctx, const EVP_AEAD* aead, const 
       tlsgpu_sessions_destroy(st->sess);
     } else {
       std::lock_guard<std::mutex> lk(g_batcher_mu);
-      g_batcher->free_sessions.push_back(st->slot);
+      st->batcher->free_sessions.push_back(st->slot);
     }
     delete st;
     return 0;
   }
   if (st->slot < 0) st->slot = 0;
   else st->slot |= 0x40000000;  // marks a pool slot (see pool_slot)
+  g_evp_dev_ctx[dk].fetch_add(1, std::memory_order_relaxed);
   ctx->aead_state = st;
   return 1;
 }
@@ -1142,7 +1247,7 @@ extern "C" void EVP_AEAD_CTX_cleanup(EVP_AEAD_CTX* ctx) {
     (void)hipMemset(st->sess->d_gcm + slot, 0, sizeof(DevGcmTables));
     if (pooled) {
       std::lock_guard<std::mutex> lk(g_batcher_mu);
-      g_batcher->free_sessions.push_back((int)slot);
+      st->batcher->free_sessions.push_back((int)slot);
     } else {
       tlsgpu_sessions_destroy(st->sess);
     }
@@ -1158,14 +1263,31 @@ static int check_alias(const unsigned char* in, size_t in_len, const unsigned ch
   return 0;
 }
 
-// EVP calls whose cipher work ran on the GPU (tlsgpu_evp_call_stats).
+// EVP calls whose cipher work ran on the GPU (tlsgpu_evp_call_stats), and per
+// EVP device (tlsgpu_evp_device_stats).
 static std::atomic<uint64_t> g_evp_calls[2];  // [0] open, [1] seal
+
 
 extern "C" int tlsgpu_evp_call_stats(uint64_t* seal_calls, uint64_t* open_calls) {
   if (seal_calls) *seal_calls = g_evp_calls[1].load();
   if (open_calls) *open_calls = g_evp_calls[0].load();
   return TLSGPU_OK;
 }
+
+extern "C" int tlsgpu_evp_device_stats(uint32_t k, int* device, uint64_t* contexts,
+                                       uint64_t* calls) {
+  if (k >= evp_device_count()) return fail(TLSGPU_ERANGE, "EVP device %u of %zu", k,
+                                           evp_device_count());
+  if (device) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    *device = evp_devices_locked()[k];
+  }
+  if (contexts) *contexts = g_evp_dev_ctx[k].load();
+  if (calls) *calls = g_evp_dev_calls[k].load();
+  return TLSGPU_OK;
+}
+
+extern "C" uint32_t tlsgpu_evp_device_count(void) { return (uint32_t)evp_device_count(); }
 
 static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, size_t* out_len,
                          size_t max_out_len, const unsigned char* nonce, size_t nonce_len,
@@ -1180,7 +1302,10 @@ static int gpu_call(const AeadState* st, bool seal, unsigned char* out, size_t* 
                     size_t ad_len) {
   int r = gpu_call_impl(st, seal, out, out_len, max_out_len, nonce, nonce_len, in, in_len, ad,
                         ad_len);
-  if (r >= 0) g_evp_calls[seal ? 1 : 0].fetch_add(1, std::memory_order_relaxed);
+  if (r >= 0) {
+    g_evp_calls[seal ? 1 : 0].fetch_add(1, std::memory_order_relaxed);
+    g_evp_dev_calls[st->evp_dev].fetch_add(1, std::memory_order_relaxed);
+  }
   return r;
 }
 
@@ -1195,8 +1320,8 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
                          size_t ad_len) {
   const bool pooled = (st->slot & 0x40000000) != 0;
   if (pooled) {  // pooled context: join the coalescing queue (large jobs run alone)
-    int r = evp_queue_call(g_batcher, st, seal, out, out_len, max_out_len, nonce, nonce_len, in,
-                           in_len, ad, ad_len);
+    int r = evp_queue_call(st->batcher, st, seal, out, out_len, max_out_len, nonce, nonce_len,
+                           in, in_len, ad, ad_len);
     if (r != -2) return r;
   }
   auto al = [](size_t v) { return (v + 15) & ~(size_t)15; };
@@ -1205,10 +1330,11 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
   const size_t o_in = o_ad + al(ad_len), o_status = o_in + al(in_len);
   const size_t o_out = o_status + 16, total = o_out + al(out_bytes + 1);
   tlsgpu_engine* e = st->sess->eng;
-  if (!t_stage.ensure(e->device, total)) return -1;
-  uint8_t* d = t_stage.d_buf;
-  uint8_t* h = t_stage.h_buf;
-  hipStream_t s = t_stage.stream;
+  Staging* stg = stage_for(e->device);
+  if (!stg || !stg->ensure(e->device, total)) return -1;
+  uint8_t* d = stg->d_buf;
+  uint8_t* h = stg->h_buf;
+  hipStream_t s = stg->stream;
   RawJob* j = reinterpret_cast<RawJob*>(h);
   j->in = (uint64_t)(d + o_in);
   j->out = (uint64_t)(d + o_out);
@@ -1241,8 +1367,8 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
   const size_t back = seal ? in_len + st->tag_len : std::min(max_out_len, in_len);
   if (hipMemcpyAsync(h + o_status, d + o_status, o_out - o_status + back, hipMemcpyDeviceToHost,
                      s) != hipSuccess ||
-      hipEventRecord(t_stage.done, s) != hipSuccess ||
-      hipEventSynchronize(t_stage.done) != hipSuccess)
+      hipEventRecord(stg->done, s) != hipSuccess ||
+      hipEventSynchronize(stg->done) != hipSuccess)
     return -1;
   const int32_t status = *reinterpret_cast<const int32_t*>(h + o_status);
   if (status < 0) {  // the kernel's zero-fill of max_out_len bytes (evp_aead.c:137-143)
@@ -1396,9 +1522,10 @@ int run_program(GpuGcm* g, const Step* steps, int nsteps) {
     o_out[i] = total;
     total += al(steps[i].out ? steps[i].len : 0);
   }
-  if (!t_stage.ensure(e->device, total)) return -100;
-  uint8_t* b = t_stage.d_buf;
-  hipStream_t s = t_stage.stream;
+  Staging* stg = stage_for(e->device);
+  if (!stg || !stg->ensure(e->device, total)) return -100;
+  uint8_t* b = stg->d_buf;
+  hipStream_t s = stg->stream;
   std::vector<GcmStreamOp> ops(nsteps);
   for (int i = 0; i < nsteps; i++) {
     ops[i].kind = steps[i].kind;
@@ -1427,7 +1554,8 @@ int run_program(GpuGcm* g, const Step* steps, int nsteps) {
 }
 
 bool gcm_set_key(GpuGcm* g, const unsigned char* key, int key_len) {
-  tlsgpu_engine* e = default_engine();
+  // a cipher context keeps the GPU of its first key (its session table lives there)
+  tlsgpu_engine* e = g->sess ? g->sess->eng : evp_engine(evp_pick());
   if (!e) return false;
   if (!g->sess && tlsgpu_sessions_create(e, 1, &g->sess) != TLSGPU_OK) return false;
   if (!g->d_st) {
@@ -1811,25 +1939,33 @@ void EvpBatcher::dispatch_loop() {
 void EvpBatcher::submit(EvpSlot* s) {
   s->ok = false;
   if (hipSetDevice(pool->eng->device) != hipSuccess) return;
+  if (!submit_work(s)) {
+    // part of the batch may already be queued: let it drain before the slot's
+    // pinned and device buffers go back to the ring for the next batch
+    (void)hipStreamSynchronize(s->stream);
+    return;
+  }
+  s->ok = true;
+}
+
+bool EvpBatcher::submit_work(EvpSlot* s) {
   const uint32_t ns = s->nseal, no = s->nopen;
   int32_t* d_status = reinterpret_cast<int32_t*>(s->d + kEvpStatusOff);
   const RawJob* d_desc = reinterpret_cast<const RawJob*>(s->d);
   if (hipMemcpyAsync(s->d, s->h, kEvpDescBytes + s->in_used, hipMemcpyHostToDevice, s->stream) !=
       hipSuccess)
-    return;
+    return false;
   if (ns && run_batch(pool, d_desc, ns, nullptr, nullptr, d_status, s->stream, true, true,
                      nullptr, s->kinds_seal) != TLSGPU_OK)
-    return;
+    return false;
   if (no && run_batch(pool, d_desc + (kEvpMaxJobs - no), no, nullptr, nullptr,
                       d_status + (kEvpMaxJobs - no), s->stream, false, true, nullptr,
                       s->kinds_open) != TLSGPU_OK)
-    return;
-  if (hipMemcpyAsync(s->h + kEvpStatusOff, s->d + kEvpStatusOff,
-                     kEvpOutOff - kEvpStatusOff + s->out_used, hipMemcpyDeviceToHost,
-                     s->stream) != hipSuccess ||
-      hipEventRecord(s->done, s->stream) != hipSuccess)
-    return;
-  s->ok = true;
+    return false;
+  return hipMemcpyAsync(s->h + kEvpStatusOff, s->d + kEvpStatusOff,
+                        kEvpOutOff - kEvpStatusOff + s->out_used, hipMemcpyDeviceToHost,
+                        s->stream) == hipSuccess &&
+         hipEventRecord(s->done, s->stream) == hipSuccess;
 }
 
 void EvpBatcher::complete_loop() {
@@ -1839,7 +1975,10 @@ void EvpBatcher::complete_loop() {
     EvpSlot* s = submitted.front();
     submitted.pop_front();
     lk.unlock();
-    if (s->ok && hipEventSynchronize(s->done) != hipSuccess) s->ok = false;
+    if (s->ok && hipEventSynchronize(s->done) != hipSuccess) {
+      s->ok = false;
+      (void)hipStreamSynchronize(s->stream);  // nothing of the slot may still run
+    }
     const uint64_t gpu_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(
                                 std::chrono::steady_clock::now() - s->submitted_at)
                                 .count();
@@ -1855,66 +1994,104 @@ void EvpBatcher::complete_loop() {
   }
 }
 
-extern "C" int tlsgpu_evp_set_batching(unsigned window_us, unsigned max_jobs,
-                                       unsigned pool_sessions) {
-  std::lock_guard<std::mutex> lk(g_batcher_mu);
-  if (g_batcher) {  // already running: adjust the window / batch size only
-    std::lock_guard<std::mutex> lk2(g_batcher->mu);
-    g_batcher->window_us = window_us;
-    if (max_jobs) g_batcher->max_jobs = std::min(max_jobs, kEvpMaxJobs);
-    return TLSGPU_OK;
-  }
-  if (window_us == 0 && max_jobs == 0) return TLSGPU_OK;  // stays off
-  tlsgpu_engine* e = default_engine();
-  if (!e) return fail(TLSGPU_EHIP, "no GPU engine for the EVP path");
+// One device's queue: pool table, kEvpSlots staging slots, dispatcher and
+// completer threads (they live as long as the process).  nullptr on failure.
+static EvpBatcher* make_batcher(tlsgpu_engine* e, unsigned window_us, unsigned max_jobs,
+                                uint32_t cap) {
   auto* b = new (std::nothrow) EvpBatcher();
-  if (!b) return fail(TLSGPU_ENOMEM, "batcher");
+  if (!b) {
+    fail(TLSGPU_ENOMEM, "batcher");
+    return nullptr;
+  }
   b->window_us = window_us;
   b->max_jobs = max_jobs ? std::min(max_jobs, kEvpMaxJobs) : kEvpMaxJobs;
-  const uint32_t cap = pool_sessions ? pool_sessions : 1024;
-  int rc = tlsgpu_sessions_create(e, cap, &b->pool);
-  if (rc != TLSGPU_OK) {
+  if (tlsgpu_sessions_create(e, cap, &b->pool) != TLSGPU_OK) {
     delete b;
-    return rc;
+    return nullptr;
   }
-  // the batcher lives as long as the process (its threads never exit)
-  HIPCHK(hipSetDevice(e->device));
+  bool ok = hipSetDevice(e->device) == hipSuccess;
   for (EvpSlot& s : b->slots) {
-    HIPCHK(hipHostMalloc((void**)&s.h, kEvpSlotBytes, hipHostMallocDefault));
-    HIPCHK(hipMalloc((void**)&s.d, kEvpSlotBytes));
-    HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    ok = ok && hipHostMalloc((void**)&s.h, kEvpSlotBytes, hipHostMallocDefault) == hipSuccess &&
+         hipMalloc((void**)&s.d, kEvpSlotBytes) == hipSuccess &&
+         hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) == hipSuccess &&
+         hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
+  }
+  if (!ok) {  // never started: nothing queued on its streams
+    fail(TLSGPU_EHIP, "EVP queue staging on device %d", e->device);
+    for (EvpSlot& s : b->slots) {
+      if (s.h) (void)hipHostFree(s.h);
+      if (s.d) (void)hipFree(s.d);
+    }
+    tlsgpu_sessions_destroy(b->pool);
+    delete b;
+    return nullptr;
   }
   b->building = &b->slots[0];
   for (uint32_t i = kEvpSlots - 1; i >= 1; i--) b->free_ring.push_back(&b->slots[i]);
   for (int i = (int)cap - 1; i >= 0; i--) b->free_sessions.push_back(i);
-  if (getenv("TLSGPU_EVP_STATS")) {
-    atexit([] {
-      EvpBatcher* q = g_batcher;
-      std::lock_guard<std::mutex> lk(q->mu);
-      const double nb = q->batches ? (double)q->batches : 1.0;
-      fprintf(stderr,
-              "{\"evp_queue\": {\"batches\": %llu, \"jobs\": %llu, \"jobs_per_batch\": %.2f, "
-              "\"us_first_to_close\": %.1f, \"us_writers\": %.1f, \"us_submit\": %.1f, "
-              "\"us_submit_to_done\": %.1f}}\n",
-              (unsigned long long)q->batches, (unsigned long long)q->jobs_done,
-              q->jobs_done / nb, q->ns_wait / nb / 1e3, q->ns_writers / nb / 1e3,
-              q->ns_submit / nb / 1e3, q->ns_gpu / nb / 1e3);
-    });
-  }
   b->disp = std::thread([b] { b->dispatch_loop(); });
   b->comp = std::thread([b] { b->complete_loop(); });
-  g_batcher = b;
+  return b;
+}
+
+extern "C" int tlsgpu_evp_set_batching(unsigned window_us, unsigned max_jobs,
+                                       unsigned pool_sessions) {
+  std::lock_guard<std::mutex> lk(g_batcher_mu);
+  if (g_batcher_on) {  // already running: adjust the window / batch size only
+    for (EvpBatcher* b : g_batchers) {
+      if (!b) continue;
+      std::lock_guard<std::mutex> lk2(b->mu);
+      b->window_us = window_us;
+      if (max_jobs) b->max_jobs = std::min(max_jobs, kEvpMaxJobs);
+    }
+    return TLSGPU_OK;
+  }
+  if (window_us == 0 && max_jobs == 0) return TLSGPU_OK;  // stays off
+  // one queue per EVP device: contexts initialised afterwards take a pool slot
+  // on the device evp_pick gives them
+  const uint32_t cap = pool_sessions ? pool_sessions : 1024;
+  const size_t ndev = evp_device_count();
+  for (size_t k = 0; k < ndev; k++) {
+    tlsgpu_engine* e = evp_engine(k);
+    if (!e) return fail(TLSGPU_EHIP, "no GPU engine for EVP device %zu", k);
+    EvpBatcher* b = make_batcher(e, window_us, max_jobs, cap);
+    if (!b) return TLSGPU_EHIP;
+    g_batchers[k] = b;
+  }
+  g_batcher_on = true;
+  if (getenv("TLSGPU_EVP_STATS")) {
+    atexit([] {
+      uint64_t nb = 0, nj = 0, w = 0, wr = 0, sb = 0, gp = 0;
+      for (EvpBatcher* q : g_batchers) {
+        if (!q) continue;
+        std::lock_guard<std::mutex> lk3(q->mu);
+        nb += q->batches;
+        nj += q->jobs_done;
+        w += q->ns_wait;
+        wr += q->ns_writers;
+        sb += q->ns_submit;
+        gp += q->ns_gpu;
+      }
+      const double d = nb ? (double)nb : 1.0;
+      fprintf(stderr,
+              "{\"evp_queue\": {\"devices\": %zu, \"batches\": %llu, \"jobs\": %llu, "
+              "\"jobs_per_batch\": %.2f, \"us_first_to_close\": %.1f, \"us_writers\": %.1f, "
+              "\"us_submit\": %.1f, \"us_submit_to_done\": %.1f}}\n",
+              evp_device_count(), (unsigned long long)nb, (unsigned long long)nj, nj / d,
+              w / d / 1e3, wr / d / 1e3, sb / d / 1e3, gp / d / 1e3);
+    });
+  }
   return TLSGPU_OK;
 }
 
 extern "C" int tlsgpu_evp_batch_stats(uint64_t* batches, uint64_t* jobs) {
   std::lock_guard<std::mutex> lk(g_batcher_mu);
   uint64_t nb = 0, nj = 0;
-  if (g_batcher) {
-    std::lock_guard<std::mutex> lk2(g_batcher->mu);
-    nb = g_batcher->batches;
-    nj = g_batcher->jobs_done;
+  for (EvpBatcher* b : g_batchers) {
+    if (!b) continue;
+    std::lock_guard<std::mutex> lk2(b->mu);
+    nb += b->batches;
+    nj += b->jobs_done;
   }
   if (batches) *batches = nb;
   if (jobs) *jobs = nj;

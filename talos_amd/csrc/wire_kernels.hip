@@ -384,12 +384,15 @@ __global__ __launch_bounds__(256) void wire_seal_frame_kernel(
   const bool ok = active && st.session < n_sessions && sessions[st.session].kind != 0;
   const uint32_t frag = st.max_fragment == 0 || st.max_fragment > kMaxPlain ? kMaxPlain
                                                                            : st.max_fragment;
-  uint32_t nrec = ok ? (st.data_len + frag - 1) / frag : 0;  // len 0: nothing (:593-594)
+  // record count in 64 bits (data_len near 2^32 must not wrap; same arithmetic
+  // as tlsgpu_seal_wire_size), then at most max_records slots per stream
+  const uint64_t nrec64 = ok ? ((uint64_t)st.data_len + frag - 1) / frag : 0;  // len 0: nothing (:593-594)
+  uint32_t nrec = (uint32_t)min(nrec64, (uint64_t)max_records);
   const uint32_t slot0 = wave_reserve(total, nrec);
   if (!active) return;
   const uint32_t first = nrec ? slot0 : 0u;
   if (first >= max_records) nrec = 0;
-  else if (first + nrec > max_records) nrec = max_records - first;
+  else if ((uint64_t)first + nrec > max_records) nrec = max_records - first;
   res.first = first;
   if (nrec) {
     const DevSession& S = sessions[st.session];
@@ -398,7 +401,7 @@ __global__ __launch_bounds__(256) void wire_seal_frame_kernel(
     for (uint32_t k = 0; k < nrec; k++) {
       const uint32_t len = min(frag, st.data_len - k * frag);
       const uint32_t L = len + over;  // the length field (s3_pkt.c:733)
-      if (pos + kHdr + L <= wire_bytes) {
+      if (pos <= wire_bytes && (uint64_t)kHdr + L <= wire_bytes - pos) {  // no wrap
         uint8_t* h = wire + pos;
         h[0] = st.type;
         h[1] = (uint8_t)(st.version >> 8);

@@ -26,13 +26,15 @@ def device_for(local_rank: int, visible: int) -> int:
 
 def shard_by_bytes(lengths: np.ndarray, world: int, rank: int) -> tuple[int, int]:
     """[lo, hi) of the records rank `rank` owns: contiguous slices with balanced
-    payload bytes (equal record counts when lengths are equal)."""
+    payload bytes (equal record counts when lengths are equal).  Cut k is the
+    first record boundary whose byte prefix reaches k/world of the total, in
+    exact integer arithmetic — the rule of the C ABI's tlsgpu_split_by_bytes."""
     n = len(lengths)
     if world <= 1:
         return 0, n
     csum = np.concatenate([[0], np.cumsum(lengths, dtype=np.int64)])
     total = int(csum[-1])
-    cuts = [0] + [int(np.searchsorted(csum, total * k / world, side="left")) for k in
+    cuts = [0] + [int(np.searchsorted(csum * world, total * k, side="left")) for k in
                   range(1, world)] + [n]
     return cuts[rank], cuts[rank + 1]
 

@@ -8,7 +8,13 @@ test can regenerate any record independently:
   start sequence number = fill(seed ^ SEQ_TAG, s) (8 bytes, little endian);
 * record r belongs to session r // (R / S) (records grouped by connection, as a
   server's read-ahead batches are), seq = start_seq + r % (R / S);
-* plaintext of record r = fill(seed, index0 + r, length_r).
+* plaintext of record r = fill(seed, r, length_r).
+
+A batch split across GPUs (config E) is ONE such batch: the
+GPU of shard [lo, hi) builds records lo..hi-1 with their global index (session,
+sequence number, plaintext and tamper rule all keyed by it) and installs only
+the sessions those records use, so a shard's outputs equal that slice of the
+whole batch's — oracle/batch_digest range=LO:HI pins each slice.
 
 Ciphertexts for the decrypt configurations are produced on the device by the
 validated sealer (tlsgpu_seal_batch), as SURVEY.md §8d prescribes.
@@ -90,15 +96,25 @@ class Workload:
     """
 
     def __init__(self, engine, kind: int, n_records: int, n_sessions: int, seed: int,
-                 lengths=None, record_len: int = 16384, index0: int = 0, tamper_every: int = 0,
-                 interleave: bool = False):
+                 lengths=None, record_len: int = 16384, tamper_every: int = 0,
+                 interleave: bool = False, shard: tuple[int, int] | None = None):
+        """n_records / n_sessions describe the whole batch; `shard` = (lo, hi)
+        keeps records [lo, hi) of it on this engine (default: all).  `lengths`
+        are the kept records' lengths."""
+        lo, hi = shard if shard is not None else (0, n_records)
+        if not 0 <= lo <= hi <= n_records:
+            raise ValueError(f"shard {lo}:{hi} outside the {n_records}-record batch")
         self.engine = engine
         self.kind = kind
-        self.n = n_records
+        self.lo = lo
+        self.n = hi - lo
         self.seed = seed
-        self.S = n_sessions
-        self.lengths = (np.full(n_records, record_len, dtype=np.int64) if lengths is None
+        self.lengths = (np.full(self.n, record_len, dtype=np.int64) if lengths is None
                         else np.asarray(lengths, dtype=np.int64))
+        if len(self.lengths) != self.n:
+            raise ValueError("lengths must cover the shard's records")
+        total = n_records
+        n_records = hi - lo   # from here on: this shard's records
         eiv = EXPLICIT_NONCE_LEN[kind]
         pt_slot = (self.lengths + 15) // 16 * 16
         body_slot = (self.lengths + eiv + TAG_LEN + 15 + 16) // 16 * 16
@@ -108,10 +124,17 @@ class Workload:
         self.pt_bytes = int(pt_slot.sum())
         self.body_bytes = int(body_slot.sum()) + 16
 
-        # sessions, record -> session map and sequence numbers
-        self.params, self.start_seq, self.session, self.seq = session_plan(
-            kind, n_records, n_sessions, seed, interleave)
-        self.table = SessionTable(engine, n_sessions)
+        # sessions, record -> session map and sequence numbers of the whole
+        # batch, then this shard's slice; the device table holds the sessions
+        # [s0, s0 + S) the slice uses (local id = global id - s0)
+        params, start_seq, session, seq = session_plan(kind, total, n_sessions, seed, interleave)
+        session, self.seq = session[lo:hi], seq[lo:hi]
+        self.s0 = int(session.min()) if self.n else 0
+        s1 = int(session.max()) + 1 if self.n else 1
+        self.S = s1 - self.s0
+        self.params, self.start_seq = params[self.s0:s1], start_seq[self.s0:s1]
+        self.session = (session - self.s0).astype(np.uint32)
+        self.table = SessionTable(engine, self.S)
         self.table.install(0, self.params)
         self.rtype = np.full(n_records, 23, dtype=np.uint32)
 
@@ -120,16 +143,16 @@ class Workload:
         self.d_body = DeviceBuffer(engine, self.body_bytes)
         self.d_out = DeviceBuffer(engine, self.pt_bytes)
         self.d_status = DeviceBuffer(engine, 4 * n_records)
-        if lengths is None:  # record i's plaintext = fill(seed, index0 + i) at pt_off[i]
+        if lengths is None:  # record i's plaintext = fill(seed, lo + i) at pt_off[i]
             engine.fill_synthetic(self.d_pt.ptr, (record_len + 15) // 16 * 16, record_len,
-                                  n_records, seed, index0)
+                                  n_records, seed, lo)
         else:  # variable spans: one launch over (offset, length) arrays
             d_offs = DeviceBuffer(engine, 8 * n_records)
             d_lens = DeviceBuffer(engine, 4 * n_records)
             d_offs.upload(self.pt_off.astype(np.uint64).view(np.uint8))
             d_lens.upload(self.lengths.astype(np.uint32).view(np.uint8))
             engine.fill_synthetic_spans(self.d_pt.ptr, d_offs.ptr, d_lens.ptr, n_records, seed,
-                                        index0)
+                                        lo)
             engine.sync()
             d_offs.free()
             d_lens.free()
@@ -163,14 +186,17 @@ class Workload:
 
     def apply_tamper(self, every: int) -> None:
         """Flip one ciphertext/tag bit of records every//2, every//2 + every, ...
-        (SURVEY.md §8d tamper subset): bit i%8 of body byte eiv + (i*7919) %
-        (len + 16).  oracle/batch_digest.c applies the same rule."""
+        of the whole batch (SURVEY.md §8d tamper subset): bit g%8 of body byte
+        eiv + (g*7919) % (len + 16) for global record index g.
+        oracle/batch_digest.c applies the same rule."""
         eiv = EXPLICIT_NONCE_LEN[self.kind]
-        idx = np.arange(every // 2, self.n, every)
+        first = (every // 2 - self.lo) % every
+        idx = np.arange(first, self.n, every)
         for i in idx:
-            pos = int(self.body_off[i]) + eiv + int((i * 7919) % (self.lengths[i] + TAG_LEN))
+            g = self.lo + int(i)
+            pos = int(self.body_off[i]) + eiv + int((g * 7919) % (self.lengths[i] + TAG_LEN))
             b = self.d_body.download(1, pos)
-            b[0] ^= 1 << int(i % 8)
+            b[0] ^= 1 << (g % 8)
             self.d_body.upload(b, pos)
         self.tampered[idx] = True
 

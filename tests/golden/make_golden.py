@@ -152,10 +152,19 @@ BATCHES = {
     "D_small": ("aes-256-gcm", 256, 16, 0x5EED0003, 32, "zipf"),
     "old_small": ("chacha20-poly1305-old", 128, 8, 0x5EED0005, 16, 1000),
     "inter_small": ("aes-256-gcm", 200, 7, 0x5EED0006, 16, "zipf", "interleave"),
+    # a shard of a split batch at CPU-restatement size (config E's rules)
+    "E_shard_small": ("aes-128-gcm", 512, 64, 0x5EED0004, 16, 1024, "range=256:384"),
 }
+# config E: ONE batch of 524,288 x 16 KiB records, 8,192 sessions
+# of 64 records, split across 8 GPUs; shard r = records [65536 r, 65536 (r + 1))
+E_RECORDS, E_SESSIONS, E_SHARDS = 524288, 8192, 8
+for _r in range(E_SHARDS):
+    _lo = _r * (E_RECORDS // E_SHARDS)
+    BATCHES[f"E_shard{_r}"] = ("aes-128-gcm", E_RECORDS, E_SESSIONS, 0x5EED0004, 1024, 16384,
+                               f"range={_lo}:{_lo + E_RECORDS // E_SHARDS}")
 
 
-def make_batch_digests():
+def make_batch_digests(only=None):
     import subprocess
     import tempfile
 
@@ -165,6 +174,8 @@ def make_batch_digests():
     exe = os.path.join(ROOT, "oracle", "_ref", "batch_digest")
     out = {}
     for name, (aead, n, S, seed, tamper, ln, *order) in BATCHES.items():
+        if only and name not in only:
+            continue
         with tempfile.NamedTemporaryFile(suffix=".u32") as f:
             if ln == "zipf":
                 f.write(zipf_lengths(n, seed).astype(np.uint32).tobytes())
@@ -182,6 +193,13 @@ def make_batch_digests():
 
 
 def main():
+    if len(sys.argv) > 2 and sys.argv[1] == "--digests":
+        # recompute only the named batch digests and merge them into the fixture
+        path = os.path.join(HERE, "batch_digests.json")
+        d = json.load(open(path))
+        d["batches"].update(make_batch_digests(set(sys.argv[2:])))
+        json.dump(d, open(path, "w"), indent=1)
+        return
     os.makedirs(HERE, exist_ok=True)
     shutil.copyfile(os.path.join(REFT, "aeadtests.txt"), os.path.join(HERE, "aeadtests.txt"))
     json.dump(parse_gcm128(os.path.join(REFT, "gcm128test.c")),

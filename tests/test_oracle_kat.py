@@ -124,6 +124,7 @@ def test_batch_digests_oracle(oracle, name):
     d = _batches()[name]
     kind = po.KIND_BY_NAME[d["aead"]]
     n, S, seed, te = d["records"], d["sessions"], d["seed"], d["tamper_every"]
+    lo, hi = d.get("range", (0, n))     # a shard of a split batch: global record indices
     lengths = (zipf_lengths(n, seed) if d["lengths"] == "zipf"
                else np.full(n, d["lengths"], dtype=np.int64))
     params, _, session, seq = session_plan(kind, n, S, seed, d.get("interleave", False))
@@ -131,7 +132,7 @@ def test_batch_digests_oracle(oracle, name):
     oracle.lib.oracle_fill_bytes.argtypes = [C.c_uint64, C.c_uint64, C.c_void_p, C.c_size_t]
     eiv = 8 if kind in (po.AES_128_GCM, po.AES_256_GCM) else 0
     hs, ho, bad = hashlib.sha256(), hashlib.sha256(), 0
-    for r in range(n):
+    for r in range(lo, hi):
         ln = int(lengths[r])
         buf = (C.c_ubyte * max(ln, 1))()
         oracle.lib.oracle_fill_bytes(seed, r, buf, ln)
