@@ -166,20 +166,43 @@ int tlsgpu_open_host(tlsgpu_sessions *t, const tlsgpu_record *h_recs, uint32_t n
 int tlsgpu_seal_host(tlsgpu_sessions *t, const tlsgpu_record *h_recs, uint32_t n,
     const uint8_t *h_in, size_t in_bytes, uint8_t *h_out, size_t out_bytes, int32_t *h_status);
 
-/* TaLoS plaintext-processing hooks (src/talos/enclaveshim/tls_processing_interface.h:
- * tls_processing_ssl_read / _ssl_write, called from ssl3_read_bytes after
- * decryption and from do_ssl3_write before encryption, s3_pkt.c.patch:39-52,
- * 19-33).  The host-resident calls run them on the host plaintext of each
- * record: on_read after tlsgpu_open_host has the batch in h_out (records with
- * status >= 0, in record order), on_write before tlsgpu_seal_host copies the
- * batch to the device (in record order; the hook may rewrite the bytes in
- * place, not their length).  `session` and `seq` stand in for the SSL*.
- * NULL clears a hook.  Device-resident callers run their own hook after
- * their D2H of a delivered record. */
-typedef void (*tlsgpu_plaintext_hook)(void *user, uint32_t session, uint64_t seq, uint8_t *data,
-    uint32_t len);
-int tlsgpu_set_plaintext_hooks(tlsgpu_engine *e, tlsgpu_plaintext_hook on_read,
-    tlsgpu_plaintext_hook on_write, void *user);
+/* TaLoS plaintext-processing hooks.  libtlsgpu implements TaLoS's own
+ * interface (include/tlsgpu_talos.h: tls_processing_register_*_cb with the
+ * reference signatures, tls_processing_interface.h:23-27), so a TaLoS module
+ * registers against the engine unchanged.  The registered read / write
+ * callbacks run on host plaintext, with the SSL* the caller associated with
+ * the record's session (NULL if none):
+ *   write  tlsgpu_seal_host: each record before the batch is copied to the
+ *          device, in record order (do_ssl3_write's call, s3_pkt.c.patch:19-33);
+ *          the module may rewrite the bytes in place and shorten the record;
+ *          tlsgpu_hook_write_streams: each fragment of host application data
+ *          that tlsgpu_seal_wire will seal;
+ *   read   tlsgpu_open_host and tlsgpu_deliver_host (the batch and wire paths'
+ *          host delivery): each delivered record's plaintext once it is in
+ *          host memory, in record order (ssl3_read_bytes' call,
+ *          s3_pkt.c.patch:39-52); a module that shortens *len shortens the
+ *          delivered status.
+ * tlsgpu_group_* calls run them per member, in record order within each
+ * member's slice. */
+int tlsgpu_sessions_set_owner(tlsgpu_sessions *t, uint32_t first, uint32_t n,
+    const void *const *owners);
+/* Host delivery of a device-resident open (tlsgpu_open_batch, or
+ * tlsgpu_open_wire with d_out = d_wire): copies the n descriptors' statuses to
+ * h_status and the delivered records' output range [first out_off, last
+ * out_off + status) of d_out to the same offsets of h_out (out_bytes = size of
+ * d_out / h_out), then runs the read hook on each delivered record.
+ * Synchronous on `stream` (NULL = engine stream; order it after the open). */
+int tlsgpu_deliver_host(tlsgpu_sessions *t, const tlsgpu_record *d_recs, const int32_t *d_status,
+    uint32_t n, const uint8_t *d_out, size_t out_bytes, uint8_t *h_out, int32_t *h_status,
+    void *stream);
+/* Write hook over host application data before the caller uploads it for
+ * tlsgpu_seal_wire: every fragment of every stream (h_streams: host copy of
+ * the write streams, offsets into h_data), in place, lengths unchanged. */
+int tlsgpu_hook_write_streams(tlsgpu_sessions *t, const struct tlsgpu_write_stream *h_streams,
+    uint32_t n_streams, uint8_t *h_data, size_t data_bytes);
+/* read / write hook invocations since load (from the patched record layer
+ * and the engine's paths alike). */
+int tlsgpu_talos_hook_stats(uint64_t *read_calls, uint64_t *write_calls);
 /* Pipeline shape of tlsgpu_open_host: `streams` compute streams (1..8, default
  * 2; copies in and out have a stream each), chunks of about `chunk_bytes`
  * input bytes (default 32 MiB). */

@@ -20,9 +20,19 @@
  * exchange must have sealed and opened, so a test can check that every record
  * ran on the GPU.
  *
+ * -m (TaLoS module check, for the TaLoS-patched build _ref/ssl_loopback_talos):
+ * before any SSL object exists the harness calls ecall_tls_processing_module_init
+ * (src/talos/enclaveshim/tls_processing_interface.c:60, what TaLoS's
+ * initialize_library does, enclaveshim_ecalls.c:440), so the linked module
+ * (oracle/talos_module.c) registers its callbacks; afterwards it checks that the
+ * module saw, per SSL object and direction, the plaintext of every application
+ * record in order (hooks of s3_pkt.c.patch:19-33 and :39-52) and one
+ * new/free connection call per SSL object (ssl_lib.c.patch).
+ *
  * usage: ssl_loopback -p server.pem [-c cipher] [-r record_bytes]
- *                     [-n records_per_direction] [-t threads]
- * prints one JSON line; exit status 0 only if every byte round-tripped.
+ *                     [-n records_per_direction] [-t threads] [-m]
+ * prints one JSON line; exit status 0 only if every byte round-tripped (and,
+ * with -m, the module check passed).
  */
 #define _GNU_SOURCE	/* RTLD_DEFAULT */
 #include <dlfcn.h>
@@ -47,6 +57,7 @@ static const char *cipher = "ECDHE-RSA-AES128-GCM-SHA256";
 static long rec_bytes = 1024;
 static long nrec = 4096;
 static int nthreads = 1;
+static int module_check = 0;
 
 /* LibreSSL 2.4.1 takes OpenSSL-1.0-style locking callbacks from the app. */
 static pthread_mutex_t *locks;
@@ -94,6 +105,7 @@ fill(unsigned char *p, long n, uint64_t key)
 struct targ {
 	int id;
 	int ok;
+	SSL *c, *s;	/* freed by main after the module check (no address reuse) */
 	char err[200];
 	char negotiated[64];
 	double t_data;
@@ -101,6 +113,87 @@ struct targ {
 };
 
 static SSL_CTX *s_ctx, *c_ctx;
+
+/* ---- TaLoS module check (-m) ---- */
+struct talos_log_entry {
+	const void *ssl;
+	uint32_t dir, len;
+	uint64_t fnv;
+};
+
+static uint64_t
+fnv1a(const unsigned char *p, long n)
+{
+	uint64_t h = 0xcbf29ce484222325ull;
+	for (long i = 0; i < n; i++)
+		h = (h ^ p[i]) * 0x100000001b3ull;
+	return h;
+}
+
+/* The last nrec chunks the module logged for (ssl, dir) must be the nrec
+ * payloads of that direction, in order (earlier chunks are handshake records). */
+static int
+check_stream(const struct talos_log_entry *e, uint64_t n, const void *ssl, uint32_t dir,
+    int id, int echo, unsigned char *buf, long *seen)
+{
+	long cnt = 0;
+	for (uint64_t i = 0; i < n; i++)
+		cnt += e[i].ssl == ssl && e[i].dir == dir;
+	*seen += cnt;
+	if (cnt < nrec)
+		return 0;
+	long skip = cnt - nrec, k = 0;
+	for (uint64_t i = 0; i < n; i++) {
+		if (e[i].ssl != ssl || e[i].dir != dir || skip-- > 0)
+			continue;
+		fill(buf, rec_bytes, ((uint64_t)id << 40) ^ ((uint64_t)k << 1) ^ (uint64_t)echo);
+		if (e[i].len != (uint32_t)rec_bytes || e[i].fnv != fnv1a(buf, rec_bytes))
+			return 0;
+		k++;
+	}
+	return k == nrec;
+}
+
+static int
+check_module(struct targ *ta, char *out, size_t outlen)
+{
+	const struct talos_log_entry *(*get)(uint64_t *, uint64_t *, uint64_t *) =
+	    (const struct talos_log_entry *(*)(uint64_t *, uint64_t *, uint64_t *))dlsym(
+	    RTLD_DEFAULT, "talos_module_log");
+	int (*hooks)(uint64_t *, uint64_t *) =
+	    (int (*)(uint64_t *, uint64_t *))dlsym(RTLD_DEFAULT, "tlsgpu_talos_hook_stats");
+	uint64_t hr = 0, hw = 0;
+	if (hooks)
+		hooks(&hr, &hw);
+	if (!get || rec_bytes > MAX_PLAIN) {
+		snprintf(out, outlen, "{\"ok\": false, \"why\": \"%s\"}",
+		    get ? "record_bytes > 16384" : "no module linked");
+		return 0;
+	}
+	uint64_t n, nnew, nfree;
+	const struct talos_log_entry *e = get(&n, &nnew, &nfree);
+	unsigned char *buf = malloc(rec_bytes);
+	long seen = 0, streams_ok = 0;
+	for (int t = 0; t < nthreads; t++) {
+		/* client writes k, server reads it; server echoes k ^ 1, client reads it */
+		streams_ok += check_stream(e, n, ta[t].c, 1, t, 0, buf, &seen);
+		streams_ok += check_stream(e, n, ta[t].s, 0, t, 0, buf, &seen);
+		streams_ok += check_stream(e, n, ta[t].s, 1, t, 1, buf, &seen);
+		streams_ok += check_stream(e, n, ta[t].c, 0, t, 1, buf, &seen);
+	}
+	free(buf);
+	const int ok = streams_ok == 4L * nthreads && nnew == 2ull * nthreads;
+	snprintf(out, outlen,
+	    "{\"ok\": %s, \"chunks_logged\": %llu, \"streams_ok\": %ld, \"streams\": %d, "
+	    "\"app_records_checked\": %ld, \"new_connections\": %llu, \"freed_before_check\": %llu, "
+	    "\"tlsgpu_hook_read_calls\": %llu, \"tlsgpu_hook_write_calls\": %llu, "
+	    "\"tlsgpu_hooks\": %s}",
+	    ok ? "true" : "false", (unsigned long long)n, streams_ok, 4 * nthreads,
+	    4L * nthreads * nrec, (unsigned long long)nnew, (unsigned long long)nfree,
+	    (unsigned long long)hr, (unsigned long long)hw, hooks ? "true" : "false");
+	(void)seen;
+	return ok;
+}
 
 static int
 want_io(SSL *s, int rc)
@@ -197,10 +290,8 @@ run(void *arg)
 	t->bytes = 2LL * nrec * rec_bytes;
 	t->ok = 1;
 out:
-	if (c)
-		SSL_free(c);
-	if (s)
-		SSL_free(s);
+	t->c = c;
+	t->s = s;
 	free(buf);
 	free(rbuf);
 	return NULL;
@@ -210,8 +301,9 @@ int
 main(int argc, char **argv)
 {
 	int o;
-	while ((o = getopt(argc, argv, "p:c:r:n:t:")) != -1) {
+	while ((o = getopt(argc, argv, "p:c:r:n:t:m")) != -1) {
 		switch (o) {
+		case 'm': module_check = 1; break;
 		case 'p': pem = optarg; break;
 		case 'c': cipher = optarg; break;
 		case 'r': rec_bytes = atol(optarg); break;
@@ -250,6 +342,15 @@ main(int argc, char **argv)
 	EC_KEY_free(ecdh);
 	SSL_CTX_set_verify(c_ctx, SSL_VERIFY_NONE, NULL);
 
+	if (module_check) {	/* TaLoS initialize_library -> module init */
+		void (*init)(void) = (void (*)(void))dlsym(RTLD_DEFAULT,
+		    "ecall_tls_processing_module_init");
+		if (!init) {
+			fprintf(stderr, "no TaLoS tls_processing interface in this process\n");
+			return 1;
+		}
+		init();
+	}
 	/* libtlsgpu's EVP call counters, present only when it is interposed */
 	int (*stats)(uint64_t *, uint64_t *) =
 	    (int (*)(uint64_t *, uint64_t *))dlsym(RTLD_DEFAULT, "tlsgpu_evp_call_stats");
@@ -284,6 +385,15 @@ main(int argc, char **argv)
 	}
 	if (!ok)
 		ERR_print_errors_fp(stderr);
+	char mod[400] = "null";
+	if (module_check)
+		ok &= check_module(ta, mod, sizeof(mod));
+	for (int i = 0; i < nthreads; i++) {
+		if (ta[i].c)
+			SSL_free(ta[i].c);
+		if (ta[i].s)
+			SSL_free(ta[i].s);
+	}
 	/* records each side must seal (and the peer open): its Finished plus
 	 * nrec writes of ceil(rec_bytes / max_send_fragment) records each
 	 * (ssl3_write_bytes splits at 16 KiB, s3_pkt.c:531-536) */
@@ -293,11 +403,11 @@ main(int argc, char **argv)
 	    "\"writes_per_direction\": %ld, \"payload_bytes\": %lld, \"data_seconds_max\": %.6f, "
 	    "\"wall_seconds\": %.6f, \"gib_per_s\": %.4f, \"records_sealed_expected\": %lld, "
 	    "\"records_opened_expected\": %lld, \"tlsgpu_interposed\": %s, "
-	    "\"tlsgpu_seal_calls\": %llu, \"tlsgpu_open_calls\": %llu}\n",
+	    "\"tlsgpu_seal_calls\": %llu, \"tlsgpu_open_calls\": %llu, \"talos_module\": %s}\n",
 	    ok ? "true" : "false", ta[0].negotiated, nthreads, rec_bytes, nrec, bytes, tmax, wall,
 	    tmax > 0 ? bytes / tmax / (1024.0 * 1024 * 1024) : 0.0, expect, expect,
 	    stats ? "true" : "false", (unsigned long long)(seal1 - seal0),
-	    (unsigned long long)(open1 - open0));
+	    (unsigned long long)(open1 - open0), mod);
 	SSL_CTX_free(s_ctx);
 	SSL_CTX_free(c_ctx);
 	return ok ? 0 : 1;

@@ -142,7 +142,14 @@ def load_library(path: str = LIBPATH) -> C.CDLL:
         "tlsgpu_seal_wire_size": (u64, [i32, u32, u32, u32]),
         "tlsgpu_host_pipeline": (i32, [vp, C.c_uint, C.c_size_t]),
         "tlsgpu_seal_host": (i32, [vp, vp, u32, vp, C.c_size_t, vp, C.c_size_t, vp]),
-        "tlsgpu_set_plaintext_hooks": (i32, [vp, vp, vp, vp]),
+        "tlsgpu_sessions_set_owner": (i32, [vp, u32, u32, vp]),
+        "tlsgpu_deliver_host": (i32, [vp, vp, vp, u32, vp, C.c_size_t, vp, vp, vp]),
+        "tlsgpu_hook_write_streams": (i32, [vp, vp, u32, vp, C.c_size_t]),
+        "tlsgpu_talos_hook_stats": (i32, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+        "tls_processing_register_ssl_read_processing_cb": (None, [vp]),
+        "tls_processing_register_ssl_write_processing_cb": (None, [vp]),
+        "tls_processing_register_new_connection_cb": (None, [vp]),
+        "tls_processing_register_free_connection_cb": (None, [vp]),
         "tlsgpu_evp_cipher_stats": (i32, [C.POINTER(C.c_uint64)]),
         "tlsgpu_evp_set_batching": (i32, [C.c_uint, C.c_uint, C.c_uint]),
         "tlsgpu_evp_batch_stats": (i32, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
@@ -443,20 +450,48 @@ def seal_host(table: SessionTable, h_recs: int, n: int, h_in: int, in_bytes: int
                                       h_status), "tlsgpu_seal_host")
 
 
-PLAINTEXT_HOOK = C.CFUNCTYPE(None, C.c_void_p, C.c_uint32, C.c_uint64, C.POINTER(C.c_uint8),
-                             C.c_uint32)
+# TaLoS module callbacks: void (*)(const SSL*, char*, unsigned int*)
+TALOS_RW_CB = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(C.c_uint8), C.POINTER(C.c_uint))
 
 
-def set_plaintext_hooks(engine: "Engine", on_read=None, on_write=None) -> tuple:
-    """Install TaLoS-style plaintext hooks (tlsgpu_set_plaintext_hooks); Python
-    callables f(session, seq, data_ptr, length).  Returns the ctypes callbacks,
-    which the caller keeps alive while they are installed."""
-    cbs = tuple(PLAINTEXT_HOOK((lambda f: lambda u, s, q, d, n: f(s, q, d, n))(f)) if f else None
-                for f in (on_read, on_write))
-    _check(engine.lib.tlsgpu_set_plaintext_hooks(
-        engine.handle, C.cast(cbs[0], C.c_void_p) if cbs[0] else None,
-        C.cast(cbs[1], C.c_void_p) if cbs[1] else None, None), "tlsgpu_set_plaintext_hooks")
+def talos_register(on_read=None, on_write=None) -> tuple:
+    """Register TaLoS read / write processing callbacks through the reference
+    interface libtlsgpu.so exports (tls_processing_register_ssl_*_processing_cb,
+    include/tlsgpu_talos.h).  Python callables f(ssl, data_ptr, len_ptr); None
+    clears.  Returns the ctypes callbacks, which the caller keeps alive."""
+    lib = load_library()
+    cbs = tuple(TALOS_RW_CB(f) if f else None for f in (on_read, on_write))
+    lib.tls_processing_register_ssl_read_processing_cb(C.cast(cbs[0], C.c_void_p) if cbs[0] else None)
+    lib.tls_processing_register_ssl_write_processing_cb(C.cast(cbs[1], C.c_void_p) if cbs[1] else None)
     return cbs
+
+
+def set_session_owners(table: "SessionTable", first: int, owners: list[int]) -> None:
+    """Associate an SSL* (any pointer-sized value) with sessions first.. for the
+    TaLoS hooks (tlsgpu_sessions_set_owner)."""
+    arr = (C.c_void_p * len(owners))(*owners)
+    _check(table.lib.tlsgpu_sessions_set_owner(table.handle, first, len(owners), arr),
+           "tlsgpu_sessions_set_owner")
+
+
+def talos_hook_stats() -> tuple[int, int]:
+    r, w = C.c_uint64(0), C.c_uint64(0)
+    _check(load_library().tlsgpu_talos_hook_stats(C.byref(r), C.byref(w)), "tlsgpu_talos_hook_stats")
+    return r.value, w.value
+
+
+def deliver_host(table: "SessionTable", d_recs: int, d_status: int, n: int, d_out: int,
+                 out_bytes: int, h_out: int, h_status: int, stream: int | None = None) -> None:
+    """Host delivery of a device-resident open, read hooks included (tlsgpu_deliver_host)."""
+    _check(table.lib.tlsgpu_deliver_host(table.handle, d_recs, d_status, n, d_out, out_bytes,
+                                         h_out, h_status, stream), "tlsgpu_deliver_host")
+
+
+def hook_write_streams(table: "SessionTable", h_streams: int, n: int, h_data: int,
+                       data_bytes: int) -> None:
+    """Write hooks over host application data of tlsgpu_seal_wire streams."""
+    _check(table.lib.tlsgpu_hook_write_streams(table.handle, h_streams, n, h_data, data_bytes),
+           "tlsgpu_hook_write_streams")
 
 
 def host_pipeline(engine: "Engine", streams: int = 0, chunk_bytes: int = 0) -> None:
@@ -626,8 +661,9 @@ def header_symbols() -> list[str]:
     """Function names declared in include/*.h (the exported ABI)."""
     import re
     names = []
-    for h in ("tlsgpu.h", "tlsgpu_evp.h"):
+    for h in ("tlsgpu.h", "tlsgpu_evp.h", "tlsgpu_talos.h"):
         src = open(os.path.join(INCLUDE, h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-        names += re.findall(r"\b((?:tlsgpu|EVP)_\w+)\s*\(", src)
+        names += re.findall(r"\b((?:tlsgpu|EVP|tls_processing|ecall_tls_processing)_\w+)\s*\(",
+                            src)
     return sorted(set(n for n in names if not n.startswith("TLSGPU")))

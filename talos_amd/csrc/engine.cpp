@@ -82,8 +82,6 @@ struct HostPipe {
   tlsgpu_record* d_recs = nullptr;
   int32_t* d_status = nullptr;
   size_t cap_in = 0, cap_out = 0, cap_recs = 0, cap_status = 0;
-  tlsgpu_plaintext_hook on_read = nullptr, on_write = nullptr;  // TaLoS hooks
-  void* hook_user = nullptr;
 };
 
 struct tlsgpu_engine {
@@ -135,6 +133,7 @@ struct tlsgpu_sessions {
   DevGcmTables* d_gcm;
   std::vector<int32_t> kinds;  // host mirror of installed kinds
   std::vector<uint8_t> tag_lens;  // and tag lengths (host pipeline output spans)
+  std::vector<const void*> owners;  // SSL* per session for the TaLoS hooks (set_owner)
   bool have[5];                // any session of kind k installed
 };
 
@@ -199,6 +198,7 @@ extern "C" int tlsgpu_sessions_create(tlsgpu_engine* e, uint32_t capacity, tlsgp
   t->capacity = capacity;
   t->kinds.assign(capacity, 0);
   t->tag_lens.assign(capacity, 16);
+  t->owners.assign(capacity, nullptr);
   memset(t->have, 0, sizeof(t->have));
   if (hipMalloc(&t->d_sess, sizeof(DevSession) * (size_t)capacity) != hipSuccess ||
       hipMalloc(&t->d_gcm, sizeof(DevGcmTables) * (size_t)capacity) != hipSuccess) {
@@ -574,13 +574,26 @@ static int host_batch(tlsgpu_sessions* t, bool seal, const tlsgpu_record* h_recs
   HostPipe& hp = e->host;
   std::lock_guard<std::mutex> lk(hp.mu);
   HIPCHK(hipSetDevice(e->device));
-  if (seal && hp.on_write) {  // tls_processing_ssl_write (s3_pkt.c.patch:19-33 placement)
+  // TaLoS tls_processing_ssl_write (do_ssl3_write, s3_pkt.c.patch:19-33): on
+  // each record's host plaintext before it goes to the device, in record
+  // order; the module may rewrite the bytes and shorten the record (then a
+  // private copy of the descriptors carries the new length)
+  std::vector<tlsgpu_record> hooked;
+  if (seal && talos_write_hooked()) {
     for (uint32_t i = 0; i < n; i++) {
-      const uint64_t len = h_recs[i].len_type & 0xFFFFFFu;
-      if (h_recs[i].session < t->capacity && h_recs[i].in_off + len <= in_bytes)
-        hp.on_write(hp.hook_user, h_recs[i].session, h_recs[i].seq,
-                    const_cast<uint8_t*>(h_in) + h_recs[i].in_off, (uint32_t)len);
+      const uint32_t len = h_recs[i].len_type & 0xFFFFFFu;
+      if (h_recs[i].session >= t->capacity || h_recs[i].in_off > in_bytes ||
+          len > in_bytes - h_recs[i].in_off)
+        continue;  // the bounds pass rejects it
+      uint32_t hl = len;
+      talos_write(t->owners[h_recs[i].session], const_cast<uint8_t*>(h_in) + h_recs[i].in_off,
+                  &hl);
+      if (hl < len) {
+        if (hooked.empty()) hooked.assign(h_recs, h_recs + n);
+        hooked[i].len_type = (hooked[i].len_type & 0xFF000000u) | hl;
+      }
     }
+    if (!hooked.empty()) h_recs = hooked.data();
   }
   const bool in_place = h_out == h_in;
   if (in_place) out_bytes = in_bytes;
@@ -705,11 +718,16 @@ static int host_batch(tlsgpu_sessions* t, bool seal, const tlsgpu_record* h_recs
       rc = fail(TLSGPU_EHIP, "host pipeline sync: %s", hipGetErrorString(e));
   }
   if (rc != TLSGPU_OK) return rc;
-  if (!seal && hp.on_read) {  // tls_processing_ssl_read (s3_pkt.c.patch:39-52 placement)
-    for (uint32_t i = 0; i < n; i++)
-      if (h_status[i] >= 0)
-        hp.on_read(hp.hook_user, h_recs[i].session, h_recs[i].seq, h_out + h_recs[i].out_off,
-                   (uint32_t)h_status[i]);
+  // TaLoS tls_processing_ssl_read (ssl3_read_bytes, s3_pkt.c.patch:39-52): on
+  // each delivered record's plaintext in h_out, in record order; a module that
+  // shortens it shortens what is delivered (h_status)
+  if (!seal && talos_read_hooked()) {
+    for (uint32_t i = 0; i < n; i++) {
+      if (h_status[i] < 0) continue;
+      uint32_t hl = (uint32_t)h_status[i];
+      talos_read(t->owners[h_recs[i].session], h_out + h_recs[i].out_off, &hl);
+      if (hl < (uint32_t)h_status[i]) h_status[i] = (int32_t)hl;
+    }
   }
   return TLSGPU_OK;
 }
@@ -727,13 +745,79 @@ extern "C" int tlsgpu_seal_host(tlsgpu_sessions* t, const tlsgpu_record* h_recs,
   return host_batch(t, true, h_recs, n, h_in, in_bytes, h_out, out_bytes, h_status);
 }
 
-extern "C" int tlsgpu_set_plaintext_hooks(tlsgpu_engine* e, tlsgpu_plaintext_hook on_read,
-                                          tlsgpu_plaintext_hook on_write, void* user) {
-  if (!e) return fail(TLSGPU_EINVAL, "null engine");
-  std::lock_guard<std::mutex> lk(e->host.mu);
-  e->host.on_read = on_read;
-  e->host.on_write = on_write;
-  e->host.hook_user = user;
+extern "C" int tlsgpu_sessions_set_owner(tlsgpu_sessions* t, uint32_t first, uint32_t n,
+                                         const void* const* owners) {
+  if (!t || (n && !owners)) return fail(TLSGPU_EINVAL, "bad arguments");
+  if ((uint64_t)first + n > t->capacity)
+    return fail(TLSGPU_ERANGE, "sessions [%u, %u) exceed capacity %u", first, first + n,
+                t->capacity);
+  for (uint32_t i = 0; i < n; i++) t->owners[first + i] = owners[i];
+  return TLSGPU_OK;
+}
+
+// Host delivery of device-resident opens (tlsgpu_open_batch / tlsgpu_open_wire):
+// descriptors and statuses back to the host, the delivered records' output
+// range to h_out (same offsets as d_out), then the TaLoS read hook on each
+// delivered record in record order.
+extern "C" int tlsgpu_deliver_host(tlsgpu_sessions* t, const tlsgpu_record* d_recs,
+                                   const int32_t* d_status, uint32_t n, const uint8_t* d_out,
+                                   size_t out_bytes, uint8_t* h_out, int32_t* h_status,
+                                   void* stream) {
+  if (!t || (n && (!d_recs || !d_status || !d_out || !h_out || !h_status)))
+    return fail(TLSGPU_EINVAL, "bad arguments");
+  if (n == 0) return TLSGPU_OK;
+  HIPCHK(hipSetDevice(t->eng->device));
+  hipStream_t s = stream ? (hipStream_t)stream : t->eng->stream;
+  std::vector<tlsgpu_record> recs(n);
+  HIPCHK(hipMemcpyAsync(recs.data(), d_recs, sizeof(tlsgpu_record) * (size_t)n,
+                        hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(h_status, d_status, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost,
+                        s));
+  HIPCHK(hipStreamSynchronize(s));
+  uint64_t lo = UINT64_MAX, hi = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if (h_status[i] < 0) continue;
+    const uint64_t o = recs[i].out_off, e = o + (uint64_t)h_status[i];
+    if (o > out_bytes || e > out_bytes || recs[i].session >= t->capacity)
+      return fail(TLSGPU_ERANGE, "record %u output [%llu, %llu) outside %zu bytes", i,
+                  (unsigned long long)o, (unsigned long long)e, out_bytes);
+    lo = std::min(lo, o);
+    hi = std::max(hi, e);
+  }
+  if (hi > lo) {
+    HIPCHK(hipMemcpyAsync(h_out + lo, d_out + lo, hi - lo, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
+  if (talos_read_hooked()) {
+    for (uint32_t i = 0; i < n; i++) {
+      if (h_status[i] < 0) continue;
+      uint32_t hl = (uint32_t)h_status[i];
+      talos_read(t->owners[recs[i].session], h_out + recs[i].out_off, &hl);
+      if (hl < (uint32_t)h_status[i]) h_status[i] = (int32_t)hl;
+    }
+  }
+  return TLSGPU_OK;
+}
+
+// The write side of tlsgpu_seal_wire for callers whose application data starts
+// in host memory: the TaLoS write hook on every fragment do_ssl3_write would
+// make of each stream (max_send_fragment split, s3_pkt.c:531-536), in place,
+// before the caller copies h_data to the device.  Lengths stay.
+extern "C" int tlsgpu_hook_write_streams(tlsgpu_sessions* t, const tlsgpu_write_stream* h_streams,
+                                         uint32_t n_streams, uint8_t* h_data, size_t data_bytes) {
+  if (!t || (n_streams && (!h_streams || !h_data))) return fail(TLSGPU_EINVAL, "bad arguments");
+  if (!talos_write_hooked()) return TLSGPU_OK;
+  for (uint32_t i = 0; i < n_streams; i++) {
+    const tlsgpu_write_stream& st = h_streams[i];
+    if (st.session >= t->capacity || st.data_off > data_bytes ||
+        st.data_len > data_bytes - st.data_off)
+      continue;
+    const uint32_t frag = st.max_fragment == 0 || st.max_fragment > 16384 ? 16384 : st.max_fragment;
+    for (uint64_t off = 0; off < st.data_len; off += frag) {
+      uint32_t hl = (uint32_t)std::min<uint64_t>(frag, st.data_len - off);
+      talos_write(t->owners[st.session], h_data + st.data_off + off, &hl);
+    }
+  }
   return TLSGPU_OK;
 }
 

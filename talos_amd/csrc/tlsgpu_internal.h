@@ -257,4 +257,11 @@ int launch_check_bounds(const tlsgpu_record* recs, tlsgpu_record* safe, uint32_t
                         uint64_t out_bytes, bool seal, int32_t* status, hipStream_t s);
 int launch_fill_synthetic_spans(uint8_t* d_out, const uint64_t* d_offs, const uint32_t* d_lens,
                                 uint32_t n, uint64_t seed, uint64_t index0, hipStream_t s);
+// TaLoS TLS-processing hooks (talos_hooks.cpp): is a callback registered, and
+// fire it (the callback may change *len) — used by the host-delivery paths.
+bool talos_read_hooked();
+bool talos_write_hooked();
+void talos_read(const void* ssl, uint8_t* data, uint32_t* len);
+void talos_write(const void* ssl, uint8_t* data, uint32_t* len);
+
 }  // namespace tg
