@@ -14,6 +14,11 @@
  *   @file: NREC little-endian uint32 record lengths (the config-D Zipf mix)
  *   AEAD: aes-128-gcm | aes-256-gcm | chacha20-poly1305
  *   OP:   open | seal | both  (both = seal then open per record, config C)
+ *         init  connection churn: every thread loops EVP_AEAD_CTX_init with a
+ *               fresh key + one seal of a REC_LEN record + EVP_AEAD_CTX_cleanup
+ *               (a connection direction's key install at ChangeCipherSpec,
+ *               t1_enc.c:444-495 -> e_aes.c:1372-1413, its first record, and
+ *               ssl_clear_cipher_ctx); reports contexts/s
  * prints one JSON object.
  */
 #include <dlfcn.h>
@@ -34,6 +39,7 @@ typedef int (*crypt_fn)(const EVP_AEAD_CTX *, unsigned char *, size_t *, size_t,
 
 static init_fn p_init;
 static crypt_fn p_seal, p_open;
+static void (*p_cleanup)(EVP_AEAD_CTX *);
 
 #define NSESS 64
 
@@ -83,6 +89,40 @@ fill(uint64_t seed, unsigned char *p, size_t n)
 			seed = sm64(&seed) ^ i;
 		p[i] = (unsigned char)(seed >> (8 * (i % 8)));
 	}
+}
+
+static const void *g_aead;
+static size_t g_key_len;
+
+/* OP init: contexts per second (key install + first record + cleanup) */
+static void *
+churn_worker(void *arg)
+{
+	struct targ *t = arg;
+	unsigned char *pt = calloc(1, rec_len + 1), *out = malloc(rec_len + 16);
+	unsigned char key[32], nonce[12] = {0}, ad[13] = {0};
+	size_t out_len;
+	uint64_t seed = 0xC4A2ULL + t->lo;
+	double t0 = now();
+	for (;;) {
+		EVP_AEAD_CTX c;
+		fill(sm64(&seed), key, g_key_len);
+		if (!p_init(&c, g_aead, key, g_key_len, 0, NULL)) {
+			t->failures++;
+			break;
+		}
+		if (!p_seal(&c, out, &out_len, rec_len + 16, nonce, 12, pt, rec_len, ad, 13))
+			t->failures++;
+		p_cleanup(&c);
+		t->records++;
+		t->bytes += rec_len;
+		if (now() - t0 >= budget)
+			break;
+	}
+	t->secs = now() - t0;
+	free(pt);
+	free(out);
+	return NULL;
 }
 
 static void *
@@ -146,6 +186,7 @@ main(int argc, char **argv)
 	p_init = (init_fn)dlsym(h, "EVP_AEAD_CTX_init");
 	p_seal = (crypt_fn)dlsym(h, "EVP_AEAD_CTX_seal");
 	p_open = (crypt_fn)dlsym(h, "EVP_AEAD_CTX_open");
+	p_cleanup = (void (*)(EVP_AEAD_CTX *))dlsym(h, "EVP_AEAD_CTX_cleanup");
 	if (!strcmp(argv[2], "aes-128-gcm")) {
 		which = (aead_fn)dlsym(h, "EVP_aead_aes_128_gcm");
 		key_len = 16;
@@ -161,7 +202,8 @@ main(int argc, char **argv)
 		return 1;
 	}
 	aead = which();
-	op = !strcmp(argv[3], "open") ? 0 : !strcmp(argv[3], "seal") ? 1 : 2;
+	op = !strcmp(argv[3], "open") ? 0 : !strcmp(argv[3], "seal") ? 1 :
+	    !strcmp(argv[3], "init") ? 3 : 2;
 	nrec = strtoul(argv[5], NULL, 0);
 	uint32_t *lens = NULL;
 	if (argv[4][0] == '@') {
@@ -183,6 +225,33 @@ main(int argc, char **argv)
 		return 2;
 	}
 
+	if (op == 3) {	/* connection churn */
+		if (!p_cleanup || argv[4][0] == '@') {
+			fprintf(stderr, "init needs EVP_AEAD_CTX_cleanup and a fixed REC_LEN\n");
+			return 2;
+		}
+		g_aead = aead;
+		g_key_len = key_len;
+		tid = calloc(threads, sizeof(*tid));
+		ta = calloc(threads, sizeof(*ta));
+		for (i = 0; i < threads; i++) {
+			ta[i].lo = (size_t)i;
+			pthread_create(&tid[i], NULL, churn_worker, &ta[i]);
+		}
+		for (i = 0; i < threads; i++) {
+			pthread_join(tid[i], NULL);
+			records += ta[i].records;
+			failures += ta[i].failures;
+			if (ta[i].secs > secs)
+				secs = ta[i].secs;
+		}
+		printf("{\"aead\": \"%s\", \"op\": \"init\", \"rec_len\": %zu, \"threads\": %d, "
+		    "\"contexts\": %llu, \"seconds\": %.4f, \"contexts_per_s\": %.1f, "
+		    "\"us_per_context_per_thread\": %.2f, \"failures\": %llu}\n", argv[2], rec_len,
+		    threads, records, secs, records / secs, secs * 1e6 * threads / (records ? records : 1),
+		    failures);
+		return failures ? 1 : 0;
+	}
 	for (i = 0; i < NSESS; i++) {
 		unsigned char key[32];
 		fill(0x5EED0001ULL + 977 * i, key, key_len);

@@ -135,6 +135,7 @@ struct tlsgpu_sessions {
   std::vector<uint8_t> tag_lens;  // and tag lengths (host pipeline output spans)
   std::vector<const void*> owners;  // SSL* per session for the TaLoS hooks (set_owner)
   bool have[5];                // any session of kind k installed
+  std::mutex mu;               // host mirrors, when several threads install at once
 };
 
 extern "C" int tlsgpu_device_count(int* count) {
@@ -255,6 +256,7 @@ extern "C" int tlsgpu_sessions_install(tlsgpu_sessions* t, uint32_t first, uint3
   if (err != hipSuccess || rc != 0 || serr != hipSuccess)
     return fail(TLSGPU_EHIP, "session install failed: %s",
                 hipGetErrorString(err != hipSuccess ? err : serr));
+  std::lock_guard<std::mutex> lk(t->mu);
   for (uint32_t i = 0; i < n; i++) {
     t->kinds[first + i] = params[i].aead;
     t->tag_lens[first + i] = (uint8_t)(params[i].tag_len ? params[i].tag_len : 16);
@@ -354,6 +356,25 @@ extern "C" int tlsgpu_debug_phase_stats(tlsgpu_engine* e, unsigned long long* ou
   return TLSGPU_OK;
 }
 
+// Hybrid-kernel experiment flags (TLSGPU_HY_FLAGS, tlsgpu_internal.h).  Bit 2
+// parks the waves of gcm_hy_kernel that are not bitsliced-pair waves, bit 4 the
+// bitsliced-pair waves.  A setting that parks every wave of the kernel that
+// runs leaves every record of the batch unprocessed: round 2's
+// gpurun_out/b16ab2 ("workload seal failed for 65536 records") ran the queue
+// kernel, whose waves (T-table and packed-bitsliced role alike, BSW = 0) all
+// obey bit 2.  Refused here: the park bits are dropped with a warning.
+static uint32_t sane_hy_flags(uint32_t f, int impl) {
+  const uint32_t parks = impl == TLSGPU_GCM_HYBRID ? 6u : impl == TLSGPU_GCM_BITSLICE ? 4u : 2u;
+  if ((f & parks) == parks) {
+    static std::once_flag warned;
+    std::call_once(warned, [f] {
+      fprintf(stderr, "libtlsgpu: TLSGPU_HY_FLAGS=%#x would park every wave; ignoring the "
+                      "park bits\n", f);
+    });
+    return f & ~6u;
+  }
+  return f;
+}
 static uint32_t g_hy_flags = []() {
   const char* v = getenv("TLSGPU_HY_FLAGS");
   return v ? (uint32_t)strtoul(v, nullptr, 0) & 15u : 0u;
@@ -405,7 +426,7 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   a.status = d_status;
   a.n_sessions = t->capacity;
   a.bs_reserve = g_bs_reserve;
-  a.hy_flags = g_hy_flags;
+
   a.dbg = g_phase_stats;
   a.bs16_min = g_bs16_min;
   a.pack = g_pack;
@@ -430,6 +451,7 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   const int impl = raw ? TLSGPU_GCM_TTABLE
                        : split ? TLSGPU_GCM_SPLIT
                        : sel_impl == TLSGPU_GCM_AUTO ? TLSGPU_GCM_QUEUE : sel_impl;
+  a.hy_flags = sane_hy_flags(g_hy_flags, impl);
   const bool gcm_pre = impl != TLSGPU_GCM_TTABLE && impl != TLSGPU_GCM_SPLIT &&
                        (have[TLSGPU_AES_128_GCM] || have[TLSGPU_AES_256_GCM]);
   // per-stream scratch: [RecPre x n (queue kernels) | ctl_bytes control words |
@@ -1087,13 +1109,46 @@ static size_t evp_pick() { return g_evp_rr.fetch_add(1) % evp_device_count(); }
 
 struct EvpBatcher;
 struct AeadState {
-  tlsgpu_sessions* sess;  // the shared EVP pool table (slot >= 0) or a private one
-  int slot;               // session id in sess
+  tlsgpu_sessions* sess;  // the device table holding the context's session
+  uint32_t slot;          // session id in sess
   int kind;
   unsigned tag_len;
-  EvpBatcher* batcher;    // the queue of the context's device (pooled contexts)
+  EvpBatcher* batcher;    // the queue of the context's device (pooled contexts), or null
   uint32_t evp_dev;       // index of the context's device among the EVP devices
 };
+
+// EVP context storage without a device allocation per context (connection
+// churn): contexts outside the coalescing queue take a slot of
+// per-device slab tables of kSlabSessions sessions, grown on demand; the slot
+// is scrubbed on cleanup and reused.
+constexpr uint32_t kSlabSessions = 1024;
+struct EvpSlab {
+  std::mutex mu;
+  std::vector<tlsgpu_sessions*> chunks;
+  std::vector<std::pair<tlsgpu_sessions*, uint32_t>> free;
+};
+static EvpSlab g_slabs[kMaxEvpDevices];
+
+static bool slab_take(size_t dk, tlsgpu_engine* e, tlsgpu_sessions** t, uint32_t* slot) {
+  EvpSlab& sl = g_slabs[dk];
+  std::lock_guard<std::mutex> lk(sl.mu);
+  if (sl.free.empty()) {
+    tlsgpu_sessions* c = nullptr;
+    if (tlsgpu_sessions_create(e, kSlabSessions, &c) != TLSGPU_OK) return false;
+    sl.chunks.push_back(c);
+    for (uint32_t i = kSlabSessions; i-- > 0;) sl.free.emplace_back(c, i);
+  }
+  *t = sl.free.back().first;
+  *slot = sl.free.back().second;
+  sl.free.pop_back();
+  return true;
+}
+
+static void slab_give(size_t dk, tlsgpu_sessions* t, uint32_t slot) {
+  EvpSlab& sl = g_slabs[dk];
+  std::lock_guard<std::mutex> lk(sl.mu);
+  sl.free.emplace_back(t, slot);
+}
 
 // ---------------------------------------------------------------------------
 // EVP coalescing queue (TaLoS make_asynchronous_ecall,
@@ -1169,8 +1224,18 @@ struct EvpBatcher {
 // one coalescing queue per EVP device (index as evp_engine); g_batcher_on once
 // tlsgpu_evp_set_batching has created them
 static EvpBatcher* g_batchers[kMaxEvpDevices] = {};
-static bool g_batcher_on = false;
 static std::mutex g_batcher_mu;
+
+// Give a context's session slot back to its queue pool or slab.
+static void release_slot(AeadState* st) {
+  if (st->batcher) {
+    std::lock_guard<std::mutex> lk(g_batcher_mu);
+    st->batcher->free_sessions.push_back((int)st->slot);
+  } else {
+    slab_give(st->evp_dev, st->sess, st->slot);
+  }
+}
+static bool g_batcher_on = false;
 
 static inline void futex_wait(std::atomic<uint32_t>* w, uint32_t v) {
   syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAIT_PRIVATE, v, nullptr, nullptr, 0);
@@ -1251,6 +1316,44 @@ static Staging* stage_for(int dev) {
   return st;
 }
 
+// One session install for an EVP context, on the calling thread's call stream
+// through its pinned staging (no device allocation, no engine-stream
+// serialisation): the key install of one connection direction.
+static int install_one(tlsgpu_sessions* t, uint32_t slot, const tlsgpu_session_params& p) {
+  if (!valid_params(p) || slot >= t->capacity) return fail(TLSGPU_EINVAL, "bad session");
+  Staging* stg = stage_for(t->eng->device);
+  if (!stg || !stg->ensure(t->eng->device, sizeof(p))) return fail(TLSGPU_ENOMEM, "staging");
+  memcpy(stg->h_buf, &p, sizeof(p));
+  auto* d_params = reinterpret_cast<tlsgpu_session_params*>(stg->d_buf);
+  const bool ok =
+      hipMemcpyAsync(d_params, stg->h_buf, sizeof(p), hipMemcpyHostToDevice, stg->stream) ==
+          hipSuccess &&
+      launch_session_install(t->d_sess, t->d_gcm, d_params, slot, 1, stg->stream) == 0 &&
+      hipEventRecord(stg->done, stg->stream) == hipSuccess &&
+      hipEventSynchronize(stg->done) == hipSuccess;
+  memset(stg->h_buf, 0, sizeof(p));
+  if (!ok) return fail(TLSGPU_EHIP, "session install: %s", hipGetErrorString(hipGetLastError()));
+  std::lock_guard<std::mutex> lk(t->mu);
+  t->kinds[slot] = p.aead;
+  t->tag_lens[slot] = (uint8_t)(p.tag_len ? p.tag_len : 16);
+  t->have[p.aead] = true;
+  return TLSGPU_OK;
+}
+
+// Zero a session slot's key material on the calling thread's stream and wait.
+static void scrub_slot(tlsgpu_sessions* t, uint32_t slot) {
+  Staging* stg = stage_for(t->eng->device);
+  if (stg && stg->ensure(t->eng->device, 16) &&
+      hipMemsetAsync(t->d_sess + slot, 0, sizeof(DevSession), stg->stream) == hipSuccess &&
+      hipMemsetAsync(t->d_gcm + slot, 0, sizeof(DevGcmTables), stg->stream) == hipSuccess &&
+      hipEventRecord(stg->done, stg->stream) == hipSuccess &&
+      hipEventSynchronize(stg->done) == hipSuccess)
+    return;
+  (void)hipSetDevice(t->eng->device);  // fall back to the synchronous form
+  (void)hipMemset(t->d_sess + slot, 0, sizeof(DevSession));
+  (void)hipMemset(t->d_gcm + slot, 0, sizeof(DevGcmTables));
+}
+
 extern "C" int EVP_AEAD_CTX_init(EVP_AEAD_CTX* ctx, const EVP_AEAD* aead, const unsigned char* key,
                                  size_t key_len, size_t tag_len, ENGINE* impl) {
   (void)impl;
@@ -1274,24 +1377,21 @@ extern "C" int EVP_AEAD_CTX_init(EVP_AEAD_CTX* ctx, const EVP_AEAD* aead, const 
   if (!st) return 0;
   st->kind = aead->kind;
   st->tag_len = (unsigned)tag_len;
-  st->slot = -1;
   st->batcher = nullptr;
   st->evp_dev = (uint32_t)dk;
   {
     std::lock_guard<std::mutex> lk(g_batcher_mu);
     EvpBatcher* b = g_batchers[dk];
     if (b && !b->free_sessions.empty()) {
-      st->slot = b->free_sessions.back();
+      st->slot = (uint32_t)b->free_sessions.back();
       b->free_sessions.pop_back();
       st->sess = b->pool;
       st->batcher = b;
     }
   }
-  if (st->slot < 0) {
-    if (tlsgpu_sessions_create(e, 1, &st->sess) != TLSGPU_OK) {
-      delete st;
-      return 0;
-    }
+  if (!st->batcher && !slab_take(dk, e, &st->sess, &st->slot)) {
+    delete st;
+    return 0;
   }
   tlsgpu_session_params p;
   memset(&p, 0, sizeof(p));
@@ -1300,20 +1400,14 @@ extern "C" int EVP_AEAD_CTX_init(EVP_AEAD_CTX* ctx, const EVP_AEAD* aead, const 
   memcpy(p.key, key, key_len);
   p.tag_len = (uint32_t)tag_len;
   p.version = 0x0303;
-  int rc = tlsgpu_sessions_install(st->sess, st->slot < 0 ? 0 : (uint32_t)st->slot, 1, &p);
+  // on this thread's call stream: installs of concurrent threads overlap
+  const int rc = install_one(st->sess, st->slot, p);
   memset(&p, 0, sizeof(p));
   if (rc != TLSGPU_OK) {
-    if (st->slot < 0) {
-      tlsgpu_sessions_destroy(st->sess);
-    } else {
-      std::lock_guard<std::mutex> lk(g_batcher_mu);
-      st->batcher->free_sessions.push_back(st->slot);
-    }
+    release_slot(st);
     delete st;
     return 0;
   }
-  if (st->slot < 0) st->slot = 0;
-  else st->slot |= 0x40000000;  // marks a pool slot (see pool_slot)
   g_evp_dev_ctx[dk].fetch_add(1, std::memory_order_relaxed);
   ctx->aead_state = st;
   return 1;
@@ -1323,18 +1417,10 @@ extern "C" void EVP_AEAD_CTX_cleanup(EVP_AEAD_CTX* ctx) {
   if (ctx->aead == nullptr) return;
   auto* st = (AeadState*)ctx->aead_state;
   if (st) {
-    // scrub the device key material before freeing (explicit_bzero analogue)
-    const bool pooled = (st->slot & 0x40000000) != 0;
-    const uint32_t slot = (uint32_t)(st->slot & 0x3FFFFFFF);
-    (void)hipSetDevice(st->sess->eng->device);
-    (void)hipMemset(st->sess->d_sess + slot, 0, sizeof(DevSession));
-    (void)hipMemset(st->sess->d_gcm + slot, 0, sizeof(DevGcmTables));
-    if (pooled) {
-      std::lock_guard<std::mutex> lk(g_batcher_mu);
-      st->batcher->free_sessions.push_back((int)slot);
-    } else {
-      tlsgpu_sessions_destroy(st->sess);
-    }
+    // scrub the device key material before the slot is reused
+    // (explicit_bzero analogue, e_aes.c:1415-1422), on this thread's stream
+    scrub_slot(st->sess, st->slot);
+    release_slot(st);
     delete st;
   }
   ctx->aead_state = nullptr;
@@ -1402,8 +1488,7 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
                          size_t max_out_len, const unsigned char* nonce, size_t nonce_len,
                          const unsigned char* in, size_t in_len, const unsigned char* ad,
                          size_t ad_len) {
-  const bool pooled = (st->slot & 0x40000000) != 0;
-  if (pooled) {  // pooled context: join the coalescing queue (large jobs run alone)
+  if (st->batcher) {  // pooled context: join the coalescing queue (large jobs run alone)
     int r = evp_queue_call(st->batcher, st, seal, out, out_len, max_out_len, nonce, nonce_len,
                            in, in_len, ad, ad_len);
     if (r != -2) return r;
@@ -1427,7 +1512,7 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
   j->in_len = (uint32_t)in_len;
   j->nonce_len = (uint32_t)nonce_len;
   j->aad_len = (uint32_t)ad_len;
-  j->session = (uint32_t)(st->slot & 0x3FFFFFFF);
+  j->session = st->slot;
   j->max_out = max_out_len;
   if (nonce_len) memcpy(h + o_nonce, nonce, nonce_len);
   if (ad_len) memcpy(h + o_ad, ad, ad_len);
@@ -1947,7 +2032,7 @@ static int evp_queue_call(EvpBatcher* b, const AeadState* st, bool seal, unsigne
   rj->in_len = (uint32_t)in_len;
   rj->nonce_len = (uint32_t)nonce_len;
   rj->aad_len = (uint32_t)ad_len;
-  rj->session = (uint32_t)(st->slot & 0x3FFFFFFF);
+  rj->session = st->slot;
   rj->max_out = max_out_len;
   s->writers.fetch_sub(1, std::memory_order_release);
   while (s->gen.load(std::memory_order_acquire) == gen) futex_wait(&s->gen, gen);

@@ -10,7 +10,7 @@
 
 namespace tg {
 
-__device__ const ByteTable g_sbox = kSbox;
+__device__ const ByteTable g_sbox __attribute__((aligned(16))) = kSbox;
 
 struct U128 { uint64_t hi, lo; };  // big-endian halves, x^0 = MSB of hi
 
@@ -21,48 +21,43 @@ __device__ inline U128 gf_mulx(U128 v) {
   return v;
 }
 
-__device__ inline U128 gf_mul(U128 a, U128 b) {  // SP 800-38D Algorithm 1
-  U128 z{0, 0};
-  for (int i = 0; i < 128; i++) {
-    uint64_t bit = (i < 64) ? (a.hi >> (63 - i)) & 1 : (a.lo >> (127 - i)) & 1;
-    if (bit) { z.hi ^= b.hi; z.lo ^= b.lo; }
-    b = gf_mulx(b);
-  }
-  return z;
-}
-
-__device__ inline uint32_t sub_word(uint32_t w) {
-  return ((uint32_t)g_sbox.v[w >> 24] << 24) | ((uint32_t)g_sbox.v[(w >> 16) & 0xff] << 16) |
-         ((uint32_t)g_sbox.v[(w >> 8) & 0xff] << 8) | g_sbox.v[w & 0xff];
+// S-box lookups from the workgroup's LDS copy (a global-memory table costs a
+// dependent L2 round trip per round of the serial key schedule)
+__device__ inline uint32_t sub_word(const uint8_t* sb, uint32_t w) {
+  return ((uint32_t)sb[w >> 24] << 24) | ((uint32_t)sb[(w >> 16) & 0xff] << 16) |
+         ((uint32_t)sb[(w >> 8) & 0xff] << 8) | sb[w & 0xff];
 }
 
 // FIPS-197 key expansion (aes_core.c:628-723); big-endian words.
-__device__ inline int expand_key(const uint8_t* key, int key_len, uint32_t* rk_be) {
+__device__ inline int expand_key(const uint8_t* sb, const uint8_t* key, int key_len,
+                                 uint32_t* rk_be) {
   int nk = key_len / 4, rounds = nk + 6, total = 4 * (rounds + 1);
   uint32_t rcon = 1;
   for (int i = 0; i < nk; i++)
     rk_be[i] = ((uint32_t)key[4 * i] << 24) | ((uint32_t)key[4 * i + 1] << 16) |
                ((uint32_t)key[4 * i + 2] << 8) | key[4 * i + 3];
+  uint32_t prev = rk_be[nk - 1];
   for (int i = nk; i < total; i++) {
-    uint32_t t = rk_be[i - 1];
+    uint32_t t = prev;
     if (i % nk == 0) {
-      t = sub_word((t << 8) | (t >> 24)) ^ (rcon << 24);
+      t = sub_word(sb, (t << 8) | (t >> 24)) ^ (rcon << 24);
       rcon = xtime8((uint8_t)rcon);
     } else if (nk > 6 && i % nk == 4) {
-      t = sub_word(t);
+      t = sub_word(sb, t);
     }
-    rk_be[i] = rk_be[i - nk] ^ t;
+    prev = rk_be[i] = rk_be[i - nk] ^ t;
   }
   return rounds;
 }
 
 // Byte-wise AES encryption of one block (aes_core.c:789-972), cold path only.
-__device__ inline void aes_encrypt_bytes(const uint32_t* rk_be, int rounds, uint8_t s[16]) {
+__device__ inline void aes_encrypt_bytes(const uint8_t* sb, const uint32_t* rk_be, int rounds,
+                                         uint8_t s[16]) {
   uint8_t t[16];
   for (int i = 0; i < 16; i++) s[i] ^= (uint8_t)(rk_be[i / 4] >> (24 - 8 * (i % 4)));
   for (int r = 1; r <= rounds; r++) {
     for (int c = 0; c < 4; c++)
-      for (int i = 0; i < 4; i++) t[c * 4 + i] = g_sbox.v[s[((c + i) & 3) * 4 + i]];
+      for (int i = 0; i < 4; i++) t[c * 4 + i] = sb[s[((c + i) & 3) * 4 + i]];
     for (int c = 0; c < 4; c++) {
       uint8_t a0 = t[4 * c], a1 = t[4 * c + 1], a2 = t[4 * c + 2], a3 = t[4 * c + 3];
       if (r != rounds) {
@@ -85,93 +80,147 @@ __device__ inline void store_le(uint32_t* w, U128 v) {  // 16-byte string -> LE 
   w[2] = bswap32((uint32_t)(v.lo >> 32));
   w[3] = bswap32((uint32_t)v.lo);
 }
-__device__ inline void store_be(uint32_t* w, U128 v) {
-  w[0] = (uint32_t)(v.hi >> 32);
-  w[1] = (uint32_t)v.hi;
-  w[2] = (uint32_t)(v.lo >> 32);
-  w[3] = (uint32_t)v.lo;
+__device__ inline uint4 be_words(U128 v) {
+  return make_uint4((uint32_t)(v.hi >> 32), (uint32_t)v.hi, (uint32_t)(v.lo >> 32), (uint32_t)v.lo);
 }
 
-// One wave per session (blockIdx.x = session index): the key schedule and H
-// are computed by every lane (wave-uniform), then the 65 GHASH powers, their
-// Shoup tables, the H^64 basis and the bitsliced round-key masks are split
-// over the lanes.  Lane e gets H^(e+1) by square-and-multiply from the seven
-// squarings H^(2^k), so the longest chain is 6 squarings + 6 products instead
-// of the 64 serial products of a one-thread-per-session form (487 us per
-// session on MI355X, which was the EVP_AEAD_CTX_init latency).
+// Shoup 4-bit table of y (gcm128.c:255-324 layout, big-endian words):
+// m[8] = y, m[4] = y.x, m[2] = y.x^2, m[1] = y.x^3, m[a ^ b] = m[a] ^ m[b].
+__device__ inline void shoup_table(U128 y, U128 (&m)[16]) {
+  m[0] = U128{0, 0};
+  m[8] = y;
+  m[4] = gf_mulx(m[8]);
+  m[2] = gf_mulx(m[4]);
+  m[1] = gf_mulx(m[2]);
+  for (int a = 2; a < 16; a <<= 1)
+    for (int b = 1; b < a; b++) m[a + b] = U128{m[a].hi ^ m[b].hi, m[a].lo ^ m[b].lo};
+}
+
+// rem_4bit[r] >> 32 (gcm128.c:327-331) on the VALU: (r * 0xE1) << 21, carry-less
+__device__ inline uint32_t rem4v(uint32_t r) {
+  return (r << 21) ^ ((r ^ (r << 1) ^ (r << 2)) << 26);
+}
+
+// z = x * y with y's Shoup table in LDS (16 x 16 B = all 64 banks: lanes with
+// different nibbles never conflict, equal ones broadcast) — gcm_gmult_4bit
+// (gcm128.c:333-393); 32 nibble steps instead of the 128 of a bit-serial product.
+__device__ inline U128 gf_mul_tab(U128 x, const uint4* tab) {
+  const uint32_t X[4] = {(uint32_t)(x.hi >> 32), (uint32_t)x.hi, (uint32_t)(x.lo >> 32),
+                         (uint32_t)x.lo};
+  uint4 m = tab[X[3] & 0xF];
+  uint32_t z0 = m.x, z1 = m.y, z2 = m.z, z3 = m.w;
+#pragma unroll
+  for (int k = 1; k < 32; k++) {
+    const uint32_t nib = (X[3 - k / 8] >> (4 * (k % 8))) & 0xF;
+    const uint32_t rem = z3 & 0xF;
+    z3 = __builtin_amdgcn_alignbit(z2, z3, 4);
+    z2 = __builtin_amdgcn_alignbit(z1, z2, 4);
+    z1 = __builtin_amdgcn_alignbit(z0, z1, 4);
+    z0 = (z0 >> 4) ^ rem4v(rem);
+    const uint4 t = tab[nib];
+    z0 ^= t.x; z1 ^= t.y; z2 ^= t.z; z3 ^= t.w;
+  }
+  return U128{((uint64_t)z0 << 32) | z1, ((uint64_t)z2 << 32) | z3};
+}
+
+// One wave per session (blockIdx.x = session index), the work of
+// aead_aes_gcm_init / CRYPTO_gcm128_init (e_aes.c:1372-1413, gcm128.c:681-747)
+// plus the tables of the batch kernels.  The latency of one install is the
+// latency of EVP_AEAD_CTX_init and of a connection's key install, so it is
+// written for latency: the S-box and the session header are built in LDS (no
+// scratch memory, one 16-B store per lane), the key schedule and H = E_K(0)
+// run on one lane from LDS, the seven squarings H^(2^k) and the per-lane powers
+// H^e (lane e, square-and-multiply over them) use 4-bit products against
+// Shoup tables shared in LDS.  Round 2 measured 104 us per install with
+// global-memory S-box lookups, a scratch DevSession and bit-serial products.
 __global__ __launch_bounds__(64) void install_sessions(DevSession* __restrict__ sessions,
                                                        DevGcmTables* __restrict__ tables,
                                                        const tlsgpu_session_params* __restrict__ params,
                                                        uint32_t first, uint32_t n) {
+  __shared__ __attribute__((aligned(16))) uint8_t sb[256];
+  __shared__ uint32_t rk_be[60];
+  __shared__ uint8_t hb[16];
+  __shared__ uint4 hdr[sizeof(DevSession) / 16];
+  __shared__ uint4 sqtab[7][16];  // Shoup tables of H^(2^k), k = 0..6
   const uint32_t i = blockIdx.x;
   const uint32_t lane = threadIdx.x;
   if (i >= n) return;
+  static_assert(sizeof(DevSession) / 16 == 64, "one 16-B chunk of the header per lane");
+  reinterpret_cast<uint32_t*>(sb)[lane] = reinterpret_cast<const uint32_t*>(g_sbox.v)[lane];
+  hdr[lane] = make_uint4(0, 0, 0, 0);
   const tlsgpu_session_params p = params[i];
-  DevSession s = {};
-  uint32_t id = first + i;
-  bool gcm = p.aead == TLSGPU_AES_128_GCM || p.aead == TLSGPU_AES_256_GCM;
-  bool cc = p.aead == TLSGPU_CHACHA20_POLY1305 || p.aead == TLSGPU_CHACHA20_POLY1305_OLD;
-  uint32_t want_key = p.aead == TLSGPU_AES_128_GCM ? 16 : 32;
-  uint32_t tag = p.tag_len == 0 ? 16 : p.tag_len;
-  if ((!gcm && !cc) || p.key_len != want_key || tag > 16 || p.fixed_iv_len > 12) {
-    if (lane == 0) sessions[id] = s;  // kind 0: empty / invalid
-    return;
+  const uint32_t id = first + i;
+  const bool gcm = p.aead == TLSGPU_AES_128_GCM || p.aead == TLSGPU_AES_256_GCM;
+  const bool cc = p.aead == TLSGPU_CHACHA20_POLY1305 || p.aead == TLSGPU_CHACHA20_POLY1305_OLD;
+  const uint32_t want_key = p.aead == TLSGPU_AES_128_GCM ? 16 : 32;
+  const uint32_t tag = p.tag_len == 0 ? 16 : p.tag_len;
+  const bool valid = (gcm || cc) && p.key_len == want_key && tag <= 16 && p.fixed_iv_len <= 12;
+  __syncthreads();
+  DevSession& s = *reinterpret_cast<DevSession*>(hdr);
+  uint32_t rounds = 0;
+  if (valid && lane == 0) {  // header fields; kind stays 0 for an invalid slot
+    s.kind = (uint32_t)p.aead;
+    s.tag_len = tag;
+    s.key_len = p.key_len;
+    s.fixed_nonce_len = p.fixed_iv_len;
+    s.xor_fixed_nonce = p.aead == TLSGPU_CHACHA20_POLY1305;
+    s.nonce_in_record = gcm;
+    s.version = p.version;
+    for (uint32_t k = 0; k < p.fixed_iv_len; k++) s.fixed_nonce[k] = p.fixed_iv[k];
+    if (cc)
+      for (int k = 0; k < 32; k++) s.chacha_key[k] = p.key[k];
+    if (gcm) {
+      s.rounds = (uint32_t)expand_key(sb, p.key, (int)p.key_len, rk_be);
+      for (int k = 0; k < 16; k++) hb[k] = 0;
+      aes_encrypt_bytes(sb, rk_be, (int)s.rounds, hb);  // H = E_K(0^128)
+    }
   }
-  s.kind = (uint32_t)p.aead;
-  s.tag_len = tag;
-  s.key_len = p.key_len;
-  s.fixed_nonce_len = p.fixed_iv_len;
-  s.xor_fixed_nonce = p.aead == TLSGPU_CHACHA20_POLY1305;
-  s.nonce_in_record = gcm;
-  s.version = p.version;
-  for (uint32_t k = 0; k < p.fixed_iv_len; k++) s.fixed_nonce[k] = p.fixed_iv[k];
-  if (cc) {
-    for (int k = 0; k < 32; k++) s.chacha_key[k] = p.key[k];
-    if (lane == 0) sessions[id] = s;
-    return;
+  __syncthreads();
+  if (valid && gcm) {
+    rounds = s.rounds;
+    if (lane < 4 * (rounds + 1)) {
+      const uint32_t w = bswap32(rk_be[lane]);
+      s.rk[lane] = w;
+      s.rk_rot[lane] = __builtin_amdgcn_alignbit(w, w, 16);
+    }
   }
-  uint32_t rk_be[60];
-  s.rounds = (uint32_t)expand_key(p.key, (int)p.key_len, rk_be);
-  for (int k = 0; k < 4 * ((int)s.rounds + 1); k++) {
-    s.rk[k] = bswap32(rk_be[k]);
-    s.rk_rot[k] = __builtin_amdgcn_alignbit(s.rk[k], s.rk[k], 16);
-  }
-  uint8_t hb[16] = {};
-  aes_encrypt_bytes(rk_be, (int)s.rounds, hb);  // H = E_K(0^128)
   U128 H{0, 0};
   for (int k = 0; k < 8; k++) {
     H.hi = (H.hi << 8) | hb[k];
     H.lo = (H.lo << 8) | hb[8 + k];
   }
-  store_le(s.h_le, H);
-  if (lane == 0) sessions[id] = s;
+  if (valid && gcm && lane == 0) store_le(s.h_le, H);
+  __syncthreads();
+  reinterpret_cast<uint4*>(sessions + id)[lane] = hdr[lane];
+  if (!valid || !gcm) return;
 
   DevGcmTables* t = &tables[id];
   // bitsliced AddRoundKey masks: (rounds + 1) x 128 words over the lanes
-  for (uint32_t w = lane; w < 128u * (s.rounds + 1); w += 64) {
+  for (uint32_t w = lane; w < 128u * (rounds + 1); w += 64) {
     const uint32_t r = w / 128, b = (w % 128) / 8, k = w % 8;
     t->bsrk[r][8 * b + k] = 0u - ((s.rk[4 * r + b / 4] >> (8 * (b % 4) + k)) & 1u);
   }
-  U128 sq[7];  // H^(2^k)
+  // sq[k] = H^(2^k), each squaring against the previous power's shared table
+  U128 sq[7];
   sq[0] = H;
-  for (int k = 1; k < 7; k++) sq[k] = gf_mul(sq[k - 1], sq[k - 1]);
-  for (uint32_t e = lane + 1; e <= (uint32_t)kPowMax; e += 64) {
-    U128 pw{0, 0};
-    bool have = false;
-    for (int k = 0; k < 7; k++) {
-      if (!((e >> k) & 1)) continue;
-      pw = have ? gf_mul(pw, sq[k]) : sq[k];
-      have = true;
+  for (int k = 0; k < 7; k++) {
+    if (k > 0) sq[k] = gf_mul_tab(sq[k - 1], sqtab[k - 1]);
+    if (lane < 16) {
+      U128 m[16];
+      shoup_table(sq[k], m);
+      sqtab[k][lane] = be_words(m[lane]);
     }
+    __syncthreads();
+  }
+  // lane e - 1 (and lane 0 for e = 65): H^e by square-and-multiply, its Shoup table
+  for (uint32_t e = lane + 1; e <= (uint32_t)kPowMax; e += 64) {
+    int k0 = __builtin_ctz(e);
+    U128 pw = sq[k0];
+    for (int k = k0 + 1; k < 7; k++)
+      if ((e >> k) & 1) pw = gf_mul_tab(pw, sqtab[k]);
     U128 m[16];
-    m[0] = U128{0, 0};
-    m[8] = pw;
-    m[4] = gf_mulx(m[8]);
-    m[2] = gf_mulx(m[4]);
-    m[1] = gf_mulx(m[2]);
-    for (int a = 2; a < 16; a <<= 1)
-      for (int b = 1; b < a; b++) m[a + b] = U128{m[a].hi ^ m[b].hi, m[a].lo ^ m[b].lo};
-    for (int v = 0; v < 16; v++) store_be(t->shoup[e - 1][v], m[v]);
+    shoup_table(pw, m);
+    for (int v = 0; v < 16; v++) *reinterpret_cast<uint4*>(t->shoup[e - 1][v]) = be_words(m[v]);
   }
   // basis[q] = K * x^q, K = H^64 = sq[6]; lanes q and q + 64
   for (uint32_t q = lane; q < 128; q += 64) {
