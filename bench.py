@@ -162,6 +162,55 @@ def load_traffic(config: str, kernel: str):
     return None, None
 
 
+# Measured pipe rates (tools/ubench.hip, profiles/r03a_ubench.jsonl, 16 waves
+# per CU): CU cycles per ds_read_b32 in dependent lookup chains and per
+# conflict-free ds_read_b128 — the LDS issue the T-table GCM loop is bound by.
+LDS_B32_CYC, LDS_B128_CYC = 2.32, 4.96
+AES_LOOKUPS = {10: 138, 14: 202}   # ds_read_b32 per 64-block step (TLS counter shortcut)
+GHASH_B128 = 16                    # ds_read_b128 per 64-block Horner step (byte-position table)
+
+
+def pmc_profile(config: str, kernel: str):
+    p = os.path.join(ROOT, "profiles", f"pmc_config{config}.json")
+    try:
+        d = json.load(open(p))
+        return d if kernel in d.get("kernel", "") else None
+    except (OSError, ValueError):
+        return None
+
+
+def compute_roofline(kind_name: str, lengths, per_launch_s: float, prof, cus: int) -> dict:
+    """The binding on-chip pipe: for AES-GCM the LDS, priced
+    with the measured rates above — compute_ceiling = the payload rate at which
+    this launch's algorithmic lookups would keep every CU's LDS busy at those
+    rates, at the clock the kernel ran under PMC (GRBM_GUI_ACTIVE / 8 XCDs /
+    duration, profiles/pmc_config*.json).  Plus the PMC pipe-busy fractions."""
+    out = {}
+    clock = 2.05e9
+    c = (prof or {}).get("counters_per_launch_mean", {})
+    dur = (prof or {}).get("mean_duration_ns_profiled")
+    if c.get("GRBM_GUI_ACTIVE") and dur:
+        clock = c["GRBM_GUI_ACTIVE"] / 8 / (dur * 1e-9)
+        cyc = c["GRBM_GUI_ACTIVE"] / 8
+        if c.get("SQ_LDS_IDX_ACTIVE"):
+            out["pmc_lds_busy"] = round(c["SQ_LDS_IDX_ACTIVE"] / (cus * cyc), 3)
+        if c.get("SQ_INSTS_VALU"):   # 2 cycles per wave64 VALU op on a SIMD-32 (lower bound)
+            out["pmc_valu_busy_lb"] = round(c["SQ_INSTS_VALU"] * 2 / (4 * cus * cyc), 3)
+        out["pmc_clock_ghz"] = round(clock / 1e9, 3)
+    if "gcm" in kind_name:
+        rounds = 10 if "128" in kind_name else 14
+        steps = sum((int(l) + 16 + 15) // 16 / 64.0 for l in lengths)   # data + AAD + lengths blocks
+        lds_cyc = steps * (AES_LOOKUPS[rounds] * LDS_B32_CYC + GHASH_B128 * LDS_B128_CYC) / cus
+        ceiling = float(sum(int(l) for l in lengths)) / (lds_cyc / clock) / GIB
+        out.update({"compute_bound": "lds", "compute_ceiling_GiBps": round(ceiling, 1),
+                    "compute_model": f"{AES_LOOKUPS[rounds]} ds_read_b32 x {LDS_B32_CYC} + "
+                                     f"{GHASH_B128} ds_read_b128 x {LDS_B128_CYC} CU-cycles per "
+                                     f"64-block step at {clock / 1e9:.2f} GHz"})
+    else:
+        out["compute_bound"] = "valu"
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -287,7 +336,12 @@ def main():
     # session runs of the batch (prep-pass selection, tlsgpu_internal.h pws_selected)
     runs = per_gpu if args.interleave and sessions > 1 else min(sessions, per_gpu)
     kernel = main_kernel(kind_name, op, CONFIGS[args.config][3] is None, runs * 12 > per_gpu, wl.n)
-    traffic, traffic_src = load_traffic(args.config, kernel)
+    prof_cfg = "B" if args.config == "E" else args.config   # same kernel, same per-GPU batch
+    traffic, traffic_src = load_traffic(prof_cfg, kernel)
+    comp = compute_roofline(kind_name, [rec_len] * wl.n if lengths is None else lengths.tolist(),
+                            per_launch_s, pmc_profile(prof_cfg, kernel), eng.num_cus)
+    if "compute_ceiling_GiBps" in comp:
+        comp["compute_frac"] = round(value / world / comp["compute_ceiling_GiBps"], 4)
 
     line = {
         "metric": METRIC if args.config in ("B", "E") else
@@ -324,7 +378,7 @@ def main():
                      "read_frac": round(algo_rd / per_launch_s / 1e9 / HBM_PEAK_GBS, 4),
                      "kernel": kernel, "traffic_source": traffic_src,
                      "timing": "HIP events around each whole step on the engine stream "
-                               "(prep pass + status memset + main kernel)"},
+                               "(prep pass + status memset + main kernel)", **comp},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if rec_len:
