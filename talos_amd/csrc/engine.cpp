@@ -446,8 +446,6 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
     a.records_per_group = 1;
     groups = (int)n;
   }
-  // records whose session is empty/invalid keep this status
-  HIPCHK(hipMemsetD32Async((hipDeviceptr_t)d_status, (int)TLSGPU_REC_PUBLIC_INVALID, n, s));
   const int impl = raw ? TLSGPU_GCM_TTABLE
                        : split ? TLSGPU_GCM_SPLIT
                        : sel_impl == TLSGPU_GCM_AUTO ? TLSGPU_GCM_QUEUE : sel_impl;
@@ -475,19 +473,28 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
     }
     if (!scratch) return fail(TLSGPU_ENOMEM, "batch scratch (%u records)", n);
   }
-  if (bounds) {
-    auto* safe = reinterpret_cast<tlsgpu_record*>(scratch + pre_bytes);
-    if (launch_check_bounds(reinterpret_cast<const tlsgpu_record*>(d_descs), safe, n, t->d_sess,
-                            t->capacity, bounds->in_bytes, bounds->out_bytes, seal, d_status, s))
-      return fail(TLSGPU_EHIP, "bounds launch: %s", hipGetErrorString(hipGetLastError()));
-    a.descs = safe;
-  }
   RecPre* pre = nullptr;  // per-record constants of the queue kernels (per-stream scratch)
   uint8_t* ctl = nullptr;
   if (gcm_pre) {
     pre = reinterpret_cast<RecPre*>(scratch);
     ctl = reinterpret_cast<uint8_t*>(pre + n);
-    if (impl == TLSGPU_GCM_QUEUE) HIPCHK(hipMemsetAsync(ctl, 0, ctl_bytes, s));
+  }
+  uint8_t* const ctl_zero = impl == TLSGPU_GCM_QUEUE ? ctl : nullptr;
+  if (bounds) {
+    // one setup launch: sanitized descriptors, every record's initial status
+    // (records whose session is empty / invalid keep TLSGPU_REC_PUBLIC_INVALID)
+    // and the zeroed control words
+    auto* safe = reinterpret_cast<tlsgpu_record*>(scratch + pre_bytes);
+    if (launch_check_bounds(reinterpret_cast<const tlsgpu_record*>(d_descs), safe, n, t->d_sess,
+                            t->capacity, bounds->in_bytes, bounds->out_bytes, seal, d_status,
+                            reinterpret_cast<uint32_t*>(ctl_zero),
+                            ctl_zero ? (uint32_t)(ctl_bytes / 4) : 0u, s))
+      return fail(TLSGPU_EHIP, "bounds launch: %s", hipGetErrorString(hipGetLastError()));
+    a.descs = safe;
+  } else {
+    // records whose session is empty / invalid keep this status
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)d_status, (int)TLSGPU_REC_PUBLIC_INVALID, n, s));
+    if (ctl_zero) HIPCHK(hipMemsetAsync(ctl_zero, 0, ctl_bytes, s));
   }
   for (int rounds : {10, 14}) {
     if (!have[rounds == 10 ? TLSGPU_AES_128_GCM : TLSGPU_AES_256_GCM]) continue;

@@ -292,14 +292,22 @@ int launch_fill_synthetic_spans(uint8_t* d_out, const uint64_t* d_offs, const ui
 // from the kernels' copy of the descriptors (session 0xFFFFFFFF, which every
 // batch kernel skips) and gets TLSGPU_REC_OUT_OF_BOUNDS.  Output span = the
 // plaintext on open (fragment - explicit nonce - tag), the fragment on seal.
+// Also the batch's setup (one launch instead of three): every record's
+// initial status (TLSGPU_REC_PUBLIC_INVALID, the status of a record no kernel
+// takes, or TLSGPU_REC_OUT_OF_BOUNDS) and, from block 0, the zeroed control
+// words of the queue kernels (ctl_words uint32s, may be 0).
 __global__ void check_record_bounds(const tlsgpu_record* __restrict__ recs,
                                     tlsgpu_record* __restrict__ safe, uint32_t n,
                                     const DevSession* __restrict__ sessions, uint32_t n_sessions,
                                     uint64_t in_bytes, uint64_t out_bytes, int seal,
-                                    int32_t* __restrict__ status) {
+                                    int32_t* __restrict__ status, uint32_t* __restrict__ ctl,
+                                    uint32_t ctl_words) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.x == 0)
+    for (uint32_t w = threadIdx.x; w < ctl_words; w += blockDim.x) ctl[w] = 0;
   if (i >= n) return;
   tlsgpu_record r = recs[i];
+  int32_t st = TLSGPU_REC_PUBLIC_INVALID;
   if (r.session < n_sessions) {
     const DevSession& S = sessions[r.session];
     const uint64_t eiv = S.nonce_in_record ? 8u : 0u, tag = S.tag_len;
@@ -309,18 +317,21 @@ __global__ void check_record_bounds(const tlsgpu_record* __restrict__ recs,
     if (r.in_off > in_bytes || in_len > in_bytes - r.in_off || r.out_off > out_bytes ||
         out_len > out_bytes - r.out_off) {
       r.session = 0xFFFFFFFFu;
-      status[i] = TLSGPU_REC_OUT_OF_BOUNDS;
+      st = TLSGPU_REC_OUT_OF_BOUNDS;
     }
   }
+  status[i] = st;
   safe[i] = r;
 }
 
 int launch_check_bounds(const tlsgpu_record* recs, tlsgpu_record* safe, uint32_t n,
                         const DevSession* sessions, uint32_t n_sessions, uint64_t in_bytes,
-                        uint64_t out_bytes, bool seal, int32_t* status, hipStream_t s) {
+                        uint64_t out_bytes, bool seal, int32_t* status, uint32_t* ctl,
+                        uint32_t ctl_words, hipStream_t s) {
   if (n == 0) return 0;
   hipLaunchKernelGGL(check_record_bounds, dim3((n + 255) / 256), dim3(256), 0, s, recs, safe, n,
-                     sessions, n_sessions, in_bytes, out_bytes, seal ? 1 : 0, status);
+                     sessions, n_sessions, in_bytes, out_bytes, seal ? 1 : 0, status, ctl,
+                     ctl_words);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

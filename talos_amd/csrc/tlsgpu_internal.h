@@ -254,7 +254,8 @@ int launch_fill_synthetic(uint8_t* d_out, uint64_t stride, uint32_t span_len,
                           uint32_t n, uint64_t seed, uint64_t index0, hipStream_t s);
 int launch_check_bounds(const tlsgpu_record* recs, tlsgpu_record* safe, uint32_t n,
                         const DevSession* sessions, uint32_t n_sessions, uint64_t in_bytes,
-                        uint64_t out_bytes, bool seal, int32_t* status, hipStream_t s);
+                        uint64_t out_bytes, bool seal, int32_t* status, uint32_t* ctl,
+                        uint32_t ctl_words, hipStream_t s);
 int launch_fill_synthetic_spans(uint8_t* d_out, const uint64_t* d_offs, const uint32_t* d_lens,
                                 uint32_t n, uint64_t seed, uint64_t index0, hipStream_t s);
 // TaLoS TLS-processing hooks (talos_hooks.cpp): is a callback registered, and
