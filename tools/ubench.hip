@@ -65,9 +65,10 @@ __device__ __forceinline__ void stamp_end(Stamp* st, unsigned long long t0, unsi
 
 // ---------------------------------------------------------------------------
 // VALU issue throughput
-enum { OP_PERM, OP_BITOP3, OP_ALIGNBIT, OP_XOR, OP_MAD64, OP_ADD, OP_N };
+enum { OP_PERM, OP_BITOP3, OP_ALIGNBIT, OP_XOR, OP_MAD64, OP_ADD, OP_SDWA, OP_N };
 static const char* kOpName[OP_N] = {"v_perm_b32", "v_bitop3_b32", "v_alignbit_b32",
-                                    "v_xor_b32", "v_mad_u64_u32", "v_add_u32"};
+                                    "v_xor_b32", "v_mad_u64_u32", "v_add_u32",
+                                    "v_xor_b32_sdwa"};
 
 template <int OP>
 __global__ void valu_kernel(int iters, uint32_t k1, uint32_t k2, Stamp* st, uint32_t* out) {
@@ -100,6 +101,9 @@ __global__ void valu_kernel(int iters, uint32_t k1, uint32_t k2, Stamp* st, uint
           asm volatile("v_alignbit_b32 %0, %0, %1, 16" : "+v"(r[i]) : "v"(k1));
         else if constexpr (OP == OP_XOR)
           asm volatile("v_xor_b32 %0, %0, %1" : "+v"(r[i]) : "v"(k1));
+        else if constexpr (OP == OP_SDWA)
+          asm volatile("v_xor_b32_sdwa %0, %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE "
+                       "src0_sel:WORD_0 src1_sel:WORD_0" : "+v"(r[i]) : "v"(k1));
         else
           asm volatile("v_add_u32 %0, %0, %1" : "+v"(r[i]) : "v"(k1));
       }
@@ -450,7 +454,7 @@ static void valu(int op, int w) {
   auto launch = [&](int th, size_t lds) {
     switch (op) {
 #define L(O) case O: valu_kernel<O><<<g_cus, th, lds>>>(iters, 0x05040100u, 0x0c0d0e0fu, g_st, g_out); break;
-      L(OP_PERM) L(OP_BITOP3) L(OP_ALIGNBIT) L(OP_XOR) L(OP_MAD64) L(OP_ADD)
+      L(OP_PERM) L(OP_BITOP3) L(OP_ALIGNBIT) L(OP_XOR) L(OP_MAD64) L(OP_ADD) L(OP_SDWA)
 #undef L
     }
   };
@@ -642,6 +646,7 @@ int main(int argc, char** argv) {
        {(const void*)valu_kernel<OP_PERM>, (const void*)valu_kernel<OP_BITOP3>,
         (const void*)valu_kernel<OP_ALIGNBIT>, (const void*)valu_kernel<OP_XOR>,
         (const void*)valu_kernel<OP_MAD64>, (const void*)valu_kernel<OP_ADD>,
+        (const void*)valu_kernel<OP_SDWA>,
         (const void*)lds_b32_kernel<true, 4>, (const void*)lds_b32_kernel<true, 8>,
         (const void*)lds_b32_kernel<false, 4>, (const void*)lds_b32_kernel<false, 8>,
         (const void*)lds_b128_kernel<4>, (const void*)lds_b128_kernel<8>,
@@ -660,6 +665,7 @@ int main(int argc, char** argv) {
   for (const void* f : {(const void*)aes4t_kernel<1>, (const void*)aes4t_kernel<2>})
     CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
   if (argc > 1 && !strcmp(argv[1], "set2")) {
+    for (int w : {1, 4}) valu(OP_SDWA, w);
     set2();
     return 0;
   }
