@@ -36,22 +36,8 @@ __device__ __forceinline__ void zero_fill_lane(uint8_t* d, uint64_t n) {
   for (; o < n; o++) d[o] = 0;
 }
 
-// rotl16(a ^ b) as two full-rate SDWA xors, each writing one half of the
-// result from the other halves of a and b: v_alignbit_b32 measured ~3.7
-// cycles per wave64 instruction at 4 waves/SIMD against 2 for v_xor_b32
-// (tools/ubench.hip, profiles/r03a_ubench.jsonl), and a quarter of ChaCha's
-// rotations are by 16.
-__device__ __forceinline__ uint32_t xor_rotl16(uint32_t a, uint32_t b) {
-  uint32_t d;
-  asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_1\n\t"
-      "v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0"
-      : "=&v"(d)
-      : "v"(a), "v"(b));
-  return d;
-}
-
 #define CC_QR(a, b, c, d)            \
-  a += b; d = xor_rotl16(d, a);      \
+  a += b; d = rotl32(d ^ a, 16);     \
   c += d; b = rotl32(b ^ c, 12);     \
   a += b; d = rotl32(d ^ a, 8);      \
   c += d; b = rotl32(b ^ c, 7);
