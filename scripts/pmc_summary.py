@@ -26,9 +26,19 @@ for f in sorted(glob.glob(os.path.join(run, "pmc*", "pmc_kernel_trace.csv"))):
         if r["Kernel_Name"].startswith(prefix):
             durs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 mean = {k: sum(v) / len(v) for k, v in vals.items()}
+# the bench line each profiled pass printed (same process as its PMC and kernel trace)
+bench = []
+for f in sorted(glob.glob(os.path.join(run, "pmc*.log"))):
+    for line in open(f):
+        if line.startswith("{") and '"ms_per_step"' in line:
+            d = json.loads(line)
+            bench.append({"pass": os.path.basename(f), "value": d["value"],
+                          "ms_per_step": d["ms_per_step"]})
 res = {"kernel": prefix, "label": label, "launches_sampled": len(durs),
        "mean_duration_ns_profiled": sum(durs) / len(durs) if durs else None,
-       "counters_per_launch_mean": mean}
+       "counters_per_launch_mean": mean, "bench_lines_of_these_passes": bench}
+if durs and bench:  # the main kernel must fit in the step it was timed in
+    res["kernel_ms_le_step_ms"] = all(sum(durs) / len(durs) / 1e6 <= b["ms_per_step"] for b in bench)
 if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
     res["hbm_read_bytes_per_launch"] = mean["FETCH_SIZE"] * 1024 * 2
     res["hbm_write_bytes_per_launch"] = mean["WRITE_SIZE"] * 1024
