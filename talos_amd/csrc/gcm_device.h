@@ -60,9 +60,15 @@ __device__ __forceinline__ uint4 lds_u128(uint32_t off) {
 // The lane's T-table operand: its bank offset (lane % 32) * 4 in byte 0 and
 // the table base AES_OFF >> 16 in byte 2.
 __device__ __forceinline__ uint32_t aes_laneoff(uint32_t lane) { return ((lane & 31) * 4) | AES_OFF; }
-// address of Te0[byte r of w] for this lane: [0, AES_OFF >> 16, byte, lane bank]
+// address of Te0[byte r of w] for this lane: [0, AES_OFF >> 16, byte, lane bank].
+// Byte 1 already sits where the address wants it: (w & 0xFF00) | laneoff in one
+// full-rate v_bitop3_b32 (truth table 0xEA = (a & b) | c) instead of a
+// v_perm_b32, which measured 3.4 cycles per wave64 instruction at 4 waves/SIMD
+// against 2.1 (tools/ubench.hip); VALU issue adds to the T-table waves' LDS
+// lookup time nearly 1:1 (profiles/r03b_ubench_set2.jsonl).
 template <int R>
 __device__ __forceinline__ uint32_t taddr(uint32_t w, uint32_t laneoff) {
+  if constexpr (R == 1) return __builtin_amdgcn_bitop3_b32(w, 0xFF00u, laneoff, 0xEA);
   return __builtin_amdgcn_perm(w, laneoff, 0x0C020000u | ((4u + R) << 8));
 }
 __device__ __forceinline__ uint32_t rotl16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
