@@ -224,6 +224,9 @@ def main():
                     help="deal records to sessions round-robin (a many-connection server "
                          "batch) instead of grouping each session's records")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-hints", action="store_true",
+                    help="do not state the batch-shape hints (tlsgpu_sessions_hint) the "
+                         "workload's lengths and session order imply")
     ap.add_argument("--host-streams", type=int, default=0, help="host mode: pipeline streams")
     ap.add_argument("--host-chunk-mib", type=int, default=0, help="host mode: chunk size")
     ap.add_argument("--mode", default="device", choices=["device", "host", "wire", "copy", "pcie"],
@@ -273,6 +276,12 @@ def main():
                   tamper_every=1024 if op == "open" and args.mode != "wire" else 0,
                   interleave=args.interleave, shard=(lo, hi))
     total_len = int(wl.lengths.sum())
+    # what the caller that built the batch knows about its shape (no short GCM
+    # records / long session runs): the engine then skips the launches of the
+    # kernel variants the device would not select (tlsgpu.h tlsgpu_sessions_hint)
+    hints = 0 if args.no_hints else ta.batch_hints(wl.lengths, wl.session, seal=op != "open")
+    wl.table.hint(hints)
+    args.hints = hints
     if args.mode == "host":
         return host_mode(args, eng, wl, kind_name, total_len)
     if args.mode == "wire":
@@ -369,6 +378,7 @@ def main():
                    "records_per_gpu": per_gpu, "sessions_per_gpu": sessions,
                    "session_order": "interleaved" if args.interleave else "grouped",
                    "gcm_impl": ta.get_gcm_impl() if "gcm" in kind_name else None,
+                   "batch_hints": args.hints,
                    "payload_bytes_per_gpu": total_len, "parallelism": f"batch split x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -138,6 +138,25 @@ int tlsgpu_seal_batch(tlsgpu_sessions *t, const tlsgpu_record *d_recs, uint32_t 
     const uint8_t *d_in, size_t in_bytes, uint8_t *d_out, size_t out_bytes, int32_t *d_status,
     void *stream);
 
+/* Batch-shape hints for the AES-GCM batch calls of this session table
+ * (performance only: results never depend on them, any batch stays correct).
+ * The default kernel selection happens on the device, so every GCM batch
+ * dispatches the long-record kernel, its short-record-pack variant and the
+ * per-wave-session kernel, and the two not selected exit at once (~5 us each).
+ * A caller that knows its batches rules them out:
+ *   TLSGPU_HINT_NO_SHORT_RECORDS  no GCM record of <= 62 blocks (open: length
+ *                                 <= 1,016 B with the 8-B explicit nonce and a
+ *                                 16-B tag): the pack variant is not launched;
+ *   TLSGPU_HINT_SESSION_RUNS      records come in session runs of >= 12
+ *                                 records on average: the per-wave-session
+ *                                 kernel is not launched.
+ * A wrong hint costs speed only (short records then take the long-record
+ * path, short runs the run-at-a-time queue).  tlsgpu_open_host /
+ * tlsgpu_seal_host derive the hints from the host descriptors themselves. */
+#define TLSGPU_HINT_NO_SHORT_RECORDS 1u
+#define TLSGPU_HINT_SESSION_RUNS 2u
+int tlsgpu_sessions_hint(tlsgpu_sessions *t, unsigned hints);
+
 /* ---------------------------------------------------------------------------
  * Host-resident batch open: records that start and end in
  * host memory, as socket buffers do.  Replaces, for a batch of connections,

@@ -11,7 +11,8 @@ cd /tmp && export TMPDIR=/tmp
 i=0
 for grp in "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
-           "FETCH_SIZE" "WRITE_SIZE" ${EXTRA_GROUPS}; do
+           "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" \
+           "TCC_EA0_RDREQ_32B_sum TCC_EA0_WRREQ_64B_sum" ${EXTRA_GROUPS}; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $O/pmc$i -o pmc -- \
     python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > $O/pmc$i.log 2>&1

@@ -44,5 +44,14 @@ if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
     res["hbm_write_bytes_per_launch"] = mean["WRITE_SIZE"] * 1024
     res["hbm_bytes_per_launch"] = res["hbm_read_bytes_per_launch"] + res["hbm_write_bytes_per_launch"]
     res["correction"] = "FETCH_SIZE x2 (gfx950 half-count of wide streaming reads), KB x1024"
+# calibrated read bytes: the L2's memory-side read requests by size (the
+# FETCH_SIZE x2 rule holds for 128-B requests only; partial-line accesses
+# issue 64-B and 32-B requests)
+if "TCC_EA0_RDREQ_128B_sum" in mean and "TCC_EA0_RDREQ_64B_sum" in mean:
+    rd = (128 * mean["TCC_EA0_RDREQ_128B_sum"] + 64 * mean["TCC_EA0_RDREQ_64B_sum"] +
+          32 * mean.get("TCC_EA0_RDREQ_32B_sum", 0.0))
+    res["hbm_read_bytes_per_launch_by_request_size"] = rd
+    if "WRITE_SIZE" in mean:
+        res["hbm_bytes_per_launch_by_request_size"] = rd + mean["WRITE_SIZE"] * 1024
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))

@@ -126,6 +126,7 @@ def load_library(path: str = LIBPATH) -> C.CDLL:
         "tlsgpu_sessions_create": (i32, [vp, u32, C.POINTER(vp)]),
         "tlsgpu_sessions_destroy": (None, [vp]),
         "tlsgpu_sessions_install": (i32, [vp, u32, u32, vp]),
+        "tlsgpu_sessions_hint": (i32, [vp, u32]),
         "tlsgpu_open_batch": (i32, [vp, vp, u32, vp, C.c_size_t, vp, C.c_size_t, vp, vp]),
         "tlsgpu_seal_batch": (i32, [vp, vp, u32, vp, C.c_size_t, vp, C.c_size_t, vp, vp]),
         "tlsgpu_fill_synthetic": (i32, [vp, vp, u64, u32, u32, u64, u64, vp]),
@@ -361,10 +362,33 @@ class SessionTable:
         _check(self.lib.tlsgpu_sessions_install(self.handle, first, len(params), arr),
                "tlsgpu_sessions_install")
 
+    def hint(self, hints: int) -> None:
+        """Batch-shape hints (tlsgpu_sessions_hint): HINT_NO_SHORT_RECORDS,
+        HINT_SESSION_RUNS; performance only."""
+        _check(self.lib.tlsgpu_sessions_hint(self.handle, hints), "tlsgpu_sessions_hint")
+
     def close(self) -> None:
         if self.handle:
             self.lib.tlsgpu_sessions_destroy(self.handle)
             self.handle = None
+
+
+HINT_NO_SHORT_RECORDS, HINT_SESSION_RUNS = 1, 2
+
+
+def batch_hints(lengths, sessions, seal: bool) -> int:
+    """The hints a caller that built the batch can state (tlsgpu.h): no GCM
+    record short enough for a pack, session runs of >= 12 records on average."""
+    lengths = np.asarray(lengths)
+    sessions = np.asarray(sessions)
+    short_max = 992 if seal else 992 + 8 + 16
+    h = 0
+    if len(lengths) and int(lengths.min()) > short_max:
+        h |= HINT_NO_SHORT_RECORDS
+    runs = 1 + int(np.count_nonzero(sessions[1:] != sessions[:-1])) if len(sessions) else 0
+    if runs * 12 <= len(sessions):
+        h |= HINT_SESSION_RUNS
+    return h
 
 
 GCM_BITSLICE, GCM_TTABLE, GCM_HYBRID, GCM_QUEUE, GCM_FUSED, GCM_SPLIT, GCM_AUTO = 0, 1, 2, 3, 4, 5, 6

@@ -290,15 +290,24 @@ __device__ void cc_record(const CcRec& rc, uint32_t tag_len, int32_t* status_slo
 // data moves in 128-B steps through a per-wave LDS tile of 64 rows: lane l
 // serves pieces of records 8k + l/8 (k = 0..7), so each load/store instruction
 // covers 8 records x 128 contiguous bytes; each lane then en/decrypts and MACs
-// its own record's row.  Rows are padded to 144 B so the row-wise ds_read_b128
-// of the 64 lanes (same column, different rows) is bank-conflict-free.
-// 128 B per record per step (64-B steps fit 4 waves/SIMD at 124 VGPRs but
-// measured 535 vs 570 GiB/s on config C: twice the LDS syncs per byte)
+// its own record's row.  Rows are 128 B with no padding: the 16-B pieces of
+// row r are stored rotated by r/2 (cc_slot), so the row-wise ds_read_b128 of
+// the 64 lanes (same piece, different rows) is bank-conflict-free while the
+// gather/scatter still write and read each 1 KiB slot group contiguously.
+// Register budget (round 3): the ChaCha key words sit in LDS (read per block),
+// the record's tag/status fields are re-derived at the end, so the kernel fits
+// 128 VGPRs = 4 waves per SIMD (round 2: 146 VGPRs, 3 waves per SIMD).
 constexpr uint32_t kCcStep = 128;
-constexpr uint32_t kCcRow = kCcStep + 16;
 constexpr int kCcP = kCcStep / 16;           // 16-B pieces of a record per step = loads per lane
 constexpr int kCcR = kWave / kCcP;           // records covered by one load instruction
 constexpr int kCcThreads = 256;
+constexpr uint32_t kCcTile = kWave * kCcStep;  // 8 KiB of rows per wave
+constexpr uint32_t kCcKeys = kWave * 32;       // the lanes' ChaCha keys, 2 KiB per wave
+
+// tile offset of piece q (0..7) of row r
+__device__ __forceinline__ uint32_t cc_slot(uint32_t r, uint32_t q) {
+  return r * kCcStep + (((q + (r >> 1)) & 7u) << 4);
+}
 
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
   const uint32_t lo = __shfl((uint32_t)v, (int)src), hi = __shfl((uint32_t)(v >> 32), (int)src);
@@ -309,57 +318,113 @@ __device__ __forceinline__ void lds_wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-template <bool SEAL>
-__device__ void cc_record_staged(const CcRec& rc, bool active, uint32_t tag_len,
-                                 int32_t* status_slot, uint32_t lane, uint8_t* tile) {
-  uint32_t st[16], ks[16];
+// ChaCha20 block (chacha-merged.c:113-270) with the key words read from LDS
+// at the start and again for the feed-forward (not held across the rounds).
+__device__ __forceinline__ void cc_block_lds(uint32_t x[16], const uint8_t* key, uint32_t c12,
+                                             uint32_t c13, uint32_t c14, uint32_t c15) {
+  const volatile u32x4* kp = reinterpret_cast<const volatile u32x4*>(key);
+  {
+    const u32x4 ka = kp[0], kb = kp[kWave];
+    x[0] = 0x61707865u; x[1] = 0x3320646eu; x[2] = 0x79622d32u; x[3] = 0x6b206574u;
+    x[4] = ka.x; x[5] = ka.y; x[6] = ka.z; x[7] = ka.w;
+    x[8] = kb.x; x[9] = kb.y; x[10] = kb.z; x[11] = kb.w;
+    x[12] = c12; x[13] = c13; x[14] = c14; x[15] = c15;
+  }
 #pragma unroll
-  for (int i = 0; i < 16; i++) st[i] = rc.st[i];
-  Poly p;
-  PolyStream ps = {{0, 0, 0, 0}, 0};
-  const uint32_t n = active ? rc.n : 0u;
-  if (active) {
-    chacha_block(st, ks);  // counter 0 block -> one-time Poly1305 key
-    poly_init(p, ks);
-    if (!rc.old) {
-      poly_block(p, rc.ad[0], rc.ad[1], rc.ad[2], rc.ad[3], 1u << 24);  // 13-B AD, pad16
-    } else {
-      for (uint32_t o = 0; o < rc.ad_len; o++) ps_byte(p, ps, (rc.ad[o >> 2] >> (8 * (o & 3))) & 0xFF);
-      ps_u64(p, ps, rc.ad_len);
+  for (int i = 0; i < 10; i++) {
+    CC_QR(x[0], x[4], x[8], x[12]);
+    CC_QR(x[1], x[5], x[9], x[13]);
+    CC_QR(x[2], x[6], x[10], x[14]);
+    CC_QR(x[3], x[7], x[11], x[15]);
+    CC_QR(x[0], x[5], x[10], x[15]);
+    CC_QR(x[1], x[6], x[11], x[12]);
+    CC_QR(x[2], x[7], x[8], x[13]);
+    CC_QR(x[3], x[4], x[9], x[14]);
+  }
+  const u32x4 ka = kp[0], kb = kp[kWave];
+  x[0] += 0x61707865u; x[1] += 0x3320646eu; x[2] += 0x79622d32u; x[3] += 0x6b206574u;
+  x[4] += ka.x; x[5] += ka.y; x[6] += ka.z; x[7] += ka.w;
+  x[8] += kb.x; x[9] += kb.y; x[10] += kb.z; x[11] += kb.w;
+  x[12] += c12; x[13] += c13; x[14] += c14; x[15] += c15;
+}
+
+// One wave: records r = (first record of the wave) + lane, one per lane
+// (t1_enc.c:832-975 for the ChaCha suites, e_chacha20poly1305.c:124-286).
+template <bool SEAL>
+__device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8_t* tile,
+                            uint8_t* keys) {
+  // --- parse (the fields the end of the record needs are re-derived there)
+  bool active = false;
+  uint32_t n = 0, tag_len = 16, c13 = 0, c14 = 0, c15 = 0;
+  uint32_t ad2 = 0;  // AD word 2 (type, version, length high byte); words 0-1 = c14/c15 (RFC)
+  const uint8_t* src = nullptr;
+  uint8_t* dst = nullptr;
+  uint32_t sq_hi = 0, sq_lo = 0;
+  if (r < a.n) {
+    const tlsgpu_record d = reinterpret_cast<const tlsgpu_record*>(a.descs)[r];
+    if (d.session < a.n_sessions) {  // else the status stays PUBLIC_INVALID
+      const DevSession* S = a.sessions + d.session;
+      const uint32_t kind = S->kind;
+      if (kind == TLSGPU_CHACHA20_POLY1305) {  // the draft ("old") suite: chacha_batch_kernel
+        tag_len = S->tag_len;
+        const uint32_t len = d.len_type & 0xFFFFFFu, type = d.len_type >> 24;
+        if (!SEAL && len < tag_len) {  // t1_enc.c:958-959 (no explicit nonce for ChaCha)
+          a.status[r] = TLSGPU_REC_PUBLIC_INVALID;
+        } else {
+          active = true;
+          n = SEAL ? len : len - tag_len;
+          src = a.in + d.in_off;
+          dst = a.out + d.out_off;
+          // nonce: RFC 7905 fixed(12) XOR (0^4 || seq)
+          sq_hi = bswap32((uint32_t)(d.seq >> 32));
+          sq_lo = bswap32((uint32_t)d.seq);
+          const uint32_t* fx = reinterpret_cast<const uint32_t*>(S->fixed_nonce);
+          c13 = fx[0];
+          c14 = fx[1] ^ sq_hi;
+          c15 = fx[2] ^ sq_lo;
+          const uint32_t v = S->version;
+          ad2 = type | (((v >> 8) & 0xFF) << 8) | ((v & 0xFF) << 16) | (((n >> 8) & 0xFF) << 24);
+          const uint4* kw = reinterpret_cast<const uint4*>(S->chacha_key);
+          reinterpret_cast<uint4*>(keys)[lane] = kw[0];
+          reinterpret_cast<uint4*>(keys)[kWave + lane] = kw[1];
+        }
+      }
     }
   }
-  // pieces this lane moves: records 8k + lane/8, bytes 16 (lane % 8) of each
-  // step; the records' pointers and lengths are fetched with ds_bpermute per
-  // step (keeping 8 x 5 of them in VGPRs would cost a wave per SIMD)
-  const uint32_t piece = 16u * (lane % kCcP);
+  uint8_t* key = keys + 16u * lane;
+  lds_wave_sync();
+  Poly p;
+  if (active) {
+    uint32_t ks[16];
+    cc_block_lds(ks, key, 0u, c13, c14, c15);  // counter 0 block -> one-time Poly1305 key
+    poly_init(p, ks);
+    poly_block(p, sq_hi, sq_lo, ad2, n & 0xFF, 1u << 24);  // 13-B AD, pad16
+  }
+  // pieces this lane moves: records 8k + lane/8, piece (lane % 8 - record/2) % 8
+  // of each step; the records' pointers and lengths are fetched with ds_bpermute
+  // per step (keeping 8 x 5 of them in VGPRs would cost a wave per SIMD)
   uint32_t steps = (n + kCcStep - 1) / kCcStep;
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) steps = max(steps, (uint32_t)__shfl_xor((int)steps, m));
-  uint8_t* myrow = tile + lane * kCcRow;
-  uint64_t ctr = ((uint64_t)st[13] << 32) | st[12];
+  uint32_t ctr = 0;
   // gather of step s: 8 records x 128 B per load instruction, into registers
   // (issued one step ahead, so the loads fly during the previous step's math)
   auto gather = [&](uint32_t base, uint4 (&v)[kCcP]) {
 #pragma unroll
     for (int k = 0; k < kCcP; k++) {
-      const uint32_t off = base + piece;
       const uint32_t rr = kCcR * k + lane / kCcP;
+      const uint32_t off = base + 16u * (((lane % kCcP) - (rr >> 1)) & 7u);
       const uint32_t snk = __shfl(n, (int)rr);
       // ds_bpermute outside the branch: an inactive source lane reads as 0
-      const uint64_t srck = shfl64((uint64_t)(uintptr_t)rc.src, rr);
+      const uint64_t srck = shfl64((uint64_t)(uintptr_t)src, rr);
       v[k] = make_uint4(0, 0, 0, 0);
       if (off < snk) {
-        const uint8_t* src = (const uint8_t*)(uintptr_t)srck + off;
-        if (off + 16 <= snk && ((uintptr_t)src & 15) == 0) {
-          v[k] = gload16(src);
-        } else if (off + 16 <= snk) {  // wire fragments: misaligned full piece
+        const uint8_t* sp = (const uint8_t*)(uintptr_t)srck + off;
+        if (((uintptr_t)sp & 15) == 0) {
+          v[k] = gload16(sp);  // full or last piece: an aligned 16 B never crosses a page
+        } else {  // wire fragments (misaligned): only dwords that hold a record byte
           uint32_t w[4];
-          load16_any(src, w);
-          v[k] = make_uint4(w[0], w[1], w[2], w[3]);
-        } else {
-          uint32_t w[4] = {0, 0, 0, 0};
-          const uint32_t nb = min(16u, snk - off);
-          for (uint32_t b = 0; b < nb; b++) w[b >> 2] |= (uint32_t)gld<uint8_t>(src)[b] << (8 * (b & 3));
+          load16_upto(sp, min(16u, snk - off), w);
           v[k] = make_uint4(w[0], w[1], w[2], w[3]);
         }
       }
@@ -371,25 +436,25 @@ __device__ void cc_record_staged(const CcRec& rc, bool active, uint32_t tag_len,
     const uint32_t base = s * kCcStep;
 #pragma unroll
     for (int k = 0; k < kCcP; k++)
-      *reinterpret_cast<uint4*>(tile + (kCcR * k + lane / kCcP) * kCcRow + piece) = pf[k];
+      *reinterpret_cast<uint4*>(tile + 1024u * k + 16u * lane) = pf[k];
     if (s + 1 < steps) gather(base + kCcStep, pf);
     lds_wave_sync();
     // en/decrypt + MAC this lane's row: 2 ChaCha blocks
     if (base < n) {
-#pragma unroll
+#pragma unroll 1
       for (int h = 0; h < (int)(kCcStep / 64); h++) {
         const uint32_t o64 = base + 64u * h;
         if (o64 >= n) break;
-        ctr += 1;
-        st[12] = (uint32_t)ctr;
-        st[13] = (uint32_t)(ctr >> 32);
-        chacha_block(st, ks);
+        ctr += 1;  // data blocks count from 1 (chacha-merged.c:230-236; TLS records < 2^32 blocks)
+        uint32_t ks[16];
+        cc_block_lds(ks, key, ctr, c13, c14, c15);
 #pragma unroll
         for (int q = 0; q < 4; q++) {
           const uint32_t o = o64 + 16 * q;
           if (o >= n) break;
           const uint32_t nb = min(16u, n - o);
-          const uint4 t = *reinterpret_cast<const uint4*>(myrow + 64 * h + 16 * q);
+          uint4* slot = reinterpret_cast<uint4*>(tile + cc_slot(lane, 4 * h + q));
+          const uint4 t = *slot;
           uint32_t in[4] = {t.x, t.y, t.z, t.w};
           uint32_t ob[4] = {in[0] ^ ks[4 * q], in[1] ^ ks[4 * q + 1], in[2] ^ ks[4 * q + 2],
                             in[3] ^ ks[4 * q + 3]};
@@ -402,13 +467,9 @@ __device__ void cc_record_staged(const CcRec& rc, bool active, uint32_t tag_len,
               in[w] &= keep;
             }
           }
-          *reinterpret_cast<uint4*>(myrow + 64 * h + 16 * q) = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+          *slot = make_uint4(ob[0], ob[1], ob[2], ob[3]);
           const uint32_t* c = SEAL ? ob : in;
-          if (!rc.old) {
-            poly_block(p, c[0], c[1], c[2], c[3], 1u << 24);
-          } else {
-            for (uint32_t k = 0; k < nb; k++) ps_byte(p, ps, (c[k >> 2] >> (8 * (k & 3))) & 0xFF);
-          }
+          poly_block(p, c[0], c[1], c[2], c[3], 1u << 24);
         }
       }
     }
@@ -416,48 +477,45 @@ __device__ void cc_record_staged(const CcRec& rc, bool active, uint32_t tag_len,
     // scatter
 #pragma unroll
     for (int k = 0; k < kCcP; k++) {
-      const uint32_t off = base + piece;
       const uint32_t rr = kCcR * k + lane / kCcP;
+      const uint32_t off = base + 16u * (((lane % kCcP) - (rr >> 1)) & 7u);
       const uint32_t snk = __shfl(n, (int)rr);
-      const uint64_t dstk = shfl64((uint64_t)(uintptr_t)rc.dst, rr);
+      const uint64_t dstk = shfl64((uint64_t)(uintptr_t)dst, rr);
       if (off < snk) {
-        uint8_t* dst = (uint8_t*)(uintptr_t)dstk + off;
-        const uint4 v = *reinterpret_cast<const uint4*>(tile + rr * kCcRow + piece);
-        if (off + 16 <= snk && ((uintptr_t)dst & 15) == 0) {
-          gstore16(dst, v);
+        uint8_t* dp = (uint8_t*)(uintptr_t)dstk + off;
+        const uint4 v = *reinterpret_cast<const uint4*>(tile + 1024u * k + 16u * lane);
+        if (off + 16 <= snk && ((uintptr_t)dp & 15) == 0) {
+          gstore16(dp, v);
         } else if (off + 16 <= snk) {
           const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-          store16_any(dst, w);
+          store16_any(dp, w);
         } else {
           const uint32_t w[4] = {v.x, v.y, v.z, v.w};
           const uint32_t nb = min(16u, snk - off);
-          for (uint32_t b = 0; b < nb; b++) gst<uint8_t>(dst)[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+          for (uint32_t b = 0; b < nb; b++) gst<uint8_t>(dp)[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
         }
       }
     }
     lds_wave_sync();
   }
   if (!active) return;
-  if (!rc.old) {
-    poly_block(p, rc.ad_len, 0, n, 0, 1u << 24);  // le64(ad_len) || le64(ct_len)
-  } else {
-    ps_u64(p, ps, n);
-    ps_final(p, ps);
-  }
+  poly_block(p, 13u, 0, n, 0, 1u << 24);  // le64(ad_len) || le64(ct_len)
   uint32_t mac[4];
   poly_finish(p, mac);
+  int32_t* slot = a.status + r;
   if (SEAL) {
-    for (uint32_t k = 0; k < tag_len; k++) rc.tag_out[k] = (uint8_t)(mac[k >> 2] >> (8 * (k & 3)));
-    *status_slot = rc.ok_status;
+    uint8_t* tag_out = dst + n;
+    for (uint32_t k = 0; k < tag_len; k++) tag_out[k] = (uint8_t)(mac[k >> 2] >> (8 * (k & 3)));
+    *slot = (int32_t)(n + tag_len);
   } else {
+    const uint8_t* tag_in = src + n;
     uint32_t diff = 0;
-    for (uint32_t k = 0; k < tag_len; k++)
-      diff |= rc.tag_in[k] ^ ((mac[k >> 2] >> (8 * (k & 3))) & 0xFF);
+    for (uint32_t k = 0; k < tag_len; k++) diff |= tag_in[k] ^ ((mac[k >> 2] >> (8 * (k & 3))) & 0xFF);
     if (diff) {
-      zero_fill_lane(rc.dst, rc.zero_len);
-      *status_slot = TLSGPU_REC_BAD_MAC;
+      zero_fill_lane(dst, n);
+      *slot = TLSGPU_REC_BAD_MAC;
     } else {
-      *status_slot = rc.ok_status;
+      *slot = (int32_t)n;
     }
   }
 }
@@ -530,23 +588,19 @@ __device__ __forceinline__ bool cc_parse_tls(const BatchArgs& a, uint32_t r, CcR
   return true;
 }
 
-// TLS batches: LDS-staged coalesced data path (cc_record_staged).
+// TLS batches: LDS-staged coalesced data path (cc_tls_wave), 4 waves per SIMD.
 template <bool SEAL>
 __global__ __launch_bounds__(kCcThreads) void chacha_tls_kernel(BatchArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t tiles[kCcThreads / kWave][kWave * kCcRow];
+  __shared__ __attribute__((aligned(16))) uint8_t tiles[kCcThreads / kWave][kCcTile];
+  __shared__ __attribute__((aligned(16))) uint8_t keys[kCcThreads / kWave][kCcKeys];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  CcRec rc;
-  rc.src = nullptr;
-  rc.dst = nullptr;
-  rc.n = 0;
-  rc.old = false;
-  uint32_t tag_len = 16;
-  const bool active = r < a.n && cc_parse_tls<SEAL>(a, r, rc, tag_len);
-  cc_record_staged<SEAL>(rc, active, tag_len, a.status + (active ? r : 0), lane, tiles[wave]);
+  cc_tls_wave<SEAL>(a, blockIdx.x * blockDim.x + threadIdx.x, lane, tiles[wave], keys[wave]);
 }
 
-template <bool SEAL, bool RAW>
+// Per-lane data path: raw EVP jobs, TLS records of the draft suite (OLD_ONLY:
+// beside chacha_tls_kernel, which takes the RFC 7905 suite), and
+// TLSGPU_CHACHA_LEGACY=1 TLS batches.
+template <bool SEAL, bool RAW, bool OLD_ONLY = false>
 __global__ __launch_bounds__(256) void chacha_batch_kernel(BatchArgs a) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= a.n) return;
@@ -589,6 +643,11 @@ __global__ __launch_bounds__(256) void chacha_batch_kernel(BatchArgs a) {
     }
     rc.zero_len = j.max_out;
   } else {
+    if (OLD_ONLY) {  // the staged kernel leaves these records' statuses alone
+      const tlsgpu_record d = reinterpret_cast<const tlsgpu_record*>(a.descs)[r];
+      if (d.session >= a.n_sessions || a.sessions[d.session].kind != TLSGPU_CHACHA20_POLY1305_OLD)
+        return;
+    }
     if (!cc_parse_tls<SEAL>(a, r, rc, tag_len)) return;
   }
   cc_record<SEAL>(rc, tag_len, slot);
@@ -604,19 +663,28 @@ static bool getenv_legacy_chacha() {
   return v;
 }
 
-int launch_chacha(const BatchArgs& a, bool seal, bool raw, int groups, hipStream_t s) {
-  (void)groups;
+// rfc / old: the batch may hold records of the RFC 7905 / draft suite.
+int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, hipStream_t s) {
   if (a.n == 0) return 0;
   dim3 grid((a.n + 255) / 256), block(256);
   const bool staged = !raw && !getenv_legacy_chacha();
-  if (seal) {
-    if (raw) hipLaunchKernelGGL((chacha_batch_kernel<true, true>), grid, block, 0, s, a);
-    else if (staged) hipLaunchKernelGGL((chacha_tls_kernel<true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((chacha_batch_kernel<true, false>), grid, block, 0, s, a);
-  } else {
-    if (raw) hipLaunchKernelGGL((chacha_batch_kernel<false, true>), grid, block, 0, s, a);
-    else if (staged) hipLaunchKernelGGL((chacha_tls_kernel<false>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((chacha_batch_kernel<false, false>), grid, block, 0, s, a);
+  if (raw || !staged) {
+    if (seal) {
+      if (raw) hipLaunchKernelGGL((chacha_batch_kernel<true, true>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((chacha_batch_kernel<true, false>), grid, block, 0, s, a);
+    } else {
+      if (raw) hipLaunchKernelGGL((chacha_batch_kernel<false, true>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((chacha_batch_kernel<false, false>), grid, block, 0, s, a);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+  if (rfc) {
+    if (seal) hipLaunchKernelGGL((chacha_tls_kernel<true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((chacha_tls_kernel<false>), grid, block, 0, s, a);
+  }
+  if (old) {
+    if (seal) hipLaunchKernelGGL((chacha_batch_kernel<true, false, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((chacha_batch_kernel<false, false, true>), grid, block, 0, s, a);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

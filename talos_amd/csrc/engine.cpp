@@ -135,6 +135,7 @@ struct tlsgpu_sessions {
   std::vector<uint8_t> tag_lens;  // and tag lengths (host pipeline output spans)
   std::vector<const void*> owners;  // SSL* per session for the TaLoS hooks (set_owner)
   bool have[5];                // any session of kind k installed
+  std::atomic<unsigned> hints{0};  // TLSGPU_HINT_* (tlsgpu_sessions_hint)
   std::mutex mu;               // host mirrors, when several threads install at once
 };
 
@@ -413,7 +414,9 @@ struct Bounds {
 // passes the kinds its jobs use).
 static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const uint8_t* d_in,
                      uint8_t* d_out, int32_t* d_status, hipStream_t s, bool seal, bool raw,
-                     const Bounds* bounds = nullptr, unsigned kinds = ~0u) {
+                     const Bounds* bounds = nullptr, unsigned kinds = ~0u,
+                     unsigned hints = ~0u) {
+  if (hints == ~0u) hints = t->hints.load(std::memory_order_relaxed);
   bool have[5];
   for (int k = 0; k < 5; k++) have[k] = t->have[k] && ((kinds >> k) & 1u);
   BatchArgs a = {};
@@ -429,8 +432,10 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
 
   a.dbg = g_phase_stats;
   a.bs16_min = g_bs16_min;
-  a.pack = g_pack;
-  a.pws = g_pws;
+  // batch-shape hints rule out the kernels the device would not select
+  // (tlsgpu_sessions_hint); the TLSGPU_PACK / TLSGPU_PWS overrides win
+  a.pack = (hints & TLSGPU_HINT_NO_SHORT_RECORDS) ? 0u : g_pack;
+  a.pws = (g_pws == 0 && (hints & TLSGPU_HINT_SESSION_RUNS)) ? 1u : g_pws;
   int groups = groups_for(t->eng, n, &a.records_per_group);
   const int sel_impl = g_gcm_impl.load();
   // small TLS batches (at most two records per CU): one record per workgroup,
@@ -533,9 +538,17 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
     }
   }
   if ((have[TLSGPU_CHACHA20_POLY1305] || have[TLSGPU_CHACHA20_POLY1305_OLD]) &&
-      launch_chacha(a, seal, raw, groups, s))
+      launch_chacha(a, seal, raw, have[TLSGPU_CHACHA20_POLY1305],
+                    have[TLSGPU_CHACHA20_POLY1305_OLD], s))
     return fail(TLSGPU_EHIP, "chacha launch: %s", hipGetErrorString(hipGetLastError()));
   if (pool_scratch) HIPCHK(hipFreeAsync(pool_scratch, s));
+  return TLSGPU_OK;
+}
+
+extern "C" int tlsgpu_sessions_hint(tlsgpu_sessions* t, unsigned hints) {
+  if (!t || (hints & ~(TLSGPU_HINT_NO_SHORT_RECORDS | TLSGPU_HINT_SESSION_RUNS)))
+    return fail(TLSGPU_EINVAL, "bad arguments");
+  t->hints.store(hints, std::memory_order_relaxed);
   return TLSGPU_OK;
 }
 
@@ -593,6 +606,22 @@ static const long g_host_fail_chunk = [] {
 // tlsgpu_seal_host).  Open: in = record fragments, out = plaintext; seal: in =
 // plaintext, out = fragments.  The TaLoS plaintext hooks run on the host
 // plaintext: after the batch for reads, before its first copy for writes.
+// The batch-shape hints of a host-resident slice (tlsgpu_sessions_hint): no
+// record short enough for a pack (GCM n <= 992 B, the open length with the
+// explicit nonce and the longest tag), and session runs long enough for the
+// run-at-a-time queue kernel (pws_selected: runs * kPwsRun <= records).
+static unsigned host_hints(const tlsgpu_record* r, uint32_t n, bool seal) {
+  const uint32_t short_max = seal ? 992u : 992u + 8u + 16u;
+  bool shorts = false;
+  uint32_t runs = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    shorts |= (r[i].len_type & 0xFFFFFFu) <= short_max;
+    runs += (i == 0 || r[i].session != r[i - 1].session) ? 1u : 0u;
+  }
+  return (shorts ? 0u : TLSGPU_HINT_NO_SHORT_RECORDS) |
+         ((uint64_t)runs * kPwsRun <= n ? TLSGPU_HINT_SESSION_RUNS : 0u);
+}
+
 static int host_batch(tlsgpu_sessions* t, bool seal, const tlsgpu_record* h_recs, uint32_t n,
                       const uint8_t* h_in, size_t in_bytes, uint8_t* h_out, size_t out_bytes,
                       int32_t* h_status) {
@@ -729,7 +758,7 @@ static int host_batch(tlsgpu_sessions* t, bool seal, const tlsgpu_record* h_recs
       if (!in_place && ohi > olo) HIPCHK(hipMemsetAsync(d_out + olo, 0, ohi - olo, hs));
       const Bounds bd = {in_bytes, out_bytes};
       const int rc = run_batch(t, hp.d_recs + a, b - a, d_in, d_out, hp.d_status + a, hs, seal,
-                               false, &bd);
+                               false, &bd, ~0u, host_hints(h_recs + a, b - a, seal));
       if (rc != TLSGPU_OK) return rc;
       HIPCHK(hipEventRecord(ev_done, hs));
       HIPCHK(hipStreamWaitEvent(s_out, ev_done, 0));
@@ -1537,7 +1566,7 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
   a.n_sessions = st->sess->capacity;
   const bool gcm = st->kind == TLSGPU_AES_128_GCM || st->kind == TLSGPU_AES_256_GCM;
   int rc = gcm ? launch_gcm(a, seal, true, st->kind == TLSGPU_AES_128_GCM ? 10 : 14, 1, s)
-               : launch_chacha(a, seal, true, 1, s);
+               : launch_chacha(a, seal, true, true, true, s);
   if (rc) return -1;
   // success writes at most in_len + tag (seal) / in_len - tag (open) bytes
   const size_t back = seal ? in_len + st->tag_len : std::min(max_out_len, in_len);

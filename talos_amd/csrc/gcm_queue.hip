@@ -38,7 +38,7 @@ int launch_gcm_queue(const BatchArgs& a, const RecPre* pre, bool seal, int round
     if (seal) hipLaunchKernelGGL((gcm_hy_kernel<true, 14, 1024, 0, TG_QUEUE_NB>), g, b, 0, s, a, pre);
     else hipLaunchKernelGGL((gcm_hy_kernel<false, 14, 1024, 0, TG_QUEUE_NB>), g, b, 0, s, a, pre);
   }
-  if (a.sel) {  // the pack variant: runs instead when the prep pass saw a short record
+  if (a.sel && a.pack) {  // the pack variant: runs instead when the prep pass saw a short record
     if (rounds == 10) {
       if (seal) hipLaunchKernelGGL((gcm_hy_kernel<true, 10, 1024, 0, TG_QUEUE_NB, true>), g, b, 0, s, a, pre);
       else hipLaunchKernelGGL((gcm_hy_kernel<false, 10, 1024, 0, TG_QUEUE_NB, true>), g, b, 0, s, a, pre);

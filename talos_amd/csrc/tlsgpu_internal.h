@@ -126,6 +126,22 @@ __device__ __forceinline__ void load16_any(const uint8_t* p, uint32_t v[4]) {
   v[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
 }
 
+// The first nb (1..16) bytes of a block at any byte address, zero past them:
+// dword loads only where a byte below nb lies (a record's last piece may end
+// at its buffer's last page).
+__device__ __forceinline__ void load16_upto(const uint8_t* p, uint32_t nb, uint32_t v[4]) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t sh = (uint32_t)a & 3u;
+  const auto q = gld<uint32_t>((const void*)(a & ~(uintptr_t)3));
+  const uint32_t nd = (sh + nb + 3) >> 2;  // dwords holding bytes [0, nb): 1..5
+  const uint32_t w0 = q[0], w1 = nd > 1 ? q[1] : 0u, w2 = nd > 2 ? q[2] : 0u;
+  const uint32_t w3 = nd > 3 ? q[3] : 0u, w4 = nd > 4 ? q[4] : 0u;
+  v[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+  v[1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+  v[2] = __builtin_amdgcn_alignbyte(w3, w2, sh);
+  v[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
+}
+
 // The matching store: whole dwords inside the block, 1-2 byte/short stores at
 // its two ends (never a read-modify-write of a neighbour's bytes).
 __device__ __forceinline__ void store16_any(uint8_t* p, const uint32_t o[4]) {
@@ -236,7 +252,7 @@ int launch_gcm_hy14(const BatchArgs& a, const RecPre* pre, bool seal, int bs_wav
                     hipStream_t s);
 int launch_bs_ecb(const DevSession* sessions, uint32_t session, int rounds, const void* d_in,
                   void* d_out, uint32_t nblocks, hipStream_t s);
-int launch_chacha(const BatchArgs& a, bool seal, bool raw, int groups, hipStream_t s);
+int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, hipStream_t s);
 int launch_session_install(DevSession* sessions, DevGcmTables* tables,
                            const tlsgpu_session_params* d_params, uint32_t first,
                            uint32_t n, hipStream_t s);

@@ -80,3 +80,11 @@ def test_gcm_impl_selection_without_gpu(lib):
         ta.set_gcm_impl(prev)
     if not os.environ.get("TLSGPU_GCM_IMPL"):
         assert prev == "auto"
+
+
+def test_sessions_hint_rejects_bad_arguments(lib):
+    """tlsgpu_sessions_hint: a null table or an unknown hint bit is EINVAL (no GPU needed)."""
+    import ctypes as C
+    lib.tlsgpu_sessions_hint.argtypes = [C.c_void_p, C.c_uint]
+    lib.tlsgpu_sessions_hint.restype = C.c_int
+    assert lib.tlsgpu_sessions_hint(None, 1) != 0

@@ -178,12 +178,13 @@ def _records(rnd, nsess, lengths, kinds, grouped=True):
 
 
 def _run_seal_open(ta, engine, oracle, kinds, lengths, grouped=True, in_shift=0, out_shift=0,
-                   seed=1, in_place=False):
+                   seed=1, in_place=False, hints=0):
     from talos_amd.batch import RecordBatch
     rnd = random.Random(seed)
     params = _mk_sessions(ta, rnd, kinds)
     table = ta.SessionTable(engine, len(params))
     table.install(0, params)
+    table.hint(hints)
     osess = _oracle_sessions(oracle, params)
     recs = _records(rnd, len(params), lengths, kinds, grouped)
 
@@ -252,6 +253,16 @@ def gcm_impl(ta):
 def test_batch_gcm_impls_all_lengths(ta, engine, oracle, gcm_impl, impl, name):
     gcm_impl(impl)
     _run_seal_open(ta, engine, oracle, [KINDS[name]] * 2, LENGTHS, seed=21)
+
+
+@pytest.mark.parametrize("hints", [1, 2, 3])
+def test_batch_wrong_hints_still_exact(ta, engine, oracle, gcm_impl, hints):
+    """tlsgpu_sessions_hint is performance only: short records under
+    NO_SHORT_RECORDS take the long-record path, interleaved sessions under
+    SESSION_RUNS the run-at-a-time queue; results stay the oracle's."""
+    gcm_impl("queue")
+    kinds = [KINDS["aes-128-gcm"], KINDS["aes-256-gcm"]] * 3
+    _run_seal_open(ta, engine, oracle, kinds, LENGTHS, grouped=False, seed=31, hints=hints)
 
 
 # Long records: pairs of >= 16 KiB aligned records take the bitsliced passes
