@@ -40,12 +40,13 @@ class RecordBatch:
         ip = op = 0
         for i, (sid, seq, rtype, payload, kind) in enumerate(entries):
             eiv = EXPLICIT_NONCE_LEN[kind]
+            ish = in_shift[i] if isinstance(in_shift, (list, tuple)) else in_shift
             if mode == "seal":
-                ip = _align(ip, 16) + in_shift
+                ip = _align(ip, 16) + ish
                 olen = len(payload) + eiv + TAG_LEN
                 op = _align(op, 16, (16 - eiv) % 16) + out_shift
             else:
-                ip = _align(ip, 16, (16 - eiv) % 16) + in_shift
+                ip = _align(ip, 16, (16 - eiv) % 16) + ish
                 olen = max(len(payload) - eiv - TAG_LEN, 0)
                 op = _align(op, 16) + out_shift
             in_offs.append(ip)

@@ -179,6 +179,7 @@ def _records(rnd, nsess, lengths, kinds, grouped=True):
 
 def _run_seal_open(ta, engine, oracle, kinds, lengths, grouped=True, in_shift=0, out_shift=0,
                    seed=1, in_place=False, hints=0):
+    """in_shift: one shift for every record's input, or a function of the record index."""
     from talos_amd.batch import RecordBatch
     rnd = random.Random(seed)
     params = _mk_sessions(ta, rnd, kinds)
@@ -189,6 +190,8 @@ def _run_seal_open(ta, engine, oracle, kinds, lengths, grouped=True, in_shift=0,
     recs = _records(rnd, len(params), lengths, kinds, grouped)
 
     # seal on the GPU, compare with the oracle's tls1_enc(s, 1)
+    if callable(in_shift):
+        in_shift = [in_shift(i) for i in range(len(recs))]
     sb = RecordBatch(engine, recs, "seal", in_shift=in_shift, out_shift=out_shift)
     sb.run(table)
     bodies = []
@@ -253,6 +256,17 @@ def gcm_impl(ta):
 def test_batch_gcm_impls_all_lengths(ta, engine, oracle, gcm_impl, impl, name):
     gcm_impl(impl)
     _run_seal_open(ta, engine, oracle, [KINDS[name]] * 2, LENGTHS, seed=21)
+
+
+@pytest.mark.parametrize("name", ["chacha20-poly1305", "aes-128-gcm"])
+def test_batch_mixed_alignment_waves(ta, engine, oracle, name):
+    """Waves of 64 records whose inputs are all 16-B aligned next to waves with
+    one misaligned record and all-misaligned waves (ChaCha: the sector-ring and
+    line kernels take complementary waves of one batch)."""
+    lengths = [1400, 1, 15, 16, 17, 63, 64, 65, 127, 128, 129, 1000, 0, 4096, 333] * 30
+    shift = lambda i: 0 if (i // 64) % 3 == 0 else (i % 7 if (i // 64) % 3 == 2 else
+                                                   (5 if i % 64 == 17 else 0))
+    _run_seal_open(ta, engine, oracle, [KINDS[name]] * 2, lengths, seed=41, in_shift=shift)
 
 
 @pytest.mark.parametrize("hints", [1, 2, 3])
