@@ -350,7 +350,7 @@ __device__ __forceinline__ void cc_block_lds(uint32_t x[16], const uint8_t* key,
 
 // One wave: records r = (first record of the wave) + lane, one per lane
 // (t1_enc.c:832-975 for the ChaCha suites, e_chacha20poly1305.c:124-286).
-template <bool SEAL, bool RING>
+template <bool SEAL>
 __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8_t* tile,
                             uint8_t* keys) {
   // --- parse (the fields the end of the record needs are re-derived there)
@@ -391,9 +391,6 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
       }
     }
   }
-  // RING: waves whose records' inputs are all 16-B aligned (device batches);
-  // !RING: the others (wire fragments).  Both kernels decide alike per wave.
-  if (!(!RING && a.cc_line_all) && __all(!active || (((uintptr_t)src) & 15) == 0) != RING) return;
   uint8_t* key = keys + 16u * lane;
   lds_wave_sync();
   Poly p;
@@ -403,69 +400,65 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
     poly_init(p, ks);
     poly_block(p, sq_hi, sq_lo, ad2, n & 0xFF, 1u << 24);  // 13-B AD, pad16
   }
+  // pieces this lane moves: records 8k + lane/8, piece (lane % 8 - record/2) % 8
+  // of each step; the records' pointers and lengths are fetched with ds_bpermute
+  // per step (keeping 8 x 5 of them in VGPRs would cost a wave per SIMD)
+  uint32_t steps = (n + kCcStep - 1) / kCcStep;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) steps = max(steps, (uint32_t)__shfl_xor((int)steps, m));
   uint32_t ctr = 0;
-  if (RING) {
-    // 16-B-aligned inputs (device batches): sector-aligned input windows.
-    // Window w of a record = the 64-B memory sector [src - d + 64 w, + 64),
-    // d = src mod 64, i.e. record offsets [64 w - d, 64 w - d + 64); each is
-    // loaded once, whole, and kept in a 128-B ring per row (two windows) while
-    // step s processes record offsets [64 s, 64 s + 64) (windows s and s + 1).
-    // So no memory line is split between two loads a step apart (round 2's
-    // 128-B record-relative steps re-fetched the shared line from HBM after it
-    // had left L2: +73 % HBM reads on config C's open side).  Record offset o
-    // sits at ring byte (o + 16 (row / 2)) mod 128 whatever d is: the rows'
-    // ds_read_b128 of one piece are bank-conflict-free.
-    const uint32_t d = (uint32_t)(uintptr_t)src & 63u;
-    uint32_t steps = (n + 63) / 64;
+  // gather of step s: 8 records x 128 B per load instruction, into registers
+  // (issued one step ahead, so the loads fly during the previous step's math)
+  auto gather = [&](uint32_t base, uint4 (&v)[kCcP]) {
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) steps = max(steps, (uint32_t)__shfl_xor((int)steps, m));
-    // window w of 16 records per instruction: lane -> record 16k + lane/4, piece lane % 4
-    auto gather = [&](uint32_t w, uint4 (&v)[4]) {
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const uint32_t rr = 16 * k + lane / 4;
-        const uint32_t snk = __shfl(n, (int)rr);
-        const uint64_t srck = shfl64((uint64_t)(uintptr_t)src, rr);
-        const uint64_t at = (srck & ~(uint64_t)63) + 64ull * w + 16ull * (lane & 3);
-        v[k] = make_uint4(0, 0, 0, 0);
-        // a 16-B-aligned piece that holds a byte of the record's input never
-        // crosses into another page; pieces past it are not read
-        if (at < srck + snk) v[k] = gload16((const void*)(uintptr_t)at);
+    for (int k = 0; k < kCcP; k++) {
+      const uint32_t rr = kCcR * k + lane / kCcP;
+      const uint32_t off = base + 16u * (((lane % kCcP) - (rr >> 1)) & 7u);
+      const uint32_t snk = __shfl(n, (int)rr);
+      // ds_bpermute outside the branch: an inactive source lane reads as 0
+      const uint64_t srck = shfl64((uint64_t)(uintptr_t)src, rr);
+      v[k] = make_uint4(0, 0, 0, 0);
+      if (off < snk) {
+        const uint8_t* sp = (const uint8_t*)(uintptr_t)srck + off;
+        if (((uintptr_t)sp & 15) == 0) {
+          v[k] = gload16(sp);  // full or last piece: an aligned 16 B never crosses a page
+        } else {  // wire fragments (misaligned): only dwords that hold a record byte
+          uint32_t w[4];
+          load16_upto(sp, min(16u, snk - off), w);
+          v[k] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
       }
-    };
-    auto put = [&](uint32_t w, const uint4 (&v)[4]) {
+    }
+  };
+  uint4 pf[kCcP];
+  gather(0, pf);
+  for (uint32_t s = 0; s < steps; s++) {
+    const uint32_t base = s * kCcStep;
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const uint32_t rr = 16 * k + lane / 4;
-        const uint32_t dk = (uint32_t)__shfl((int)d, (int)rr);
-        const uint32_t pos = (64u * w - dk + 16u * (lane & 3) + 16u * (rr >> 1)) & 127u;
-        *reinterpret_cast<uint4*>(tile + rr * 128u + pos) = v[k];
-      }
-    };
-    uint4 pf[4];
-    gather(0, pf);
-    put(0, pf);
-    gather(1, pf);
-    for (uint32_t s = 0; s < steps; s++) {
-      put(s + 1, pf);  // into window s - 1's half of the ring (done at step s - 1)
-      if (s + 1 < steps) gather(s + 2, pf);
-      lds_wave_sync();
-      const uint32_t base = 64u * s;
-      if (base < n) {
-        ctr += 1;  // data blocks count from 1 (chacha-merged.c:230-236)
+    for (int k = 0; k < kCcP; k++)
+      *reinterpret_cast<uint4*>(tile + 1024u * k + 16u * lane) = pf[k];
+    if (s + 1 < steps) gather(base + kCcStep, pf);
+    lds_wave_sync();
+    // en/decrypt + MAC this lane's row: 2 ChaCha blocks
+    if (base < n) {
+#pragma unroll 1
+      for (int h = 0; h < (int)(kCcStep / 64); h++) {
+        const uint32_t o64 = base + 64u * h;
+        if (o64 >= n) break;
+        ctr += 1;  // data blocks count from 1 (chacha-merged.c:230-236; TLS records < 2^32 blocks)
         uint32_t ks[16];
         cc_block_lds(ks, key, ctr, c13, c14, c15);
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-          const uint32_t o = base + 16 * q;
+          const uint32_t o = o64 + 16 * q;
           if (o >= n) break;
           const uint32_t nb = min(16u, n - o);
-          uint4* slot = reinterpret_cast<uint4*>(tile + lane * 128u + ((o + 16u * (lane >> 1)) & 127u));
+          uint4* slot = reinterpret_cast<uint4*>(tile + cc_slot(lane, 4 * h + q));
           const uint4 t = *slot;
           uint32_t in[4] = {t.x, t.y, t.z, t.w};
           uint32_t ob[4] = {in[0] ^ ks[4 * q], in[1] ^ ks[4 * q + 1], in[2] ^ ks[4 * q + 2],
                             in[3] ^ ks[4 * q + 3]};
-          if (nb < 16) {  // zero the bytes past the record (MAC pad16 / ring bytes of the next record)
+          if (nb < 16) {  // zero the bytes past the record (MAC pad16 / staged garbage)
 #pragma unroll
             for (int w = 0; w < 4; w++) {
               int32_t b = (int32_t)nb - 4 * w;
@@ -479,129 +472,37 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
           poly_block(p, c[0], c[1], c[2], c[3], 1u << 24);
         }
       }
-      lds_wave_sync();
-      // scatter: record offsets [64 s, 64 s + 64) of 16 records per instruction
+    }
+    lds_wave_sync();
+    // scatter
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const uint32_t rr = 16 * k + lane / 4;
-        const uint32_t off = base + 16u * (lane & 3);
-        const uint32_t snk = __shfl(n, (int)rr);
-        const uint64_t dstk = shfl64((uint64_t)(uintptr_t)dst, rr);
-        if (off < snk) {
-          uint8_t* dp = (uint8_t*)(uintptr_t)dstk + off;
-          const uint4 v = *reinterpret_cast<const uint4*>(tile + rr * 128u + ((off + 16u * (rr >> 1)) & 127u));
-          if (off + 16 <= snk && ((uintptr_t)dp & 15) == 0) {
-            gstore16(dp, v);
-          } else if (off + 16 <= snk) {
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-            store16_any(dp, w);
-          } else {
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-            const uint32_t nb = min(16u, snk - off);
-            for (uint32_t b = 0; b < nb; b++) gst<uint8_t>(dp)[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
-          }
+    for (int k = 0; k < kCcP; k++) {
+      const uint32_t rr = kCcR * k + lane / kCcP;
+      const uint32_t off = base + 16u * (((lane % kCcP) - (rr >> 1)) & 7u);
+      const uint32_t snk = __shfl(n, (int)rr);
+      const uint64_t dstk = shfl64((uint64_t)(uintptr_t)dst, rr);
+      if (off < snk) {
+        uint8_t* dp = (uint8_t*)(uintptr_t)dstk + off;
+        const uint4 v = *reinterpret_cast<const uint4*>(tile + 1024u * k + 16u * lane);
+        if (off + 16 <= snk && ((uintptr_t)dp & 15) == 0) {
+#ifdef TG_CC_NT_STORE  // A/B: non-temporal output stores (leave L2 to the input lines)
+          u32x4 w4;
+          w4.x = v.x; w4.y = v.y; w4.z = v.z; w4.w = v.w;
+          __builtin_nontemporal_store(w4, gst<u32x4>(dp));
+#else
+          gstore16(dp, v);
+#endif
+        } else if (off + 16 <= snk) {
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+          store16_any(dp, w);
+        } else {
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+          const uint32_t nb = min(16u, snk - off);
+          for (uint32_t b = 0; b < nb; b++) gst<uint8_t>(dp)[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
         }
       }
-      lds_wave_sync();
     }
-  } else {
-    // pieces this lane moves: records 8k + lane/8, piece (lane % 8 - record/2) % 8
-    // of each step; the records' pointers and lengths are fetched with ds_bpermute
-    // per step (keeping 8 x 5 of them in VGPRs would cost a wave per SIMD)
-    uint32_t steps = (n + kCcStep - 1) / kCcStep;
-  #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) steps = max(steps, (uint32_t)__shfl_xor((int)steps, m));
-    // gather of step s: 8 records x 128 B per load instruction, into registers
-    // (issued one step ahead, so the loads fly during the previous step's math)
-    auto gather = [&](uint32_t base, uint4 (&v)[kCcP]) {
-  #pragma unroll
-      for (int k = 0; k < kCcP; k++) {
-        const uint32_t rr = kCcR * k + lane / kCcP;
-        const uint32_t off = base + 16u * (((lane % kCcP) - (rr >> 1)) & 7u);
-        const uint32_t snk = __shfl(n, (int)rr);
-        // ds_bpermute outside the branch: an inactive source lane reads as 0
-        const uint64_t srck = shfl64((uint64_t)(uintptr_t)src, rr);
-        v[k] = make_uint4(0, 0, 0, 0);
-        if (off < snk) {
-          const uint8_t* sp = (const uint8_t*)(uintptr_t)srck + off;
-          if (((uintptr_t)sp & 15) == 0) {
-            v[k] = gload16(sp);  // full or last piece: an aligned 16 B never crosses a page
-          } else {  // wire fragments (misaligned): only dwords that hold a record byte
-            uint32_t w[4];
-            load16_upto(sp, min(16u, snk - off), w);
-            v[k] = make_uint4(w[0], w[1], w[2], w[3]);
-          }
-        }
-      }
-    };
-    uint4 pf[kCcP];
-    gather(0, pf);
-    for (uint32_t s = 0; s < steps; s++) {
-      const uint32_t base = s * kCcStep;
-  #pragma unroll
-      for (int k = 0; k < kCcP; k++)
-        *reinterpret_cast<uint4*>(tile + 1024u * k + 16u * lane) = pf[k];
-      if (s + 1 < steps) gather(base + kCcStep, pf);
-      lds_wave_sync();
-      // en/decrypt + MAC this lane's row: 2 ChaCha blocks
-      if (base < n) {
-  #pragma unroll 1
-        for (int h = 0; h < (int)(kCcStep / 64); h++) {
-          const uint32_t o64 = base + 64u * h;
-          if (o64 >= n) break;
-          ctr += 1;  // data blocks count from 1 (chacha-merged.c:230-236; TLS records < 2^32 blocks)
-          uint32_t ks[16];
-          cc_block_lds(ks, key, ctr, c13, c14, c15);
-  #pragma unroll
-          for (int q = 0; q < 4; q++) {
-            const uint32_t o = o64 + 16 * q;
-            if (o >= n) break;
-            const uint32_t nb = min(16u, n - o);
-            uint4* slot = reinterpret_cast<uint4*>(tile + cc_slot(lane, 4 * h + q));
-            const uint4 t = *slot;
-            uint32_t in[4] = {t.x, t.y, t.z, t.w};
-            uint32_t ob[4] = {in[0] ^ ks[4 * q], in[1] ^ ks[4 * q + 1], in[2] ^ ks[4 * q + 2],
-                              in[3] ^ ks[4 * q + 3]};
-            if (nb < 16) {  // zero the bytes past the record (MAC pad16 / staged garbage)
-  #pragma unroll
-              for (int w = 0; w < 4; w++) {
-                int32_t b = (int32_t)nb - 4 * w;
-                uint32_t keep = b >= 4 ? 0xFFFFFFFFu : (b <= 0 ? 0u : ((1u << (8 * b)) - 1u));
-                ob[w] &= keep;
-                in[w] &= keep;
-              }
-            }
-            *slot = make_uint4(ob[0], ob[1], ob[2], ob[3]);
-            const uint32_t* c = SEAL ? ob : in;
-            poly_block(p, c[0], c[1], c[2], c[3], 1u << 24);
-          }
-        }
-      }
-      lds_wave_sync();
-      // scatter
-  #pragma unroll
-      for (int k = 0; k < kCcP; k++) {
-        const uint32_t rr = kCcR * k + lane / kCcP;
-        const uint32_t off = base + 16u * (((lane % kCcP) - (rr >> 1)) & 7u);
-        const uint32_t snk = __shfl(n, (int)rr);
-        const uint64_t dstk = shfl64((uint64_t)(uintptr_t)dst, rr);
-        if (off < snk) {
-          uint8_t* dp = (uint8_t*)(uintptr_t)dstk + off;
-          const uint4 v = *reinterpret_cast<const uint4*>(tile + 1024u * k + 16u * lane);
-          if (off + 16 <= snk && ((uintptr_t)dp & 15) == 0) {
-            gstore16(dp, v);
-          } else if (off + 16 <= snk) {
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-            store16_any(dp, w);
-          } else {
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-            const uint32_t nb = min(16u, snk - off);
-            for (uint32_t b = 0; b < nb; b++) gst<uint8_t>(dp)[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
-          }
-        }
-      }
-      lds_wave_sync();
-    }
+    lds_wave_sync();
   }
   if (!active) return;
   poly_block(p, 13u, 0, n, 0, 1u << 24);  // le64(ad_len) || le64(ct_len)
@@ -693,14 +594,13 @@ __device__ __forceinline__ bool cc_parse_tls(const BatchArgs& a, uint32_t r, CcR
   return true;
 }
 
-// TLS batches: LDS-staged coalesced data path (cc_tls_wave), 4 waves per SIMD;
-// RING = the sector-ring variant for 16-B-aligned inputs.
-template <bool SEAL, bool RING>
+// TLS batches: LDS-staged coalesced data path (cc_tls_wave), 4 waves per SIMD.
+template <bool SEAL>
 __global__ __launch_bounds__(kCcThreads) void chacha_tls_kernel(BatchArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t tiles[kCcThreads / kWave][kCcTile];
   __shared__ __attribute__((aligned(16))) uint8_t keys[kCcThreads / kWave][kCcKeys];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  cc_tls_wave<SEAL, RING>(a, blockIdx.x * blockDim.x + threadIdx.x, lane, tiles[wave], keys[wave]);
+  cc_tls_wave<SEAL>(a, blockIdx.x * blockDim.x + threadIdx.x, lane, tiles[wave], keys[wave]);
 }
 
 // Per-lane data path: raw EVP jobs, TLS records of the draft suite (OLD_ONLY:
@@ -716,9 +616,15 @@ __global__ __launch_bounds__(256) void chacha_batch_kernel(BatchArgs a) {
   uint32_t tag_len;
   if (RAW) {
     const RawJob j = reinterpret_cast<const RawJob*>(a.descs)[r];
-    if (j.session >= a.n_sessions) return;
+    // no per-batch status memset for raw jobs (run_batch): a bad or empty
+    // session is publicly invalid here (the GCM raw kernel writes the same)
+    if (j.session >= a.n_sessions) { *slot = TLSGPU_REC_PUBLIC_INVALID; return; }
     S = a.sessions + j.session;
     uint32_t kind = S->kind;
+    if (kind < TLSGPU_AES_128_GCM || kind > TLSGPU_CHACHA20_POLY1305_OLD) {
+      *slot = TLSGPU_REC_PUBLIC_INVALID;
+      return;
+    }
     if (kind != TLSGPU_CHACHA20_POLY1305 && kind != TLSGPU_CHACHA20_POLY1305_OLD) return;
     tag_len = S->tag_len;
     rc.old = kind == TLSGPU_CHACHA20_POLY1305_OLD;
@@ -770,11 +676,7 @@ static bool getenv_legacy_chacha() {
 }
 
 // rfc / old: the batch may hold records of the RFC 7905 / draft suite.
-// align: 0 unknown (both kernels: the sector-ring kernel takes the waves whose
-// inputs are all 16-B aligned, the line kernel the others), 2 wire fragments
-// (the line kernel takes every wave).
-int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, int align,
-                  hipStream_t s) {
+int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, hipStream_t s) {
   if (a.n == 0) return 0;
   dim3 grid((a.n + 255) / 256), block(256);
   const bool staged = !raw && !getenv_legacy_chacha();
@@ -788,15 +690,9 @@ int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, i
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
-  if (rfc && align != 2) {
-    if (seal) hipLaunchKernelGGL((chacha_tls_kernel<true, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((chacha_tls_kernel<false, true>), grid, block, 0, s, a);
-  }
   if (rfc) {
-    BatchArgs b = a;
-    b.cc_line_all = align == 2 ? 1u : 0u;
-    if (seal) hipLaunchKernelGGL((chacha_tls_kernel<true, false>), grid, block, 0, s, b);
-    else hipLaunchKernelGGL((chacha_tls_kernel<false, false>), grid, block, 0, s, b);
+    if (seal) hipLaunchKernelGGL((chacha_tls_kernel<true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((chacha_tls_kernel<false>), grid, block, 0, s, a);
   }
   if (old) {
     if (seal) hipLaunchKernelGGL((chacha_batch_kernel<true, false, true>), grid, block, 0, s, a);

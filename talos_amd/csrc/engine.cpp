@@ -402,10 +402,6 @@ static uint32_t g_pws = []() {
   return *v == '0' ? 1u : 2u;
 }();
 
-// Engine-internal hint bit (beside TLSGPU_HINT_*): the records are in-place
-// wire fragments (5-B headers: inputs not 16-B aligned).
-constexpr unsigned kHintWireRecords = 0x100u;
-
 // bounds: {in_bytes, out_bytes} of a caller's TLS batch (checked by a pre-pass
 // that hands the kernels a sanitized copy of the descriptors), or null for
 // descriptors the engine built itself (raw EVP jobs, wire framing).
@@ -501,8 +497,10 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
       return fail(TLSGPU_EHIP, "bounds launch: %s", hipGetErrorString(hipGetLastError()));
     a.descs = safe;
   } else {
-    // records whose session is empty / invalid keep this status
-    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)d_status, (int)TLSGPU_REC_PUBLIC_INVALID, n, s));
+    // records whose session is empty / invalid keep this status (raw EVP
+    // jobs: the raw kernels write it themselves, so a queue batch launches no
+    // fill kernel — round 2 measured ~18 K of them per queue run)
+    if (!raw) HIPCHK(hipMemsetD32Async((hipDeviceptr_t)d_status, (int)TLSGPU_REC_PUBLIC_INVALID, n, s));
     if (ctl_zero) HIPCHK(hipMemsetAsync(ctl_zero, 0, ctl_bytes, s));
   }
   for (int rounds : {10, 14}) {
@@ -543,7 +541,7 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   }
   if ((have[TLSGPU_CHACHA20_POLY1305] || have[TLSGPU_CHACHA20_POLY1305_OLD]) &&
       launch_chacha(a, seal, raw, have[TLSGPU_CHACHA20_POLY1305],
-                    have[TLSGPU_CHACHA20_POLY1305_OLD], (hints & kHintWireRecords) ? 2 : 0, s))
+                    have[TLSGPU_CHACHA20_POLY1305_OLD], s))
     return fail(TLSGPU_EHIP, "chacha launch: %s", hipGetErrorString(hipGetLastError()));
   if (pool_scratch) HIPCHK(hipFreeAsync(pool_scratch, s));
   return TLSGPU_OK;
@@ -900,8 +898,7 @@ extern "C" int tlsgpu_open_wire(tlsgpu_sessions* t, const tlsgpu_wire_stream* d_
                         d_results, d_total, s))
     return fail(TLSGPU_EHIP, "wire frame launch: %s", hipGetErrorString(hipGetLastError()));
   if (max_records) {
-    int rc = run_batch(t, d_recs, max_records, d_wire, d_wire, d_status, s, false, false, nullptr,
-                       ~0u, t->hints.load(std::memory_order_relaxed) | kHintWireRecords);
+    int rc = run_batch(t, d_recs, max_records, d_wire, d_wire, d_status, s, false, false);
     if (rc != TLSGPU_OK) return rc;
   }
   if (launch_wire_finish(n_streams, d_results, d_status, s))
@@ -1571,7 +1568,7 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
   a.n_sessions = st->sess->capacity;
   const bool gcm = st->kind == TLSGPU_AES_128_GCM || st->kind == TLSGPU_AES_256_GCM;
   int rc = gcm ? launch_gcm(a, seal, true, st->kind == TLSGPU_AES_128_GCM ? 10 : 14, 1, s)
-               : launch_chacha(a, seal, true, true, true, 0, s);
+               : launch_chacha(a, seal, true, true, true, s);
   if (rc) return -1;
   // success writes at most in_len + tag (seal) / in_len - tag (open) bytes
   const size_t back = seal ? in_len + st->tag_len : std::min(max_out_len, in_len);

@@ -131,7 +131,14 @@ __global__ __launch_bounds__(kThreads, 1) void gcm_raw_kernel(BatchArgs a) {
   const bool in_range = sid < a.n_sessions;
   const DevSession* __restrict__ S = a.sessions + (in_range ? sid : 0);
   const uint32_t kind = as_const(&S->kind)[0];
-  if (!(in_range && is_gcm(kind) && (int)as_const(&S->rounds)[0] == ROUNDS)) return;
+  if (!(in_range && is_gcm(kind) && (int)as_const(&S->rounds)[0] == ROUNDS)) {
+    // raw jobs: no per-batch status memset (run_batch); a job no kernel of
+    // this launch set takes (bad or empty session) is publicly invalid here
+    if (!TLS && threadIdx.x == 0 && !(in_range && kind >= TLSGPU_AES_128_GCM &&
+                                       kind <= TLSGPU_CHACHA20_POLY1305_OLD))
+      a.status[r] = TLSGPU_REC_PUBLIC_INVALID;
+    return;
+  }
   fill_aes_lds<kThreads>();
   load_session_tables<kThreads>(a.gcm_tables + sid);
   __syncthreads();

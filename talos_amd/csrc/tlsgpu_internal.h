@@ -202,9 +202,6 @@ struct BatchArgs {
   uint32_t pws;                     // per-wave-session kernel: 0 auto (runs shorter than
                                     // kPwsRun records on average), 1 never, 2 always
   uint32_t* wg_next;                // per-wave-session kernel: one record counter per workgroup
-  uint32_t cc_line_all;             // ChaCha TLS: 1 = the line kernel takes every wave (wire
-                                    // fragments, no ring kernel launched); 0 = the waves the
-                                    // sector-ring kernel leaves (a misaligned input)
 };
 
 // Average session-run length below which the per-wave-session kernel (gcm_pw.hip)
@@ -255,8 +252,7 @@ int launch_gcm_hy14(const BatchArgs& a, const RecPre* pre, bool seal, int bs_wav
                     hipStream_t s);
 int launch_bs_ecb(const DevSession* sessions, uint32_t session, int rounds, const void* d_in,
                   void* d_out, uint32_t nblocks, hipStream_t s);
-int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, int align,
-                  hipStream_t s);
+int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, hipStream_t s);
 int launch_session_install(DevSession* sessions, DevGcmTables* tables,
                            const tlsgpu_session_params* d_params, uint32_t first,
                            uint32_t n, hipStream_t s);
