@@ -1,0 +1,12 @@
+#!/bin/bash
+# Config C: parity suite on the in-tree build, then a same-box A/B of library
+# variants.  usage: scripts/ab_cc.sh TAG "lib ..." [rounds]
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$1
+mkdir -p $O
+cd $R
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -2 $O/tests.log
+[ $rc -ne 0 ] && exit $rc
+bash scripts/ab_bench.sh $1/ab ${3:-3} "$2" --config C

@@ -485,13 +485,7 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
         uint8_t* dp = (uint8_t*)(uintptr_t)dstk + off;
         const uint4 v = *reinterpret_cast<const uint4*>(tile + 1024u * k + 16u * lane);
         if (off + 16 <= snk && ((uintptr_t)dp & 15) == 0) {
-#ifdef TG_CC_NT_STORE  // A/B: non-temporal output stores (leave L2 to the input lines)
-          u32x4 w4;
-          w4.x = v.x; w4.y = v.y; w4.z = v.z; w4.w = v.w;
-          __builtin_nontemporal_store(w4, gst<u32x4>(dp));
-#else
           gstore16(dp, v);
-#endif
         } else if (off + 16 <= snk) {
           const uint32_t w[4] = {v.x, v.y, v.z, v.w};
           store16_any(dp, w);
