@@ -149,14 +149,17 @@ def cpu_baseline(kind_name: str, rec_len, op: str, note: str = "") -> dict | Non
 
 
 def load_traffic(config: str, kernel: str):
-    """PMC-measured HBM bytes per launch of `kernel` (FETCH_SIZE x2 + WRITE_SIZE,
-    scripts/pmc_summary.py), if a profile of that same kernel was committed."""
+    """PMC-measured HBM bytes per launch of `kernel`, if a profile of that same
+    kernel was committed (scripts/pmc_summary.py): the L2's memory-side read
+    requests by size (TCC_EA0_RDREQ_128B/64B/32B) + WRITE_SIZE when that pass
+    exists, else FETCH_SIZE x2 + WRITE_SIZE (MI355X_MICROARCH.md §HBM)."""
     p = os.path.join(ROOT, "profiles", f"pmc_config{config}.json")
     if os.path.exists(p):
         try:
             d = json.load(open(p))
             if kernel in d.get("kernel", ""):
-                return d.get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
+                return (d.get("hbm_bytes_per_launch_by_request_size") or
+                        d.get("hbm_bytes_per_launch")), os.path.relpath(p, ROOT)
         except Exception:
             return None, None
     return None, None
