@@ -434,11 +434,43 @@ __device__ __forceinline__ void mul_shoup(const uint32_t X[4], uint32_t e, uint3
   Z[0] = z0; Z[1] = z1; Z[2] = z2; Z[3] = z3;
 }
 
+// The same product with its table reads issued ahead of the chain (round 3):
+// the reads depend only on x's nibbles, but the compiler waited for each read
+// right after issuing it, so a multiply cost 32 LDS round trips in series.
+// Used by the per-record finish (GhLane::shoup); the pack path keeps
+// mul_shoup, whose lanes hold their plaintext through the multiply (the
+// look-ahead registers made that kernel spill 60 VGPRs).
+constexpr int kShoupAhead = 4;
+__device__ __forceinline__ void mul_shoup_ahead(const uint32_t X[4], uint32_t e, uint32_t Z[4]) {
+  const uint32_t base = sh_base(e);
+  uint4 t[32];
+#pragma unroll
+  for (int k = 0; k < 32; k++) t[k] = lds_u128(base + ((X[3 - k / 8] >> (4 * (k % 8))) & 0xF) * 256);
+  uint32_t z0 = t[0].x, z1 = t[0].y, z2 = t[0].z, z3 = t[0].w;
+#pragma unroll
+  for (int k = 1; k < 32; k++) {
+    const uint32_t rem = z3 & 0xF;
+    z3 = __builtin_amdgcn_alignbit(z2, z3, 4);
+    z2 = __builtin_amdgcn_alignbit(z1, z2, 4);
+    z1 = __builtin_amdgcn_alignbit(z0, z1, 4);
+    z0 = (z0 >> 4) ^ rem4(rem);
+    z0 ^= t[k].x; z1 ^= t[k].y; z2 ^= t[k].z; z3 ^= t[k].w;
+  }
+  // schedule: kShoupAhead reads first, then one read per chain step
+  __builtin_amdgcn_sched_group_barrier(0x100, kShoupAhead, 0);
+#pragma unroll
+  for (int k = 0; k < 32 - kShoupAhead; k++) {
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);
+  }
+  Z[0] = z0; Z[1] = z1; Z[2] = z2; Z[3] = z3;
+}
+
 __device__ __forceinline__ void GhLane::mul64(const uint32_t x[4], uint32_t o[4]) const {
   mul_k(x, o, *this);
 }
 __device__ __forceinline__ void GhLane::shoup(const uint32_t X[4], uint32_t e, uint32_t Z[4]) const {
-  mul_shoup(X, e, Z);
+  mul_shoup_ahead(X, e, Z);
 }
 
 // Two independent Shoup multiplies, interleaved; e == 0 gives zero.
