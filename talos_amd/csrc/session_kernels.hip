@@ -96,6 +96,19 @@ __device__ inline void shoup_table(U128 y, U128 (&m)[16]) {
     for (int b = 1; b < a; b++) m[a + b] = U128{m[a].hi ^ m[b].hi, m[a].lo ^ m[b].lo};
 }
 
+// Entry v of y's Shoup table without building the others (a lane-indexed
+// array would live in scratch memory): the XOR of m[8], m[4], m[2], m[1]
+// selected by v's bits.
+__device__ inline U128 shoup_entry(U128 y, uint32_t v) {
+  const U128 y1 = gf_mulx(y), y2 = gf_mulx(y1), y3 = gf_mulx(y2);
+  U128 r{0, 0};
+  if (v & 8) { r.hi ^= y.hi; r.lo ^= y.lo; }
+  if (v & 4) { r.hi ^= y1.hi; r.lo ^= y1.lo; }
+  if (v & 2) { r.hi ^= y2.hi; r.lo ^= y2.lo; }
+  if (v & 1) { r.hi ^= y3.hi; r.lo ^= y3.lo; }
+  return r;
+}
+
 // rem_4bit[r] >> 32 (gcm128.c:327-331) on the VALU: (r * 0xE1) << 21, carry-less
 __device__ inline uint32_t rem4v(uint32_t r) {
   return (r << 21) ^ ((r ^ (r << 1) ^ (r << 2)) << 26);
@@ -107,20 +120,33 @@ __device__ inline uint32_t rem4v(uint32_t r) {
 __device__ inline U128 gf_mul_tab(U128 x, const uint4* tab) {
   const uint32_t X[4] = {(uint32_t)(x.hi >> 32), (uint32_t)x.hi, (uint32_t)(x.lo >> 32),
                          (uint32_t)x.lo};
-  uint4 m = tab[X[3] & 0xF];
-  uint32_t z0 = m.x, z1 = m.y, z2 = m.z, z3 = m.w;
+  // the 32 table reads depend on x only: issued ahead of the chain (round 3)
+  uint4 t[32];
+#pragma unroll
+  for (int k = 0; k < 32; k++) t[k] = tab[(X[3 - k / 8] >> (4 * (k % 8))) & 0xF];
+  uint32_t z0 = t[0].x, z1 = t[0].y, z2 = t[0].z, z3 = t[0].w;
 #pragma unroll
   for (int k = 1; k < 32; k++) {
-    const uint32_t nib = (X[3 - k / 8] >> (4 * (k % 8))) & 0xF;
     const uint32_t rem = z3 & 0xF;
     z3 = __builtin_amdgcn_alignbit(z2, z3, 4);
     z2 = __builtin_amdgcn_alignbit(z1, z2, 4);
     z1 = __builtin_amdgcn_alignbit(z0, z1, 4);
     z0 = (z0 >> 4) ^ rem4v(rem);
-    const uint4 t = tab[nib];
-    z0 ^= t.x; z1 ^= t.y; z2 ^= t.z; z3 ^= t.w;
+    z0 ^= t[k].x; z1 ^= t[k].y; z2 ^= t[k].z; z3 ^= t[k].w;
+  }
+  __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+  for (int k = 0; k < 24; k++) {
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);
   }
   return U128{((uint64_t)z0 << 32) | z1, ((uint64_t)z2 << 32) | z3};
+}
+
+__device__ inline U128 shfl128(U128 v, uint32_t src) {
+  const uint32_t a = __shfl((uint32_t)(v.hi >> 32), (int)src), b = __shfl((uint32_t)v.hi, (int)src);
+  const uint32_t c = __shfl((uint32_t)(v.lo >> 32), (int)src), d = __shfl((uint32_t)v.lo, (int)src);
+  return U128{((uint64_t)a << 32) | b, ((uint64_t)c << 32) | d};
 }
 
 // One wave per session (blockIdx.x = session index), the work of
@@ -200,33 +226,39 @@ __global__ __launch_bounds__(64) void install_sessions(DevSession* __restrict__ 
     const uint32_t r = w / 128, b = (w % 128) / 8, k = w % 8;
     t->bsrk[r][8 * b + k] = 0u - ((s.rk[4 * r + b / 4] >> (8 * (b % 4) + k)) & 1u);
   }
-  // sq[k] = H^(2^k), each squaring against the previous power's shared table
-  U128 sq[7];
-  sq[0] = H;
-  for (int k = 0; k < 7; k++) {
-    if (k > 0) sq[k] = gf_mul_tab(sq[k - 1], sqtab[k - 1]);
-    if (lane < 16) {
-      U128 m[16];
-      shoup_table(sq[k], m);
-      sqtab[k][lane] = be_words(m[lane]);
-    }
+  // H^(lane + 1) by doubling (round 3): after level k, lanes [0, 2^(k+1))
+  // hold their powers; level k multiplies lane (l - 2^k)'s power by H^(2^k)
+  // for lanes l in [2^k, 2^(k+1)), against the Shoup table 16 lanes build from
+  // lane 2^k - 1.  Seven products deep in all (round 2: seven squarings, then
+  // up to five square-and-multiply products per lane).
+  U128 pw = lane == 0 ? H : U128{0, 0};
+  for (int k = 0; k < 6; k++) {
+    const uint32_t step = 1u << k;
+    const U128 b = shfl128(pw, step - 1);
+    if (lane < 16) sqtab[k][lane] = be_words(shoup_entry(b, lane));
     __syncthreads();
+    const U128 src = shfl128(pw, lane >= step ? lane - step : 0);
+    if (lane >= step && lane < 2 * step) pw = gf_mul_tab(src, sqtab[k]);
   }
-  // lane e - 1 (and lane 0 for e = 65): H^e by square-and-multiply, its Shoup table
-  for (uint32_t e = lane + 1; e <= (uint32_t)kPowMax; e += 64) {
-    int k0 = __builtin_ctz(e);
-    U128 pw = sq[k0];
-    for (int k = k0 + 1; k < 7; k++)
-      if ((e >> k) & 1) pw = gf_mul_tab(pw, sqtab[k]);
+  // H^64 (lane 63): its table gives H^65 and the basis
+  const U128 h64 = shfl128(pw, 63);
+  if (lane < 16) sqtab[6][lane] = be_words(shoup_entry(h64, lane));
+  __syncthreads();
+  // Shoup tables of H^e: lane e - 1, and lane 0 for e = 65
+  {
     U128 m[16];
     shoup_table(pw, m);
-    for (int v = 0; v < 16; v++) *reinterpret_cast<uint4*>(t->shoup[e - 1][v]) = be_words(m[v]);
+    for (int v = 0; v < 16; v++) *reinterpret_cast<uint4*>(t->shoup[lane][v]) = be_words(m[v]);
+    if (lane == 0) {
+      shoup_table(gf_mul_tab(H, sqtab[6]), m);
+      for (int v = 0; v < 16; v++) *reinterpret_cast<uint4*>(t->shoup[kPowMax - 1][v]) = be_words(m[v]);
+    }
   }
-  // basis[q] = K * x^q, K = H^64 = sq[6]; lanes q and q + 64
+  // basis[q] = H^64 * x^q: the product of the one-hot x^q (bit q from the
+  // MSB, gcm128.c's bit order) with H^64's table; lanes q and q + 64
   for (uint32_t q = lane; q < 128; q += 64) {
-    U128 b = sq[6];
-    for (uint32_t k = 0; k < q; k++) b = gf_mulx(b);
-    store_le(t->basis[q], b);
+    const U128 xq = q < 64 ? U128{1ull << (63 - q), 0} : U128{0, 1ull << (127 - q)};
+    store_le(t->basis[q], gf_mul_tab(xq, sqtab[6]));
   }
 }
 
