@@ -136,6 +136,9 @@ struct tlsgpu_sessions {
   std::vector<const void*> owners;  // SSL* per session for the TaLoS hooks (set_owner)
   bool have[5];                // any session of kind k installed
   std::atomic<unsigned> hints{0};  // TLSGPU_HINT_* (tlsgpu_sessions_hint)
+  // EVP contexts: per-slot event of the slot's last install or scrub, so init
+  // and cleanup need not wait on the device (created on a slot's first use)
+  std::vector<hipEvent_t> slot_ev;
   std::mutex mu;               // host mirrors, when several threads install at once
 };
 
@@ -218,6 +221,11 @@ extern "C" void tlsgpu_sessions_destroy(tlsgpu_sessions* t) {
   if (!t) return;
   (void)hipSetDevice(t->eng->device);
   (void)hipStreamSynchronize(t->eng->stream);
+  for (hipEvent_t ev : t->slot_ev)
+    if (ev) {
+      (void)hipEventSynchronize(ev);  // a scrub still running on a call stream
+      (void)hipEventDestroy(ev);
+    }
   (void)hipFree(t->d_sess);
   (void)hipFree(t->d_gcm);
   delete t;
@@ -1153,6 +1161,8 @@ struct AeadState {
   unsigned tag_len;
   EvpBatcher* batcher;    // the queue of the context's device (pooled contexts), or null
   uint32_t evp_dev;       // index of the context's device among the EVP devices
+  hipEvent_t installed;   // the slot's event, recorded after the context's key install
+  mutable std::atomic<bool> install_pending{true};  // no call has waited for it yet
 };
 
 // EVP context storage without a device allocation per context (connection
@@ -1354,23 +1364,34 @@ static Staging* stage_for(int dev) {
   return st;
 }
 
-// One session install for an EVP context, on the calling thread's call stream
-// through its pinned staging (no device allocation, no engine-stream
-// serialisation): the key install of one connection direction.
-static int install_one(tlsgpu_sessions* t, uint32_t slot, const tlsgpu_session_params& p) {
+// The event of a slot (created on first use).
+static hipEvent_t slot_event(tlsgpu_sessions* t, uint32_t slot) {
+  std::lock_guard<std::mutex> lk(t->mu);
+  if (t->slot_ev.size() < t->capacity) t->slot_ev.resize(t->capacity, nullptr);
+  hipEvent_t& ev = t->slot_ev[slot];
+  if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
+  return ev;
+}
+
+// One session install for an EVP context on the calling thread's call stream,
+// asynchronous (round 3): the parameters travel as a kernel argument (no
+// staging copy to wait for), the install is ordered after the slot's previous
+// scrub by the slot's event and records it again when done; the context's
+// first call waits for that event on the device (gpu_call_impl).  A
+// connection's key install at ChangeCipherSpec (t1_enc.c:444-495) then costs
+// no device round trip of its own.
+static int install_one(tlsgpu_sessions* t, uint32_t slot, const tlsgpu_session_params& p,
+                       hipEvent_t* installed) {
   if (!valid_params(p) || slot >= t->capacity) return fail(TLSGPU_EINVAL, "bad session");
   Staging* stg = stage_for(t->eng->device);
-  if (!stg || !stg->ensure(t->eng->device, sizeof(p))) return fail(TLSGPU_ENOMEM, "staging");
-  memcpy(stg->h_buf, &p, sizeof(p));
-  auto* d_params = reinterpret_cast<tlsgpu_session_params*>(stg->d_buf);
-  const bool ok =
-      hipMemcpyAsync(d_params, stg->h_buf, sizeof(p), hipMemcpyHostToDevice, stg->stream) ==
-          hipSuccess &&
-      launch_session_install(t->d_sess, t->d_gcm, d_params, slot, 1, stg->stream) == 0 &&
-      hipEventRecord(stg->done, stg->stream) == hipSuccess &&
-      hipEventSynchronize(stg->done) == hipSuccess;
-  memset(stg->h_buf, 0, sizeof(p));
+  if (!stg || !stg->ensure(t->eng->device, 16)) return fail(TLSGPU_ENOMEM, "staging");
+  const hipEvent_t ev = slot_event(t, slot);  // on the slot's device (ensure set it)
+  if (!ev) return fail(TLSGPU_EHIP, "slot event");
+  const bool ok = hipStreamWaitEvent(stg->stream, ev, 0) == hipSuccess &&
+                  launch_session_install_arg(t->d_sess, t->d_gcm, p, slot, stg->stream) == 0 &&
+                  hipEventRecord(ev, stg->stream) == hipSuccess;
   if (!ok) return fail(TLSGPU_EHIP, "session install: %s", hipGetErrorString(hipGetLastError()));
+  *installed = ev;
   std::lock_guard<std::mutex> lk(t->mu);
   t->kinds[slot] = p.aead;
   t->tag_lens[slot] = (uint8_t)(p.tag_len ? p.tag_len : 16);
@@ -1378,16 +1399,18 @@ static int install_one(tlsgpu_sessions* t, uint32_t slot, const tlsgpu_session_p
   return TLSGPU_OK;
 }
 
-// Zero a session slot's key material on the calling thread's stream and wait.
+// Zero a session slot's key material on the calling thread's stream without
+// waiting: the slot's event orders the next install of the slot after it.
 static void scrub_slot(tlsgpu_sessions* t, uint32_t slot) {
   Staging* stg = stage_for(t->eng->device);
-  if (stg && stg->ensure(t->eng->device, 16) &&
-      hipMemsetAsync(t->d_sess + slot, 0, sizeof(DevSession), stg->stream) == hipSuccess &&
+  const bool staged = stg && stg->ensure(t->eng->device, 16);
+  const hipEvent_t ev = staged ? slot_event(t, slot) : nullptr;
+  if (ev && hipMemsetAsync(t->d_sess + slot, 0, sizeof(DevSession), stg->stream) == hipSuccess &&
       hipMemsetAsync(t->d_gcm + slot, 0, sizeof(DevGcmTables), stg->stream) == hipSuccess &&
-      hipEventRecord(stg->done, stg->stream) == hipSuccess &&
-      hipEventSynchronize(stg->done) == hipSuccess)
+      hipEventRecord(ev, stg->stream) == hipSuccess)
     return;
   (void)hipSetDevice(t->eng->device);  // fall back to the synchronous form
+  (void)hipDeviceSynchronize();
   (void)hipMemset(t->d_sess + slot, 0, sizeof(DevSession));
   (void)hipMemset(t->d_gcm + slot, 0, sizeof(DevGcmTables));
 }
@@ -1438,8 +1461,9 @@ extern "C" int EVP_AEAD_CTX_init(EVP_AEAD_CTX* ctx, const EVP_AEAD* aead, const 
   memcpy(p.key, key, key_len);
   p.tag_len = (uint32_t)tag_len;
   p.version = 0x0303;
-  // on this thread's call stream: installs of concurrent threads overlap
-  const int rc = install_one(st->sess, st->slot, p);
+  // on this thread's call stream, not waited for: installs of concurrent
+  // threads overlap, and the context's first call is ordered after it
+  const int rc = install_one(st->sess, st->slot, p, &st->installed);
   memset(&p, 0, sizeof(p));
   if (rc != TLSGPU_OK) {
     release_slot(st);
@@ -1526,7 +1550,13 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
                          size_t max_out_len, const unsigned char* nonce, size_t nonce_len,
                          const unsigned char* in, size_t in_len, const unsigned char* ad,
                          size_t ad_len) {
+  // the context's key install (EVP_AEAD_CTX_init does not wait for it)
+  const bool wait_install = st->install_pending.load(std::memory_order_acquire);
   if (st->batcher) {  // pooled context: join the coalescing queue (large jobs run alone)
+    if (wait_install) {
+      if (hipEventSynchronize(st->installed) != hipSuccess) return -1;
+      st->install_pending.store(false, std::memory_order_release);
+    }
     int r = evp_queue_call(st->batcher, st, seal, out, out_len, max_out_len, nonce, nonce_len,
                            in, in_len, ad, ad_len);
     if (r != -2) return r;
@@ -1542,6 +1572,9 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
   uint8_t* d = stg->d_buf;
   uint8_t* h = stg->h_buf;
   hipStream_t s = stg->stream;
+  if (st->install_pending.load(std::memory_order_acquire) &&
+      hipStreamWaitEvent(s, st->installed, 0) != hipSuccess)
+    return -1;
   RawJob* j = reinterpret_cast<RawJob*>(h);
   j->in = (uint64_t)(d + o_in);
   j->out = (uint64_t)(d + o_out);
@@ -1577,6 +1610,7 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
       hipEventRecord(stg->done, s) != hipSuccess ||
       hipEventSynchronize(stg->done) != hipSuccess)
     return -1;
+  st->install_pending.store(false, std::memory_order_release);  // done before this call's work
   const int32_t status = *reinterpret_cast<const int32_t*>(h + o_status);
   if (status < 0) {  // the kernel's zero-fill of max_out_len bytes (evp_aead.c:137-143)
     if (max_out_len) memset(out, 0, max_out_len);

@@ -159,23 +159,39 @@ __device__ inline U128 shfl128(U128 v, uint32_t src) {
 // H^e (lane e, square-and-multiply over them) use 4-bit products against
 // Shoup tables shared in LDS.  Round 2 measured 104 us per install with
 // global-memory S-box lookups, a scratch DevSession and bit-serial products.
+__device__ __forceinline__ void install_body(DevSession* __restrict__ sessions,
+                                             DevGcmTables* __restrict__ tables,
+                                             const tlsgpu_session_params& p, uint32_t id);
+
 __global__ __launch_bounds__(64) void install_sessions(DevSession* __restrict__ sessions,
                                                        DevGcmTables* __restrict__ tables,
                                                        const tlsgpu_session_params* __restrict__ params,
                                                        uint32_t first, uint32_t n) {
+  if (blockIdx.x >= n) return;
+  install_body(sessions, tables, params[blockIdx.x], first + blockIdx.x);
+}
+
+// One session with its parameters as a kernel argument (EVP_AEAD_CTX_init):
+// no staging buffer and no copy, so the caller need not wait for the install
+// before it reuses its memory (round 3, asynchronous context init).
+__global__ __launch_bounds__(64) void install_session_arg(DevSession* __restrict__ sessions,
+                                                          DevGcmTables* __restrict__ tables,
+                                                          tlsgpu_session_params p, uint32_t id) {
+  install_body(sessions, tables, p, id);
+}
+
+__device__ __forceinline__ void install_body(DevSession* __restrict__ sessions,
+                                             DevGcmTables* __restrict__ tables,
+                                             const tlsgpu_session_params& p, uint32_t id) {
   __shared__ __attribute__((aligned(16))) uint8_t sb[256];
   __shared__ uint32_t rk_be[60];
   __shared__ uint8_t hb[16];
   __shared__ uint4 hdr[sizeof(DevSession) / 16];
   __shared__ uint4 sqtab[7][16];  // Shoup tables of H^(2^k), k = 0..6
-  const uint32_t i = blockIdx.x;
   const uint32_t lane = threadIdx.x;
-  if (i >= n) return;
   static_assert(sizeof(DevSession) / 16 == 64, "one 16-B chunk of the header per lane");
   reinterpret_cast<uint32_t*>(sb)[lane] = reinterpret_cast<const uint32_t*>(g_sbox.v)[lane];
   hdr[lane] = make_uint4(0, 0, 0, 0);
-  const tlsgpu_session_params p = params[i];
-  const uint32_t id = first + i;
   const bool gcm = p.aead == TLSGPU_AES_128_GCM || p.aead == TLSGPU_AES_256_GCM;
   const bool cc = p.aead == TLSGPU_CHACHA20_POLY1305 || p.aead == TLSGPU_CHACHA20_POLY1305_OLD;
   const uint32_t want_key = p.aead == TLSGPU_AES_128_GCM ? 16 : 32;
@@ -373,6 +389,12 @@ int launch_session_install(DevSession* sessions, DevGcmTables* tables,
   if (n == 0) return 0;
   hipLaunchKernelGGL(install_sessions, dim3(n), dim3(64), 0, s, sessions, tables,
                      d_params, first, n);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_session_install_arg(DevSession* sessions, DevGcmTables* tables,
+                               const tlsgpu_session_params& p, uint32_t id, hipStream_t s) {
+  hipLaunchKernelGGL(install_session_arg, dim3(1), dim3(64), 0, s, sessions, tables, p, id);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -253,6 +253,8 @@ int launch_gcm_hy14(const BatchArgs& a, const RecPre* pre, bool seal, int bs_wav
 int launch_bs_ecb(const DevSession* sessions, uint32_t session, int rounds, const void* d_in,
                   void* d_out, uint32_t nblocks, hipStream_t s);
 int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, hipStream_t s);
+int launch_session_install_arg(DevSession* sessions, DevGcmTables* tables,
+                               const tlsgpu_session_params& p, uint32_t id, hipStream_t s);
 int launch_session_install(DevSession* sessions, DevGcmTables* tables,
                            const tlsgpu_session_params* d_params, uint32_t first,
                            uint32_t n, hipStream_t s);
