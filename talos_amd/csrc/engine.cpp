@@ -1400,12 +1400,16 @@ static int install_one(tlsgpu_sessions* t, uint32_t slot, const tlsgpu_session_p
 }
 
 // Zero a session slot's key material on the calling thread's stream without
-// waiting: the slot's event orders the next install of the slot after it.
+// waiting: ordered after the slot's install by the slot's event, which then
+// orders the slot's next install after the scrub.
 static void scrub_slot(tlsgpu_sessions* t, uint32_t slot) {
   Staging* stg = stage_for(t->eng->device);
   const bool staged = stg && stg->ensure(t->eng->device, 16);
   const hipEvent_t ev = staged ? slot_event(t, slot) : nullptr;
-  if (ev && hipMemsetAsync(t->d_sess + slot, 0, sizeof(DevSession), stg->stream) == hipSuccess &&
+  // after the slot's install (a context cleaned up before any call, from
+  // another thread, may still have its install queued on another stream)
+  if (ev && hipStreamWaitEvent(stg->stream, ev, 0) == hipSuccess &&
+      hipMemsetAsync(t->d_sess + slot, 0, sizeof(DevSession), stg->stream) == hipSuccess &&
       hipMemsetAsync(t->d_gcm + slot, 0, sizeof(DevGcmTables), stg->stream) == hipSuccess &&
       hipEventRecord(ev, stg->stream) == hipSuccess)
     return;

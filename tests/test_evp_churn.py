@@ -45,6 +45,23 @@ def worker(t):
             ctx.cleanup()
     except Exception as exc:
         errors.append(repr(exc))
+# contexts created on one thread and cleaned up on another without any call:
+# the scrub must not overtake the install queued on the creating thread's stream
+handoff = []
+def create(t):
+    rnd = random.Random(700 + t)
+    for i in range(30):
+        kind = kinds[(t + i) % 4]
+        c = ta.EvpAead(kind, bytes(rnd.randrange(256) for _ in range(po.KEY_LEN[kind])))
+        assert c.ok == 1
+        handoff.append(c)
+ths = [threading.Thread(target=create, args=(t,)) for t in range(4)]
+[th.start() for th in ths]; [th.join() for th in ths]
+def destroy(part):
+    for c in part:
+        c.cleanup()
+ths = [threading.Thread(target=destroy, args=(handoff[k::4],)) for k in range(4)]
+[th.start() for th in ths]; [th.join() for th in ths]
 ths = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
 [th.start() for th in ths]; [th.join() for th in ths]
 assert not errors, errors[:3]
