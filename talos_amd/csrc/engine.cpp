@@ -1315,6 +1315,7 @@ struct Staging {
   hipEvent_t done = nullptr;
   uint8_t* d_buf = nullptr;
   uint8_t* h_buf = nullptr;
+  uint8_t* h_dev = nullptr;  // h_buf as the device addresses it (zero-copy calls)
   size_t cap = 0;
   ~Staging() {
     if (d_buf) (void)hipFree(d_buf);
@@ -1344,6 +1345,7 @@ struct Staging {
     size_t want = bytes < (1u << 20) ? (1u << 20) : bytes;
     if (hipMalloc(&d_buf, want) != hipSuccess) return false;
     if (hipHostMalloc((void**)&h_buf, want, hipHostMallocDefault) != hipSuccess) return false;
+    if (hipHostGetDevicePointer((void**)&h_dev, h_buf, 0) != hipSuccess) h_dev = nullptr;
     cap = want;
     return true;
   }
@@ -1530,6 +1532,11 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
                          const unsigned char* in, size_t in_len, const unsigned char* ad,
                          size_t ad_len);
 
+static const bool g_evp_zerocopy = [] {
+  const char* v = getenv("TLSGPU_EVP_ZEROCOPY");
+  return !(v && *v == '0');
+}();
+
 // One EVP call on the GPU: 1 = success, 0 = authentication failure / rejected
 // by the kernel (output zero-filled), -1 = runtime failure.
 static int gpu_call(const AeadState* st, bool seal, unsigned char* out, size_t* out_len,
@@ -1573,7 +1580,11 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
   tlsgpu_engine* e = st->sess->eng;
   Staging* stg = stage_for(e->device);
   if (!stg || !stg->ensure(e->device, total)) return -1;
-  uint8_t* d = stg->d_buf;
+  // zero-copy (round 3, default): the kernel reads the job from and writes its
+  // status and output to the pinned staging buffer itself — no H2D / D2H
+  // launches around a one-record batch; TLSGPU_EVP_ZEROCOPY=0 stages through HBM
+  const bool zc = g_evp_zerocopy && stg->h_dev;
+  uint8_t* d = zc ? stg->h_dev : stg->d_buf;
   uint8_t* h = stg->h_buf;
   hipStream_t s = stg->stream;
   if (st->install_pending.load(std::memory_order_acquire) &&
@@ -1594,7 +1605,7 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
   if (in_len) memcpy(h + o_in, in, in_len);
   // a job the kernel rejects keeps this status (never a stale one)
   *reinterpret_cast<int32_t*>(h + o_status) = TLSGPU_REC_PUBLIC_INVALID;
-  if (hipMemcpyAsync(d, h, o_status + 4, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
+  if (!zc && hipMemcpyAsync(d, h, o_status + 4, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
   BatchArgs a = {};
   a.sessions = st->sess->d_sess;
   a.gcm_tables = st->sess->d_gcm;
@@ -1609,8 +1620,8 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
   if (rc) return -1;
   // success writes at most in_len + tag (seal) / in_len - tag (open) bytes
   const size_t back = seal ? in_len + st->tag_len : std::min(max_out_len, in_len);
-  if (hipMemcpyAsync(h + o_status, d + o_status, o_out - o_status + back, hipMemcpyDeviceToHost,
-                     s) != hipSuccess ||
+  if ((!zc && hipMemcpyAsync(h + o_status, d + o_status, o_out - o_status + back,
+                             hipMemcpyDeviceToHost, s) != hipSuccess) ||
       hipEventRecord(stg->done, s) != hipSuccess ||
       hipEventSynchronize(stg->done) != hipSuccess)
     return -1;
