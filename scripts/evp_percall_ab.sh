@@ -12,6 +12,9 @@ for len in 1400 16384; do
     for zc in 0 1; do
       TLSGPU_EVP_ZEROCOPY=$zc timeout -k 10 60 "$R/oracle/_ref/cpubench" "$R/talos_amd/libtlsgpu.so" \
         aes-128-gcm seal $len $n $t 2 | sed "s/^{/{\"lib\": \"libtlsgpu per call zerocopy=$zc\", /" >> "$OUT" || exit 1
+      [ -n "$QUEUE" ] && { TLSGPU_EVP_BATCH_US=50 TLSGPU_EVP_ZEROCOPY=$zc timeout -k 10 60 "$R/oracle/_ref/cpubench" \
+        "$R/talos_amd/libtlsgpu.so" aes-128-gcm seal $len $n $t 2 \
+        | sed "s/^{/{\"lib\": \"libtlsgpu queue 50us zerocopy=$zc\", /" >> "$OUT" || exit 1; }
     done
   done
 done

@@ -1231,7 +1231,8 @@ constexpr size_t kEvpSlotBytes = kEvpOutOff + kEvpOutBytes;
 
 struct EvpSlot {
   uint8_t* h = nullptr;  // pinned: [RawJob x kEvpMaxJobs | inputs | status | outputs]
-  uint8_t* d = nullptr;  // device, same layout
+  uint8_t* d = nullptr;  // device, same layout (zero-copy: h as the device addresses it)
+  bool zc = false;       // zero-copy: no device copy of the slot, no H2D / D2H
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
   // built under EvpBatcher::mu: seal descriptors from the front, open ones
@@ -2208,8 +2209,8 @@ bool EvpBatcher::submit_work(EvpSlot* s) {
   const uint32_t ns = s->nseal, no = s->nopen;
   int32_t* d_status = reinterpret_cast<int32_t*>(s->d + kEvpStatusOff);
   const RawJob* d_desc = reinterpret_cast<const RawJob*>(s->d);
-  if (hipMemcpyAsync(s->d, s->h, kEvpDescBytes + s->in_used, hipMemcpyHostToDevice, s->stream) !=
-      hipSuccess)
+  if (!s->zc && hipMemcpyAsync(s->d, s->h, kEvpDescBytes + s->in_used, hipMemcpyHostToDevice,
+                               s->stream) != hipSuccess)
     return false;
   if (ns && run_batch(pool, d_desc, ns, nullptr, nullptr, d_status, s->stream, true, true,
                      nullptr, s->kinds_seal) != TLSGPU_OK)
@@ -2218,9 +2219,9 @@ bool EvpBatcher::submit_work(EvpSlot* s) {
                       d_status + (kEvpMaxJobs - no), s->stream, false, true, nullptr,
                       s->kinds_open) != TLSGPU_OK)
     return false;
-  return hipMemcpyAsync(s->h + kEvpStatusOff, s->d + kEvpStatusOff,
-                        kEvpOutOff - kEvpStatusOff + s->out_used, hipMemcpyDeviceToHost,
-                        s->stream) == hipSuccess &&
+  return (s->zc || hipMemcpyAsync(s->h + kEvpStatusOff, s->d + kEvpStatusOff,
+                                  kEvpOutOff - kEvpStatusOff + s->out_used,
+                                  hipMemcpyDeviceToHost, s->stream) == hipSuccess) &&
          hipEventRecord(s->done, s->stream) == hipSuccess;
 }
 
@@ -2267,8 +2268,12 @@ static EvpBatcher* make_batcher(tlsgpu_engine* e, unsigned window_us, unsigned m
   }
   bool ok = hipSetDevice(e->device) == hipSuccess;
   for (EvpSlot& s : b->slots) {
-    ok = ok && hipHostMalloc((void**)&s.h, kEvpSlotBytes, hipHostMallocDefault) == hipSuccess &&
-         hipMalloc((void**)&s.d, kEvpSlotBytes) == hipSuccess &&
+    ok = ok && hipHostMalloc((void**)&s.h, kEvpSlotBytes, hipHostMallocDefault) == hipSuccess;
+    // zero-copy (TLSGPU_EVP_ZEROCOPY, default on): the batch kernels read the
+    // jobs from and write statuses and outputs to the pinned slot directly
+    s.zc = ok && g_evp_zerocopy && hipHostGetDevicePointer((void**)&s.d, s.h, 0) == hipSuccess;
+    if (!s.zc) s.d = nullptr;
+    ok = ok && (s.zc || hipMalloc((void**)&s.d, kEvpSlotBytes) == hipSuccess) &&
          hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) == hipSuccess &&
          hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
   }
@@ -2276,7 +2281,7 @@ static EvpBatcher* make_batcher(tlsgpu_engine* e, unsigned window_us, unsigned m
     fail(TLSGPU_EHIP, "EVP queue staging on device %d", e->device);
     for (EvpSlot& s : b->slots) {
       if (s.h) (void)hipHostFree(s.h);
-      if (s.d) (void)hipFree(s.d);
+      if (s.d && !s.zc) (void)hipFree(s.d);
     }
     tlsgpu_sessions_destroy(b->pool);
     delete b;
