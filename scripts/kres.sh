@@ -6,5 +6,5 @@ for f in "$@"; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result "${flags[@]}" \
     -c "$f" -o /tmp/kres.o -Rpass-analysis=kernel-resource-usage 2>&1 |
   awk '/Function Name:/{n=$NF=="[-Rpass-analysis=kernel-resource-usage]"?$(NF-1):$NF}
-       / VGPRs: /{v=$(NF-1)} /VGPRs Spill:/{s=$(NF-1)} /Occupancy/{print n, "vgpr=" v, "spill=" s, "occ=" $(NF-1)}'
+       / VGPRs: /{v=$(NF-1)} /Occupancy/{o=$(NF-1)} /VGPRs Spill:/{print n, "vgpr=" v, "spill=" $(NF-1), "occ=" o}'
 done

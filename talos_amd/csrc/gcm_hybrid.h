@@ -446,7 +446,10 @@ __device__ void gcm_pack(const BatchArgs& a, const RecPre* __restrict__ pre, uin
     e[0] = 0; e[1] = 13u * 8u;
     e[2] = (uint32_t)(((uint64_t)n * 8) >> 32); e[3] = (uint32_t)((uint64_t)n * 8);
   }
-  if (SEAL && blk) store_block(dst + 16u * jb, nbytes, aligned, ob);
+  // open stores its plaintext now too and overwrites it with zeros below when
+  // the record's tag fails (as gcm_record's zero_len fill): ob is not held
+  // live through the multiply
+  if (blk) store_block(dst + 16u * jb, nbytes, aligned, ob);
   if (SEAL && used && j == -1) {
     for (int b = 0; b < 8; b++) op[b] = (uint8_t)(d.seq >> (56 - 8 * b));  // explicit nonce
   }
@@ -495,9 +498,9 @@ __device__ void gcm_pack(const BatchArgs& a, const RecPre* __restrict__ pre, uin
   }
   if (!SEAL) {  // plaintext, or zeros when the record's tag failed (evp_aead.c:137-143)
     const uint32_t rbad = __shfl(bad, (int)(base + rneed - 1));
-    if (blk) {
+    if (blk && rbad) {
       const uint32_t z[4] = {0, 0, 0, 0};
-      store_block(dst + 16u * jb, nbytes, aligned, rbad ? z : ob);
+      store_block(dst + 16u * jb, nbytes, aligned, z);
     }
   }
 }
