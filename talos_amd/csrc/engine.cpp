@@ -1449,7 +1449,9 @@ extern "C" int EVP_AEAD_CTX_init(EVP_AEAD_CTX* ctx, const EVP_AEAD* aead, const 
   st->evp_dev = (uint32_t)dk;
   {
     std::lock_guard<std::mutex> lk(g_batcher_mu);
-    EvpBatcher* b = g_batchers[dk];
+    // a queue counts only once tlsgpu_evp_set_batching has published every
+    // device's (a partial setup that failed leaves g_batcher_on false)
+    EvpBatcher* b = g_batcher_on ? g_batchers[dk] : nullptr;
     if (b && !b->free_sessions.empty()) {
       st->slot = (uint32_t)b->free_sessions.back();
       b->free_sessions.pop_back();
@@ -2312,7 +2314,17 @@ extern "C" int tlsgpu_evp_set_batching(unsigned window_us, unsigned max_jobs,
   // on the device evp_pick gives them
   const uint32_t cap = pool_sessions ? pool_sessions : 1024;
   const size_t ndev = evp_device_count();
+  // All devices or none: a queue built before a later device failed stays in
+  // g_batchers unused (g_batcher_on stays false, so no context takes its pool
+  // slots) and a retry reuses it instead of building a second one over it —
+  // its dispatcher and completer threads never outlive their queue's pointer.
   for (size_t k = 0; k < ndev; k++) {
+    if (g_batchers[k]) {
+      std::lock_guard<std::mutex> lk2(g_batchers[k]->mu);
+      g_batchers[k]->window_us = window_us;
+      if (max_jobs) g_batchers[k]->max_jobs = std::min(max_jobs, kEvpMaxJobs);
+      continue;
+    }
     tlsgpu_engine* e = evp_engine(k);
     if (!e) return fail(TLSGPU_EHIP, "no GPU engine for EVP device %zu", k);
     EvpBatcher* b = make_batcher(e, window_us, max_jobs, cap);

@@ -65,10 +65,12 @@ __device__ __forceinline__ void stamp_end(Stamp* st, unsigned long long t0, unsi
 
 // ---------------------------------------------------------------------------
 // VALU issue throughput
-enum { OP_PERM, OP_BITOP3, OP_ALIGNBIT, OP_XOR, OP_MAD64, OP_ADD, OP_SDWA, OP_N };
+enum { OP_PERM, OP_BITOP3, OP_ALIGNBIT, OP_XOR, OP_MAD64, OP_ADD, OP_SDWA, OP_ANDOR, OP_PKSWAP,
+       OP_BFE, OP_LSHLOR, OP_N };
 static const char* kOpName[OP_N] = {"v_perm_b32", "v_bitop3_b32", "v_alignbit_b32",
                                     "v_xor_b32", "v_mad_u64_u32", "v_add_u32",
-                                    "v_xor_b32_sdwa"};
+                                    "v_xor_b32_sdwa", "v_and_or_b32", "v_pk_add_u16_swap",
+                                    "v_bfe_u32", "v_lshl_or_b32"};
 
 template <int OP>
 __global__ void valu_kernel(int iters, uint32_t k1, uint32_t k2, Stamp* st, uint32_t* out) {
@@ -101,6 +103,14 @@ __global__ void valu_kernel(int iters, uint32_t k1, uint32_t k2, Stamp* st, uint
           asm volatile("v_alignbit_b32 %0, %0, %1, 16" : "+v"(r[i]) : "v"(k1));
         else if constexpr (OP == OP_XOR)
           asm volatile("v_xor_b32 %0, %0, %1" : "+v"(r[i]) : "v"(k1));
+        else if constexpr (OP == OP_ANDOR)
+          asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(r[i]) : "s"(k1), "v"(k2));
+        else if constexpr (OP == OP_PKSWAP)
+          asm volatile("v_pk_add_u16 %0, %0, 0 op_sel:[1,0] op_sel_hi:[0,1]" : "+v"(r[i]));
+        else if constexpr (OP == OP_BFE)
+          asm volatile("v_bfe_u32 %0, %0, 8, 8" : "+v"(r[i]));
+        else if constexpr (OP == OP_LSHLOR)
+          asm volatile("v_lshl_or_b32 %0, %0, 8, %1" : "+v"(r[i]) : "v"(k1));
         else if constexpr (OP == OP_SDWA)
           asm volatile("v_xor_b32_sdwa %0, %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE "
                        "src0_sel:WORD_0 src1_sel:WORD_0" : "+v"(r[i]) : "v"(k1));
@@ -394,6 +404,205 @@ __global__ void __launch_bounds__(1024) aes4t_kernel(int rounds, const uint32_t*
 }
 
 // ---------------------------------------------------------------------------
+// set3: a second lookup pipe.  The T-tables as a
+// 4 KiB global table (Te0..Te3, 1 KiB each) that stays in the CU's vector L1,
+// read by `buffer_load_dword ... idxen` with stride 4: the hardware scales the
+// byte index, so a lookup costs one VALU op (v_bfe / v_and / v_lshr) and one
+// vector-memory gather, no LDS cycle.
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v4i_t table_rsrc(const uint32_t* tab) {
+  const unsigned long long p = (unsigned long long)tab;
+  v4i_t r;
+  r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)p);
+  r.y = __builtin_amdgcn_readfirstlane((int)(((uint32_t)(p >> 32) & 0xffffu) | (4u << 16)));
+  r.z = 1024;  // records of 4 B
+  r.w = 0x00020000;
+  return r;
+}
+
+template <int OFF>
+__device__ __forceinline__ uint32_t ta_load(uint32_t idx, v4i_t r) {
+  uint32_t v;
+  asm volatile("buffer_load_dword %0, %1, %2, 0 idxen offset:%3" : "=v"(v) : "v"(idx), "s"(r), "i"(OFF));
+  return v;
+}
+
+// Dependent gather chains through the vector-memory path only.
+template <int NCH>
+__global__ void __launch_bounds__(1024) ta_chain_kernel(int iters, const uint32_t* __restrict__ gtab,
+                                                        Stamp* st, uint32_t* out) {
+  extern __shared__ uint32_t pad[];
+  if (iters < 0) pad[threadIdx.x] = 0;
+  const v4i_t rs = table_rsrc(gtab);
+  uint32_t x[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; c++) x[c] = (threadIdx.x * 97 + c * 31) & 255;
+  unsigned long long t0, r0;
+  stamp_begin(st, &t0, &r0);
+  for (int it = 0; it < iters; it++) {
+    uint32_t v[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; c++) v[c] = ta_load<0>(x[c] & 255, rs);
+    if constexpr (NCH == 4)
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+    else
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]),
+                   "+v"(v[5]), "+v"(v[6]), "+v"(v[7]));
+#pragma unroll
+    for (int c = 0; c < NCH; c++) x[c] = v[c] >> (c & 3);
+  }
+  uint32_t sink = 0;
+#pragma unroll
+  for (int c = 0; c < NCH; c++) sink ^= x[c];
+  stamp_end(st, t0, r0, sink, out);
+}
+
+// The T-table AES round of aes_round_kernel with the (c, d) lookups of the
+// first TAC columns taken from the L1 table (Te2, Te3 directly: those columns
+// need no alignbit).  TAC = 0 is aes_round_kernel.  The gathers of a round are
+// issued first (they depend only on the previous round's state), the LDS
+// lookups next, and one vmcnt wait per round precedes the combine.
+template <int NB, int TAC>
+__global__ void __launch_bounds__(1024) aes_ta_kernel(int rounds, const uint32_t* __restrict__ tab,
+                                                      const uint32_t* __restrict__ gtab,
+                                                      const uint32_t* __restrict__ rk_in, Stamp* st,
+                                                      uint32_t* out) {
+  extern __shared__ uint32_t lds[];
+  for (int i = threadIdx.x; i < 16384; i += blockDim.x) lds[i] = tab[i];
+  __syncthreads();
+  const v4i_t rs = table_rsrc(gtab);
+  const uint32_t lb0 = (threadIdx.x & 31) << 2;
+  const uint32_t lb1 = lb0 | 128;
+  uint32_t s[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; b++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) s[b][c] = (threadIdx.x + 1) * 0x9E3779B9u * (b * 4 + c + 1);
+  unsigned long long t0, r0;
+  stamp_begin(st, &t0, &r0);
+  for (int r = 0; r < rounds; r++) {
+    uint32_t kk[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) kk[c] = __builtin_amdgcn_readfirstlane(rk_in[(r & 15) * 4 + c]);
+    uint32_t g2[NB][4], g3[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; b++)
+#pragma unroll
+      for (int c = 0; c < TAC; c++) {
+        g2[b][c] = ta_load<2048>(__builtin_amdgcn_ubfe(s[b][(c + 2) & 3], 16, 8), rs);
+        g3[b][c] = ta_load<3072>(s[b][(c + 3) & 3] >> 24, rs);
+      }
+    uint32_t n[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; b++)
+#pragma unroll
+      for (int c = TAC; c < 4; c++) {
+        const uint32_t a0 = __builtin_amdgcn_perm(s[b][c], lb0, 0x0c0c0400u);
+        const uint32_t a1 = __builtin_amdgcn_perm(s[b][(c + 1) & 3], lb1, 0x0c0c0500u);
+        const uint32_t a2 = __builtin_amdgcn_perm(s[b][(c + 2) & 3], lb0, 0x0c0c0600u);
+        const uint32_t a3 = __builtin_amdgcn_perm(s[b][(c + 3) & 3], lb1, 0x0c0c0700u);
+        const uint32_t t0_ = lds[a0 >> 2], t1_ = lds[a1 >> 2], t2_ = lds[a2 >> 2], t3_ = lds[a3 >> 2];
+        const uint32_t inner = __builtin_amdgcn_bitop3_b32(t2_, t3_, kk[c], 0x96);
+        n[b][c] = __builtin_amdgcn_bitop3_b32(t0_, t1_, __builtin_amdgcn_alignbit(inner, inner, 16), 0x96);
+      }
+    uint32_t h0[NB][4], h1[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; b++)
+#pragma unroll
+      for (int c = 0; c < TAC; c++) {
+        const uint32_t a0 = __builtin_amdgcn_perm(s[b][c], lb0, 0x0c0c0400u);
+        const uint32_t a1 = __builtin_amdgcn_perm(s[b][(c + 1) & 3], lb1, 0x0c0c0500u);
+        h0[b][c] = lds[a0 >> 2];
+        h1[b][c] = lds[a1 >> 2];
+      }
+    if constexpr (TAC > 0) {
+      // one wait for the round's gathers, tied to their registers
+#pragma unroll
+      for (int b = 0; b < NB; b++)
+#pragma unroll
+        for (int c = 0; c < TAC; c++) asm volatile("" : "+v"(g2[b][c]), "+v"(g3[b][c]));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int b = 0; b < NB; b++)
+#pragma unroll
+        for (int c = 0; c < TAC; c++) {
+          asm volatile("" : "+v"(g2[b][c]), "+v"(g3[b][c]));
+          n[b][c] = __builtin_amdgcn_bitop3_b32(h0[b][c], h1[b][c],
+                                                __builtin_amdgcn_bitop3_b32(g2[b][c], g3[b][c], kk[c], 0x96),
+                                                0x96);
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; b++)
+#pragma unroll
+      for (int c = 0; c < 4; c++) s[b][c] = n[b][c];
+  }
+  uint32_t sink = 0;
+#pragma unroll
+  for (int b = 0; b < NB; b++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) sink ^= s[b][c];
+  stamp_end(st, t0, r0, sink, out);
+}
+
+// The T-table AES round with cheaper VALU forms (set4): MODE bit 0 — the
+// byte-1 lookup's address is (s & 0xff00) | lanebank, one v_and_or_b32 (the
+// byte is already in place) instead of a v_perm; bit 1 — the rotl16 of the
+// inner XOR is one v_pk_add_u16 with swapped halves instead of v_alignbit.
+__device__ __forceinline__ uint32_t swap16(uint32_t x) {
+  uint32_t r;
+  asm("v_pk_add_u16 %0, %1, 0 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(r) : "v"(x));
+  return r;
+}
+template <int NB, int MODE>
+__global__ void __launch_bounds__(1024) aes_v2_kernel(int rounds, const uint32_t* __restrict__ tab,
+                                                      const uint32_t* __restrict__ rk_in, Stamp* st,
+                                                      uint32_t* out) {
+  extern __shared__ uint32_t lds[];
+  for (int i = threadIdx.x; i < 16384; i += blockDim.x) lds[i] = tab[i];
+  __syncthreads();
+  const uint32_t lb0 = (threadIdx.x & 31) << 2;
+  const uint32_t lb1 = lb0 | 128;
+  uint32_t s[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; b++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) s[b][c] = (threadIdx.x + 1) * 0x9E3779B9u * (b * 4 + c + 1);
+  unsigned long long t0, r0;
+  stamp_begin(st, &t0, &r0);
+  for (int r = 0; r < rounds; r++) {
+    uint32_t kk[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) kk[c] = __builtin_amdgcn_readfirstlane(rk_in[(r & 15) * 4 + c]);
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+      uint32_t n[4];
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const uint32_t a0 = __builtin_amdgcn_perm(s[b][c], lb0, 0x0c0c0400u);
+        const uint32_t a1 = (MODE & 1) ? ((s[b][(c + 1) & 3] & 0xff00u) | lb1)
+                                       : __builtin_amdgcn_perm(s[b][(c + 1) & 3], lb1, 0x0c0c0500u);
+        const uint32_t a2 = __builtin_amdgcn_perm(s[b][(c + 2) & 3], lb0, 0x0c0c0600u);
+        const uint32_t a3 = __builtin_amdgcn_perm(s[b][(c + 3) & 3], lb1, 0x0c0c0700u);
+        const uint32_t t0_ = lds[a0 >> 2], t1_ = lds[a1 >> 2], t2_ = lds[a2 >> 2], t3_ = lds[a3 >> 2];
+        const uint32_t inner = __builtin_amdgcn_bitop3_b32(t2_, t3_, kk[c], 0x96);
+        const uint32_t rot = (MODE & 2) ? swap16(inner) : __builtin_amdgcn_alignbit(inner, inner, 16);
+        n[c] = __builtin_amdgcn_bitop3_b32(t0_, t1_, rot, 0x96);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; c++) s[b][c] = n[c];
+    }
+  }
+  uint32_t sink = 0;
+#pragma unroll
+  for (int b = 0; b < NB; b++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) sink ^= s[b][c];
+  stamp_end(st, t0, r0, sink, out);
+}
+
+// ---------------------------------------------------------------------------
 __global__ void copy_f4(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -403,6 +612,29 @@ __global__ void copy_f4(const float4* __restrict__ a, float4* __restrict__ b, si
     b[i + stride] = x1;
     b[i + 2 * stride] = x2;
     b[i + 3 * stride] = x3;
+  }
+  for (; i < n; i += stride) b[i] = a[i];
+}
+
+// Copy with U independent 16-B loads in flight per lane before the stores,
+// optionally non-temporal (the achievable-HBM denominator).
+typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) copy_u(const float4* __restrict__ a4, float4* __restrict__ b4,
+                                              size_t n) {
+  const v4u_t* a = (const v4u_t*)a4;
+  v4u_t* b = (v4u_t*)b4;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + (U - 1) * stride < n; i += U * stride) {
+    v4u_t x[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) x[u] = NT ? __builtin_nontemporal_load(a + i + u * stride) : a[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (NT) __builtin_nontemporal_store(x[u], b + i + u * stride);
+      else b[i + u * stride] = x[u];
+    }
   }
   for (; i < n; i += stride) b[i] = a[i];
 }
@@ -455,6 +687,7 @@ static void valu(int op, int w) {
     switch (op) {
 #define L(O) case O: valu_kernel<O><<<g_cus, th, lds>>>(iters, 0x05040100u, 0x0c0d0e0fu, g_st, g_out); break;
       L(OP_PERM) L(OP_BITOP3) L(OP_ALIGNBIT) L(OP_XOR) L(OP_MAD64) L(OP_ADD) L(OP_SDWA)
+      L(OP_ANDOR) L(OP_PKSWAP) L(OP_BFE) L(OP_LSHLOR)
 #undef L
     }
   };
@@ -543,6 +776,116 @@ static void copy() {
       CK(hipEventDestroy(e0));
       CK(hipEventDestroy(e1));
     }
+  }
+  CK(hipFree(a));
+  CK(hipFree(b));
+}
+
+static void set4() {
+  for (int op : {OP_PERM, OP_BITOP3, OP_ALIGNBIT, OP_ANDOR, OP_PKSWAP, OP_BFE, OP_LSHLOR})
+    for (int w : {1, 4}) valu(op, w);
+  for (int nb : {1, 2})
+    for (int mode = 0; mode < 4; mode++) {
+      const int rounds = 1024;
+      Res r = run([&](int th, size_t l) {
+#define A(NB, M) if (nb == NB && mode == M) aes_v2_kernel<NB, M><<<g_cus, th, l>>>(rounds, g_tab, g_rk, g_st, g_out);
+        A(1, 0) A(1, 1) A(1, 2) A(1, 3) A(2, 0) A(2, 1) A(2, 2) A(2, 3)
+#undef A
+      }, 1024, 96 * 1024);
+      const double br = (double)rounds * nb * 16;
+      printf("{\"bench\": \"aes_round_v2\", \"blocks_per_lane\": %d, \"and_or_byte1\": %d, "
+             "\"pk_swap_rot\": %d, \"waves_per_cu\": 16, \"cu_cycles_per_block_round\": %.3f, "
+             "\"lds_busy_frac\": %.3f, \"clock_ghz\": %.3f}\n",
+             nb, mode & 1, (mode >> 1) & 1, r.med_cycles / br, br * 32 / r.med_cycles, r.clock_ghz);
+    }
+}
+
+// set3: the vector-memory (L1) lookup pipe, alone and beside the LDS AES round,
+// and the copy variants.
+static void set3() {
+  uint32_t* gtab;
+  CK(hipMalloc(&gtab, 4096));
+  CK(hipMemcpy(gtab, g_tab, 4096, hipMemcpyDeviceToDevice));
+  for (int W : {8, 16})
+    for (int nch : {4, 8}) {
+      const int iters = 1024;
+      Res r = run([&](int th, size_t l) {
+        if (nch == 4) ta_chain_kernel<4><<<g_cus, th, l>>>(iters, gtab, g_st, g_out);
+        else ta_chain_kernel<8><<<g_cus, th, l>>>(iters, gtab, g_st, g_out);
+      }, 64 * W, 96 * 1024);
+      printf("{\"bench\": \"ta_gather\", \"instr\": \"buffer_load_dword idxen (1 KiB table, L1)\", "
+             "\"waves_per_cu\": %d, \"chains\": %d, \"cu_cycles_per_wave_gather\": %.3f, "
+             "\"clock_ghz\": %.3f}\n",
+             W, nch, r.med_cycles / ((double)iters * nch * W), r.clock_ghz);
+    }
+  for (int nb : {1, 2})
+    for (int tac = 0; tac <= 4; tac++) {
+      const int rounds = 1024;
+      Res r = run([&](int th, size_t l) {
+#define A(NB, T) if (nb == NB && tac == T) aes_ta_kernel<NB, T><<<g_cus, th, l>>>(rounds, g_tab, gtab, g_rk, g_st, g_out);
+        A(1, 0) A(1, 1) A(1, 2) A(1, 3) A(1, 4) A(2, 0) A(2, 1) A(2, 2) A(2, 3) A(2, 4)
+#undef A
+      }, 1024, 96 * 1024);
+      const double br = (double)rounds * nb * 16;
+      printf("{\"bench\": \"aes_round_ta\", \"blocks_per_lane\": %d, \"ta_columns\": %d, "
+             "\"lds_lookups_per_block_round\": %d, \"ta_lookups_per_block_round\": %d, "
+             "\"waves_per_cu\": 16, \"cu_cycles_per_block_round\": %.3f, \"lds_busy_frac\": %.3f, "
+             "\"clock_ghz\": %.3f}\n",
+             nb, tac, 16 - 2 * tac, 2 * tac, r.med_cycles / br, br * (16 - 2 * tac) * 2 / r.med_cycles,
+             r.clock_ghz);
+    }
+  CK(hipFree(gtab));
+  // copies
+  const size_t bytes = (size_t)1 << 30;
+  float4 *a, *b;
+  CK(hipMalloc(&a, bytes));
+  CK(hipMalloc(&b, bytes));
+  CK(hipMemset(a, 1, bytes));
+  const size_t n = bytes / sizeof(float4);
+  auto time_copy = [&](const char* name, int bpc, auto launch) {
+    launch(g_cus * bpc);
+    CK(hipDeviceSynchronize());
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const int reps = 10;
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < reps; i++) launch(g_cus * bpc);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("{\"bench\": \"copy\", \"kernel\": \"%s\", \"blocks_per_cu\": %d, "
+           "\"GBps_read_plus_write\": %.1f, \"frac_of_8TBs\": %.4f, \"ms\": %.4f}\n",
+           name, bpc, 2.0 * bytes * reps / (ms / 1e3) / 1e9, 2.0 * bytes * reps / (ms / 1e3) / 1e9 / 8000.0,
+           ms / reps);
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+  };
+  for (int bpc : {1, 2}) {
+    time_copy("u16_nt", bpc, [&](int g) { copy_u<16, true><<<g, 256>>>(a, b, n); });
+    time_copy("u16", bpc, [&](int g) { copy_u<16, false><<<g, 256>>>(a, b, n); });
+  }
+  for (int bpc : {2, 4, 8}) {
+    time_copy("u4", bpc, [&](int g) { copy_u<4, false><<<g, 256>>>(a, b, n); });
+    time_copy("u8", bpc, [&](int g) { copy_u<8, false><<<g, 256>>>(a, b, n); });
+    time_copy("u4_nt", bpc, [&](int g) { copy_u<4, true><<<g, 256>>>(a, b, n); });
+    time_copy("u8_nt", bpc, [&](int g) { copy_u<8, true><<<g, 256>>>(a, b, n); });
+  }
+  {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice));
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < 10; i++) CK(hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice));
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("{\"bench\": \"copy\", \"kernel\": \"hipMemcpyAsync\", \"GBps_read_plus_write\": %.1f, "
+           "\"frac_of_8TBs\": %.4f}\n", 2.0 * bytes * 10 / (ms / 1e3) / 1e9,
+           2.0 * bytes * 10 / (ms / 1e3) / 1e9 / 8000.0);
   }
   CK(hipFree(a));
   CK(hipFree(b));
@@ -646,7 +989,9 @@ int main(int argc, char** argv) {
        {(const void*)valu_kernel<OP_PERM>, (const void*)valu_kernel<OP_BITOP3>,
         (const void*)valu_kernel<OP_ALIGNBIT>, (const void*)valu_kernel<OP_XOR>,
         (const void*)valu_kernel<OP_MAD64>, (const void*)valu_kernel<OP_ADD>,
-        (const void*)valu_kernel<OP_SDWA>,
+        (const void*)valu_kernel<OP_SDWA>, (const void*)valu_kernel<OP_ANDOR>,
+        (const void*)valu_kernel<OP_PKSWAP>, (const void*)valu_kernel<OP_BFE>,
+        (const void*)valu_kernel<OP_LSHLOR>,
         (const void*)lds_b32_kernel<true, 4>, (const void*)lds_b32_kernel<true, 8>,
         (const void*)lds_b32_kernel<false, 4>, (const void*)lds_b32_kernel<false, 8>,
         (const void*)lds_b128_kernel<4>, (const void*)lds_b128_kernel<8>,
@@ -664,6 +1009,29 @@ int main(int argc, char** argv) {
     CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
   for (const void* f : {(const void*)aes4t_kernel<1>, (const void*)aes4t_kernel<2>})
     CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
+  for (const void* f :
+       {(const void*)ta_chain_kernel<4>, (const void*)ta_chain_kernel<8>,
+        (const void*)aes_ta_kernel<1, 0>, (const void*)aes_ta_kernel<1, 1>, (const void*)aes_ta_kernel<1, 2>,
+        (const void*)aes_ta_kernel<1, 3>, (const void*)aes_ta_kernel<1, 4>, (const void*)aes_ta_kernel<2, 0>,
+        (const void*)aes_ta_kernel<2, 1>, (const void*)aes_ta_kernel<2, 2>, (const void*)aes_ta_kernel<2, 3>,
+        (const void*)aes_ta_kernel<2, 4>})
+    CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+  for (const void* f :
+       {(const void*)aes_v2_kernel<1, 0>, (const void*)aes_v2_kernel<1, 1>, (const void*)aes_v2_kernel<1, 2>,
+        (const void*)aes_v2_kernel<1, 3>, (const void*)aes_v2_kernel<2, 0>, (const void*)aes_v2_kernel<2, 1>,
+        (const void*)aes_v2_kernel<2, 2>, (const void*)aes_v2_kernel<2, 3>})
+    CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+  if (argc > 1 && !strcmp(argv[1], "set4")) {
+    set4();
+    if (argc > 2) set3();
+    fflush(stdout);
+    return 0;
+  }
+  if (argc > 1 && !strcmp(argv[1], "set3")) {
+    set3();
+    fflush(stdout);
+    return 0;
+  }
   if (argc > 1 && !strcmp(argv[1], "set2")) {
     for (int w : {1, 4}) valu(OP_SDWA, w);
     set2();
