@@ -11,9 +11,14 @@ sealer; every step's outputs are verified after the warmup.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config B|C|D]
                   [--sessions S] [--interleave] [--mode device|host|wire|copy]
+                  [--split group|ranks] [--devices 0,1,...]
   N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
-       (one rank per GPU, records split by rank, no collective on the data path;
-        gloo only for the barrier and the max-over-ranks of the timing).
+       runs config E (configs[4]) through the C ABI's own batch split by
+       default: rank 0 drives a tlsgpu_group of N member GPUs (group.cpp), the
+       other ranks only join the barrier.  --split ranks: one rank per GPU,
+       records split by rank, each rank its own engine.  Either way no
+       collective on the data path; gloo only carries the barrier and the
+       max-over-ranks of the timing.
 
 Prints ONE JSON line (rank 0).  `roofline.achieved` = algorithmic bytes per
 launch / average launch time from HIP events on the engine stream;
@@ -232,6 +237,14 @@ def main():
                          "workload's lengths and session order imply")
     ap.add_argument("--host-streams", type=int, default=0, help="host mode: pipeline streams")
     ap.add_argument("--host-chunk-mib", type=int, default=0, help="host mode: chunk size")
+    ap.add_argument("--split", default=None, choices=["group", "ranks"],
+                    help="multi-GPU batch split: group = the C ABI's own split "
+                         "(tlsgpu_group_open_batch: one process drives every member GPU; the "
+                         "default for N > 1), ranks = one torch.distributed rank per GPU, each "
+                         "with its own engine")
+    ap.add_argument("--devices", default="",
+                    help="group split: comma-separated device ids (default 0..N-1); "
+                         "'0,0' rehearses a two-member group on one GPU")
     ap.add_argument("--mode", default="device", choices=["device", "host", "wire", "copy", "pcie"],
                     help="host: pinned host buffers + H2D/D2H overlap (PCIe-inclusive rate); "
                          "wire: raw TLS wire streams through tlsgpu_open_wire (framing + "
@@ -244,6 +257,8 @@ def main():
     from talos_amd.workload import Workload, zipf_lengths
 
     world, rank, local = env_rank()
+    if choose_split(args.split, world, args.devices) == "group" and args.mode == "device":
+        return group_mode(args, world, rank)
     ta.load_library()
     eng = ta.Engine(device_for(local, ta.device_count()))  # first GPU runtime user
     if args.mode == "copy":
@@ -282,7 +297,9 @@ def main():
     # what the caller that built the batch knows about its shape (no short GCM
     # records / long session runs): the engine then skips the launches of the
     # kernel variants the device would not select (tlsgpu.h tlsgpu_sessions_hint)
-    hints = 0 if args.no_hints else ta.batch_hints(wl.lengths, wl.session, seal=op != "open")
+    # descriptor lengths: fragments for an open, plaintexts for a seal
+    desc_len = wl.lengths + (ta.EXPLICIT_NONCE_LEN[kind] + ta.TAG_LEN if op == "open" else 0)
+    hints = 0 if args.no_hints else ta.batch_hints(desc_len, wl.session, seal=op != "open")
     wl.table.hint(hints)
     args.hints = hints
     if args.mode == "host":
@@ -405,6 +422,153 @@ def main():
     wl.free()
     cp.close()
     eng.close()
+
+
+def choose_split(split: str | None, world: int, devices: str) -> str:
+    """The multi-GPU split a run measures: the C ABI's group split for N > 1
+    ranks or an explicit device list, one engine per rank otherwise."""
+    if split:
+        return split
+    return "group" if world > 1 or devices else "ranks"
+
+
+def group_devices(devices: str, gpus: int, world: int) -> list[int]:
+    """Member devices of the group: the list given, else 0..N-1 with N the
+    larger of --gpus and the launcher's world size."""
+    if devices:
+        out = [int(x) for x in devices.split(",") if x.strip() != ""]
+        if not out or min(out) < 0:
+            raise SystemExit(f"bad --devices {devices!r}")
+        return out
+    return list(range(max(gpus, world, 1)))
+
+
+def group_mode(args, world, rank):
+    """Config E through the C ABI's own batch split (include/tlsgpu.h
+    tlsgpu_group_*, talos_amd/csrc/group.cpp): ONE process creates a group of
+    N member engines (one per device), member k builds shard k of config E's
+    batch in its own HBM (talos_amd.workload, global record indices, as
+    tests/golden/batch_digests.json E_shard<k> pins), the session table is
+    replicated on every member (tlsgpu_group_sessions_install), and each step
+    is one tlsgpu_group_open_batch — every member's open launched on its own
+    stream from the caller's thread — joined by tlsgpu_group_sync.  Under
+    torch.distributed.run (N ranks) rank 0 drives the whole group and the
+    other ranks only join the gloo barrier (they never touch a GPU)."""
+    import talos_amd as ta
+    from talos_amd.dist import ControlPlane, shard_by_bytes
+    from talos_amd.workload import Workload, session_plan
+
+    cp = ControlPlane(world)
+    if rank != 0:
+        cp.barrier()
+        cp.close()
+        return
+    ta.load_library()
+    devices = group_devices(args.devices, args.gpus, world)
+    n = len(devices)
+    cfg = "E" if args.config in ("B", "E") else args.config
+    if cfg != "E":
+        raise SystemExit("--split group runs config E (configs[4]) only")
+    kind_name, per_gpu, sessions, rec_len, seed, op = CONFIGS[cfg]
+    if args.records:
+        per_gpu = args.records
+    kind = ta.AEAD_NAMES[kind_name]
+    shards = max(E_GPUS, n)
+    glob = np.full(shards * per_gpu, rec_len, dtype=np.int64)
+    g = ta.Group(devices)
+    members = [ta.Engine.member(g, k) for k in range(n)]
+    wls = []
+    for k in range(n):
+        lo, hi = shard_by_bytes(glob, shards, k)
+        wls.append(Workload(members[k], kind, shards * per_gpu, shards * sessions, seed,
+                            record_len=rec_len, tamper_every=1024, shard=(lo, hi)))
+    # the group's session table, replicated on every member: every session the
+    # members' shards use, at its global id
+    n_sess = max(wl.s0 + wl.S for wl in wls)
+    params = session_plan(kind, shards * per_gpu, shards * sessions, seed)[0][:n_sess]
+    gs = ta.GroupSessionTable(g, n_sess)
+    gs.install(0, params)
+    shard_arr = np.zeros(n, dtype=ta.SHARD_DTYPE)
+    d_descs = []
+    for k, wl in enumerate(wls):
+        opn = wl.d_open.download().view(ta.RECORD_DTYPE).copy()
+        opn["session"] += np.uint32(wl.s0)     # workload-local ids -> global ids
+        d = ta.DeviceBuffer(members[k], opn.nbytes)
+        d.upload(opn.view(np.uint8))
+        d_descs.append(d)
+        shard_arr[k] = (d.ptr, wl.n, 0, wl.d_body.ptr, wl.d_body.nbytes, wl.d_out.ptr,
+                        wl.d_out.nbytes, wl.d_status.ptr)
+        hints = 0 if args.no_hints else ta.batch_hints(
+            wl.lengths + ta.EXPLICIT_NONCE_LEN[kind] + ta.TAG_LEN, wl.session, seal=False)
+        ta._check(g.lib.tlsgpu_sessions_hint(g.lib.tlsgpu_group_sessions_member(gs.handle, k),
+                                             hints), "tlsgpu_sessions_hint")
+    for _ in range(max(1, args.warmup)):
+        gs.batch(shard_arr, seal=False)
+    g.sync()
+    for wl in wls:
+        wl.verify_open()
+    evs = [(ta.Event(m), ta.Event(m)) for m in members]
+    g.sync()
+    t0 = time.perf_counter()
+    for e0, _ in evs:
+        e0.record()
+    for _ in range(args.steps):
+        gs.batch(shard_arr, seal=False)
+    for _, e1 in evs:
+        e1.record()
+    g.sync()
+    wall_s = time.perf_counter() - t0
+    dev_ms = [e0.elapsed_ms(e1) for e0, e1 in evs]
+    for wl in wls:
+        wl.verify_open()
+    total_len = sum(int(wl.lengths.sum()) for wl in wls)
+    value = total_len * args.steps / wall_s / GIB
+    per_launch_s = max(dev_ms) / 1e3 / args.steps
+    algo = sum(algo_bytes_per_record(kind_name, int(l), op) for l in wls[0].lengths.tolist())
+    algo_rd = sum(algo_bytes_per_record(kind_name, int(l), op, True)
+                  for l in wls[0].lengths.tolist())
+    kernel = main_kernel(kind_name, op, False, False, wls[0].n)
+    traffic, traffic_src = load_traffic("B", kernel)
+    line = {
+        "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": n,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(wall_s * 1e3 / args.steps, 4),
+        "member_device_ms_per_step": [round(x / args.steps, 4) for x in dev_ms],
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (counter-SplitMix64 plaintexts sealed on device; 1/1024 tampered)",
+        "config": {"workload": f"config E: {kind_name} TLS 1.2 record open, 16 KiB records, "
+                               f"{per_gpu} records/GPU, device-resident; shards 0..{n - 1} of "
+                               f"one {shards * per_gpu}-record batch (seed {seed:#x}, "
+                               f"{shards * sessions} sessions)",
+                   "records_per_gpu": per_gpu, "sessions_per_gpu": sessions,
+                   "devices": devices, "split": "tlsgpu_group_open_batch (C ABI, group.cpp): "
+                   "one process, one member engine per device, replicated session table",
+                   "payload_bytes_per_gpu": int(wls[0].lengths.sum()),
+                   "parallelism": f"batch split x{n} (tlsgpu_group)"},
+        "roofline": {"bound": "hbm", "achieved": round(algo / per_launch_s / 1e9, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(algo / per_launch_s / 1e9 / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "algorithmic_bytes_per_launch": algo,
+                     "read_achieved": round(algo_rd / per_launch_s / 1e9, 1),
+                     "read_frac": round(algo_rd / per_launch_s / 1e9 / HBM_PEAK_GBS, 4),
+                     "kernel": kernel, "traffic_source": traffic_src,
+                     "timing": "per GPU: HIP events on the slowest member's stream; value: "
+                               "wall clock around the K group calls + tlsgpu_group_sync"},
+    }
+    if n == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(kind_name, rec_len, op)
+    print(json.dumps(line), flush=True)
+    for e0, e1 in evs:
+        e0.close()
+        e1.close()
+    for d in d_descs:
+        d.free()
+    for wl in wls:
+        wl.free()
+    gs.close()
+    g.close()
+    cp.barrier()
+    cp.close()
 
 
 def copy_mode(args, eng):

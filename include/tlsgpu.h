@@ -217,6 +217,7 @@ int tlsgpu_deliver_host(tlsgpu_sessions *t, const tlsgpu_record *d_recs, const i
 /* Write hook over host application data before the caller uploads it for
  * tlsgpu_seal_wire: every fragment of every stream (h_streams: host copy of
  * the write streams, offsets into h_data), in place, lengths unchanged. */
+struct tlsgpu_write_stream; /* defined below, with tlsgpu_seal_wire */
 int tlsgpu_hook_write_streams(tlsgpu_sessions *t, const struct tlsgpu_write_stream *h_streams,
     uint32_t n_streams, uint8_t *h_data, size_t data_bytes);
 /* read / write hook invocations since load (from the patched record layer
@@ -425,6 +426,18 @@ int tlsgpu_evp_batch_stats(uint64_t *batches, uint64_t *jobs);
  * not), process-wide since load.  Lets a caller that interposed the library
  * under an unchanged libssl check that every TLS record went through it. */
 int tlsgpu_evp_call_stats(uint64_t *seal_calls, uint64_t *open_calls);
+/* Test support.  tlsgpu_evp_context_slot: the session table and slot that hold
+ * a live EVP context's device key material.  tlsgpu_sessions_debug_read: after
+ * every queued install / scrub of `slot` has finished, copy its first n bytes
+ * (DevSession, then the GCM tables) to host memory — EVP_AEAD_CTX_cleanup
+ * scrubs the slot asynchronously, and this shows the scrub happened.  (The key
+ * also travels to the install kernel as a kernel argument, in the HIP
+ * runtime's argument buffer, which later launches overwrite but nothing
+ * zeroes: DESIGN.md §4.7.) */
+struct evp_aead_ctx_st; /* EVP_AEAD_CTX, include/tlsgpu_evp.h */
+int tlsgpu_evp_context_slot(const struct evp_aead_ctx_st *ctx, tlsgpu_sessions **sessions,
+    uint32_t *slot);
+int tlsgpu_sessions_debug_read(tlsgpu_sessions *t, uint32_t slot, uint8_t *out, size_t n);
 /* The EVP surface's GPUs.  TLSGPU_DEVICES=a,b,... (a device may repeat: two
  * engines on one GPU) or TLSGPU_DEVICE=d pin them; by default every visible
  * GPU.  EVP_AEAD_CTX_init gives new contexts (and EVP_CIPHER contexts their

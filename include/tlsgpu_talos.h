@@ -15,8 +15,18 @@
  * _ssl_write also accept the BY-VALUE length the patched s3_pkt.c passes
  * (s3_pkt.c.patch:13-14 declares `unsigned int len`, the interface
  * `unsigned int *len`); the reference forwards that value as a pointer and a
- * module that reads *len faults.  A "pointer" below 64 KiB is taken as the
- * length itself (talos_amd/csrc/talos_hooks.cpp).
+ * module that reads *len faults.  How the third argument of these two entry
+ * points is read is PROCESS-WIDE, chosen by the environment variable
+ * TLSGPU_TALOS_LEN at load time (talos_amd/csrc/talos_hooks.cpp):
+ *   "value"   always the by-value length (low 32 bits of the argument) — the
+ *             setting for the TaLoS-patched record layer;
+ *   "pointer" always a pointer, as declared;
+ *   unset     a "pointer" below 64 KiB is taken as the length itself.  This
+ *             relies on the caller zero-extending the 32-bit length into the
+ *             64-bit argument register (gcc and clang do; the x86-64 SysV ABI
+ *             leaves those bits undefined), so use "value" with a patched tree
+ *             built by any other compiler.
+ * The engine's own host paths always hand the callbacks real pointers.
  */
 #ifndef TLSGPU_TALOS_H
 #define TLSGPU_TALOS_H

@@ -155,6 +155,8 @@ def load_library(path: str = LIBPATH) -> C.CDLL:
         "tlsgpu_evp_set_batching": (i32, [C.c_uint, C.c_uint, C.c_uint]),
         "tlsgpu_evp_batch_stats": (i32, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "tlsgpu_evp_call_stats": (i32, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+        "tlsgpu_evp_context_slot": (i32, [vp, C.POINTER(C.c_void_p), C.POINTER(C.c_uint32)]),
+        "tlsgpu_sessions_debug_read": (i32, [vp, u32, vp, C.c_size_t]),
         "tlsgpu_evp_device_count": (u32, []),
         "tlsgpu_evp_device_stats": (i32, [u32, C.POINTER(i32), C.POINTER(C.c_uint64),
                                           C.POINTER(C.c_uint64)]),
@@ -229,6 +231,18 @@ class Engine:
         _check(self.lib.tlsgpu_engine_create(device, C.byref(h)), "tlsgpu_engine_create")
         self.handle = h
         self.device = device
+        self._owned = True
+
+    @classmethod
+    def member(cls, group: "Group", k: int) -> "Engine":
+        """Member k's engine of a Group (tlsgpu_group_engine).  The group owns
+        it: close() leaves it alone, tlsgpu_group_destroy frees it."""
+        h = group.lib.tlsgpu_group_engine(group.handle, k)
+        if not h:
+            raise TlsGpuError(f"group has no member {k}")
+        e = cls.__new__(cls)
+        e.lib, e.handle, e.device, e._owned = group.lib, C.c_void_p(h), -1, False
+        return e
 
     @property
     def stream(self) -> int:
@@ -261,9 +275,9 @@ class Engine:
                "tlsgpu_fill_synthetic_spans")
 
     def close(self) -> None:
-        if self.handle:
+        if self.handle and getattr(self, "_owned", True):
             self.lib.tlsgpu_engine_destroy(self.handle)
-            self.handle = None
+        self.handle = None
 
 
 class DeviceBuffer:
@@ -378,7 +392,10 @@ HINT_NO_SHORT_RECORDS, HINT_SESSION_RUNS = 1, 2
 
 def batch_hints(lengths, sessions, seal: bool) -> int:
     """The hints a caller that built the batch can state (tlsgpu.h): no GCM
-    record short enough for a pack, session runs of >= 12 records on average."""
+    record short enough for a pack, session runs of >= 12 records on average.
+    `lengths` are the descriptors' length fields, as the engine's host_hints
+    reads them: fragment lengths (explicit nonce + ciphertext + tag) for an
+    open, plaintext lengths for a seal."""
     lengths = np.asarray(lengths)
     sessions = np.asarray(sessions)
     short_max = 992 if seal else 992 + 8 + 16

@@ -55,6 +55,12 @@ static int fail(int code, const char* fmt, ...) {
 
 extern "C" const char* tlsgpu_last_error(void) { return g_err; }
 
+// For group.cpp (same library, not exported): set the calling thread's
+// tlsgpu_last_error, e.g. to a member worker's reason.
+extern "C" int tg_internal_set_error(int code, const char* msg) {
+  return fail(code, "%s", msg ? msg : "");
+}
+
 // ---------------------------------------------------------------------------
 // engine / sessions
 // Per-stream scratch for the per-record constants (RecPre) of the queue
@@ -396,10 +402,12 @@ static uint32_t g_bs16_min = []() {
   return v ? (uint32_t)strtoul(v, nullptr, 0) : 0u;
 }();
 
-// Queue kernel: short-record packs (gcm_pack).  Env TLSGPU_PACK=0 turns them off.
-static uint32_t g_pack = []() {
+// Queue kernel: short-record packs (gcm_pack).  Env TLSGPU_PACK=0 turns them
+// off, =1 keeps them on even when the caller hints NO_SHORT_RECORDS; unset
+// (-1): on unless hinted off.
+static int g_pack = []() {
   const char* v = getenv("TLSGPU_PACK");
-  return v ? (uint32_t)strtoul(v, nullptr, 0) : 1u;
+  return v && *v ? (int)strtol(v, nullptr, 0) : -1;
 }();
 
 // Per-wave-session kernel (gcm_pw.hip): env TLSGPU_PWS=0 never, 1 always,
@@ -442,7 +450,7 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   a.bs16_min = g_bs16_min;
   // batch-shape hints rule out the kernels the device would not select
   // (tlsgpu_sessions_hint); the TLSGPU_PACK / TLSGPU_PWS overrides win
-  a.pack = (hints & TLSGPU_HINT_NO_SHORT_RECORDS) ? 0u : g_pack;
+  a.pack = g_pack >= 0 ? (uint32_t)g_pack : (hints & TLSGPU_HINT_NO_SHORT_RECORDS) ? 0u : 1u;
   a.pws = (g_pws == 0 && (hints & TLSGPU_HINT_SESSION_RUNS)) ? 1u : g_pws;
   int groups = groups_for(t->eng, n, &a.records_per_group);
   const int sel_impl = g_gcm_impl.load();
@@ -1496,6 +1504,31 @@ extern "C" void EVP_AEAD_CTX_cleanup(EVP_AEAD_CTX* ctx) {
   }
   ctx->aead_state = nullptr;
   ctx->aead = nullptr;
+}
+
+// Test support (include/tlsgpu.h): where a live EVP context's key material
+// sits, and the bytes of a session slot once every queued install / scrub of
+// that slot has finished — so a test can check that EVP_AEAD_CTX_cleanup's
+// asynchronous scrub really zeroes the device copy (e_aes.c:1415-1422).
+extern "C" int tlsgpu_evp_context_slot(const EVP_AEAD_CTX* ctx, tlsgpu_sessions** sessions,
+                                       uint32_t* slot) {
+  const auto* st = ctx ? (const AeadState*)ctx->aead_state : nullptr;
+  if (!st || !sessions || !slot) return fail(TLSGPU_EINVAL, "no live EVP context");
+  *sessions = st->sess;
+  *slot = st->slot;
+  return TLSGPU_OK;
+}
+
+extern "C" int tlsgpu_sessions_debug_read(tlsgpu_sessions* t, uint32_t slot, uint8_t* out,
+                                          size_t n) {
+  if (!t || !out || slot >= t->capacity || n > sizeof(DevSession) + sizeof(DevGcmTables))
+    return fail(TLSGPU_EINVAL, "bad slot read");
+  HIPCHK(hipSetDevice(t->eng->device));
+  if (const hipEvent_t ev = slot_event(t, slot)) HIPCHK(hipEventSynchronize(ev));
+  const size_t a = std::min(n, sizeof(DevSession));
+  HIPCHK(hipMemcpy(out, t->d_sess + slot, a, hipMemcpyDeviceToHost));
+  if (n > a) HIPCHK(hipMemcpy(out + a, t->d_gcm + slot, n - a, hipMemcpyDeviceToHost));
+  return TLSGPU_OK;
 }
 
 static int check_alias(const unsigned char* in, size_t in_len, const unsigned char* out) {

@@ -23,6 +23,9 @@
 
 #include "../../include/tlsgpu.h"
 
+// engine.cpp: sets the calling thread's tlsgpu_last_error (not exported)
+extern "C" int tg_internal_set_error(int code, const char* msg);
+
 namespace {
 
 // A worker thread that runs one job at a time for its member.
@@ -33,6 +36,7 @@ struct Worker {
   std::function<int()> job;
   bool has_job = false, done = false, quit = false;
   int rc = TLSGPU_OK;
+  char err[256] = "";  // the job's tlsgpu_last_error (thread-local to this worker)
 
   void loop() {
     std::unique_lock<std::mutex> lk(mu);
@@ -43,6 +47,7 @@ struct Worker {
       has_job = false;
       lk.unlock();
       const int r = f();
+      if (r != TLSGPU_OK) snprintf(err, sizeof(err), "%s", tlsgpu_last_error());
       lk.lock();
       rc = r;
       done = true;
@@ -76,12 +81,8 @@ struct tlsgpu_group_sessions {
   std::vector<tlsgpu_sessions*> members;
 };
 
-static int gfail(int code, const char* what) {
-  // the member's own tlsgpu_last_error is thread-local to its worker; keep the
-  // group-level reason on the caller's thread
-  (void)what;
-  return code;
-}
+// A group-level failure: the reason goes to the caller's tlsgpu_last_error.
+static int gfail(int code, const char* what) { return tg_internal_set_error(code, what); }
 
 extern "C" int tlsgpu_group_create(const int* devices, uint32_t n, tlsgpu_group** out) {
   if (!out) return TLSGPU_EINVAL;
@@ -137,7 +138,7 @@ extern "C" tlsgpu_engine* tlsgpu_group_engine(tlsgpu_group* g, uint32_t member) 
 
 extern "C" int tlsgpu_group_sessions_create(tlsgpu_group* g, uint32_t capacity,
                                             tlsgpu_group_sessions** out) {
-  if (!g || !out || capacity == 0) return TLSGPU_EINVAL;
+  if (!g || !out || capacity == 0) return gfail(TLSGPU_EINVAL, "group sessions: bad arguments");
   *out = nullptr;
   auto* gs = new (std::nothrow) tlsgpu_group_sessions();
   if (!gs) return TLSGPU_ENOMEM;
@@ -174,14 +175,19 @@ static int run_members(tlsgpu_group* g, const std::function<int(uint32_t)>& f) {
   int rc = TLSGPU_OK;
   for (uint32_t k = 0; k < m; k++) {
     const int r = g->workers[k]->wait();
-    if (rc == TLSGPU_OK && r != TLSGPU_OK) rc = r;
+    if (rc == TLSGPU_OK && r != TLSGPU_OK) {
+      // the member worker's reason, carried to the caller's thread
+      char msg[300];
+      snprintf(msg, sizeof(msg), "group member %u: %s", k, g->workers[k]->err);
+      rc = tg_internal_set_error(r, msg);
+    }
   }
   return rc;
 }
 
 extern "C" int tlsgpu_group_sessions_install(tlsgpu_group_sessions* gs, uint32_t first, uint32_t n,
                                              const tlsgpu_session_params* params) {
-  if (!gs || (!params && n)) return TLSGPU_EINVAL;
+  if (!gs || (!params && n)) return gfail(TLSGPU_EINVAL, "group install: bad arguments");
   std::lock_guard<std::mutex> lk(gs->g->mu);
   return run_members(gs->g, [&](uint32_t k) {
     return tlsgpu_sessions_install(gs->members[k], first, n, params);
@@ -190,7 +196,7 @@ extern "C" int tlsgpu_group_sessions_install(tlsgpu_group_sessions* gs, uint32_t
 
 extern "C" int tlsgpu_split_by_bytes(const tlsgpu_record* recs, uint32_t n, uint32_t parts,
                                      uint32_t* cuts) {
-  if (!cuts || parts == 0 || (n && !recs)) return TLSGPU_EINVAL;
+  if (!cuts || parts == 0 || (n && !recs)) return gfail(TLSGPU_EINVAL, "split_by_bytes: bad arguments");
   // prefix sums in 64 bits; cut k = first i with prefix[i] * parts >= total * k
   // (unsigned __int128 keeps the products exact for any byte total)
   unsigned __int128 total = 0;
@@ -216,7 +222,8 @@ extern "C" int tlsgpu_split_by_bytes(const tlsgpu_record* recs, uint32_t n, uint
 static int group_host(tlsgpu_group_sessions* gs, bool seal, const tlsgpu_record* h_recs,
                       uint32_t n, const uint8_t* h_in, size_t in_bytes, uint8_t* h_out,
                       size_t out_bytes, int32_t* h_status) {
-  if (!gs || (n && (!h_recs || !h_in || !h_out || !h_status))) return TLSGPU_EINVAL;
+  if (!gs || (n && (!h_recs || !h_in || !h_out || !h_status)))
+    return gfail(TLSGPU_EINVAL, "group host batch: null buffer");
   if (n == 0) return TLSGPU_OK;
   tlsgpu_group* g = gs->g;
   const uint32_t m = (uint32_t)g->engines.size();
@@ -258,7 +265,7 @@ extern "C" int tlsgpu_group_seal_host(tlsgpu_group_sessions* gs, const tlsgpu_re
 // Device-resident: launches are asynchronous, so the caller's thread issues
 // every member's batch on that member's engine stream back to back.
 static int group_batch(tlsgpu_group_sessions* gs, bool seal, const tlsgpu_shard* shards) {
-  if (!gs || !shards) return TLSGPU_EINVAL;
+  if (!gs || !shards) return gfail(TLSGPU_EINVAL, "group batch: null sessions or shards");
   tlsgpu_group* g = gs->g;
   std::lock_guard<std::mutex> lk(g->mu);
   int rc = TLSGPU_OK;

@@ -27,13 +27,27 @@
 // *len` and hands it to the callback, which logpoint-style modules
 // dereference: the reference's nosgx build crashes as soon as such a module is
 // registered (reproduced by tests/test_talos_hooks.py with the CPU build).
-// Here a "pointer" below 64 KiB — never a valid user-space address
-// (vm.mmap_min_addr), always a TLS record length (<= 18 KiB) — is taken as
-// the by-value length and the callback gets a pointer to a copy.
+// What tls_processing_ssl_read/_write make of their third argument is a
+// process-wide setting, TLSGPU_TALOS_LEN (read once at load):
+//   "value"   — always the by-value length: the low 32 bits of the argument
+//               (the upper half of a 32-bit argument register is undefined in
+//               the x86-64 SysV ABI, so only the low half is read).  For the
+//               TaLoS-patched record layer.
+//   "pointer" — always a pointer (the interface as declared).
+//   unset / "auto" — a "pointer" whose value is below 64 KiB (never a mapped
+//               user address, vm.mmap_min_addr; a TLS record length is <= 18
+//               KiB) is taken as the length.  This relies on the caller
+//               zero-extending the 32-bit length into the register, which gcc
+//               and clang do in practice but the ABI does not promise: set
+//               "value" for a patched tree built by another compiler.
+// The engine's own host-delivery paths (tg::talos_read / talos_write below)
+// always pass real pointers and are not affected by the setting.
 #include <dlfcn.h>
 
 #include <atomic>
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
 
 #include "tlsgpu_internal.h"
 
@@ -49,11 +63,21 @@ std::atomic<type_cb> g_type{nullptr};
 std::atomic<conn_cb> g_new{nullptr}, g_free{nullptr};
 std::atomic<uint64_t> g_read_calls{0}, g_write_calls{0};
 
-void call_rw(rw_cb cb, const SSL* s, char* data, unsigned int* len) {
+enum LenMode { LEN_AUTO, LEN_VALUE, LEN_POINTER };
+const LenMode g_len_mode = [] {
+  const char* v = getenv("TLSGPU_TALOS_LEN");
+  if (v && !strcmp(v, "value")) return LEN_VALUE;
+  if (v && !strcmp(v, "pointer")) return LEN_POINTER;
+  return LEN_AUTO;
+}();
+
+// external: a call from the (patched) record layer, whose third argument may
+// be the by-value length (see above); the engine's own calls pass pointers.
+void call_rw(rw_cb cb, const SSL* s, char* data, unsigned int* len, bool external) {
   if (!cb) return;
   const uintptr_t v = reinterpret_cast<uintptr_t>(len);
-  if (v < 65536) {  // s3_pkt.c.patch's by-value length (see above)
-    unsigned int n = static_cast<unsigned int>(v);
+  if (external && (g_len_mode == LEN_VALUE || (g_len_mode == LEN_AUTO && v < 65536))) {
+    unsigned int n = static_cast<unsigned int>(v & 0xFFFFFFFFu);
     cb(s, data, &n);
   } else {
     cb(s, data, len);
@@ -76,11 +100,11 @@ void ecall_tls_processing_module_init(void) {
 
 void tls_processing_ssl_read(const SSL* s, char* data, unsigned int* len) {
   g_read_calls.fetch_add(1, std::memory_order_relaxed);
-  call_rw(g_read.load(), s, data, len);
+  call_rw(g_read.load(), s, data, len, true);
 }
 void tls_processing_ssl_write(const SSL* s, char* data, unsigned int* len) {
   g_write_calls.fetch_add(1, std::memory_order_relaxed);
-  call_rw(g_write.load(), s, data, len);
+  call_rw(g_write.load(), s, data, len, true);
 }
 void tls_processing_set_ssl_type(const void* b, const long type) {
   if (type_cb cb = g_type.load()) cb(b, type);
@@ -104,9 +128,11 @@ namespace tg {
 bool talos_read_hooked() { return g_read.load() != nullptr; }
 bool talos_write_hooked() { return g_write.load() != nullptr; }
 void talos_read(const void* ssl, uint8_t* data, uint32_t* len) {
-  tls_processing_ssl_read(static_cast<const SSL*>(ssl), reinterpret_cast<char*>(data), len);
+  g_read_calls.fetch_add(1, std::memory_order_relaxed);
+  call_rw(g_read.load(), static_cast<const SSL*>(ssl), reinterpret_cast<char*>(data), len, false);
 }
 void talos_write(const void* ssl, uint8_t* data, uint32_t* len) {
-  tls_processing_ssl_write(static_cast<const SSL*>(ssl), reinterpret_cast<char*>(data), len);
+  g_write_calls.fetch_add(1, std::memory_order_relaxed);
+  call_rw(g_write.load(), static_cast<const SSL*>(ssl), reinterpret_cast<char*>(data), len, false);
 }
 }  // namespace tg

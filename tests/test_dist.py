@@ -71,3 +71,24 @@ def test_gloo_world2_control_plane():
     assert [r[1] for r in res] == [[2.0, 10.0], [2.0, 10.0]]
     assert [r[2] for r in res] == [[1.0], [1.0]]
     assert [(r[3], r[4]) for r in res] == [(0, 500), (500, 1000)]
+
+
+def test_bench_split_plumbing():
+    """bench.py's multi-GPU split choice and group member list (no GPU): N > 1
+    ranks or an explicit device list measure the C ABI's tlsgpu_group split."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "bench", os.path.join(os.path.dirname(os.path.dirname(__file__)), "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench.choose_split(None, 1, "") == "ranks"
+    assert bench.choose_split(None, 8, "") == "group"
+    assert bench.choose_split(None, 1, "0,0") == "group"
+    assert bench.choose_split("ranks", 8, "") == "ranks"
+    assert bench.choose_split("group", 1, "") == "group"
+    assert bench.group_devices("", 1, 1) == [0]
+    assert bench.group_devices("", 4, 1) == [0, 1, 2, 3]
+    assert bench.group_devices("", 1, 8) == list(range(8))
+    assert bench.group_devices("0,0", 1, 1) == [0, 0]
+    with pytest.raises(SystemExit):
+        bench.group_devices("-1", 1, 1)

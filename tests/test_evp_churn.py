@@ -79,3 +79,37 @@ def test_evp_context_churn(batch_us):
     r = subprocess.run([sys.executable, "-c", _CHILD, ROOT], env=env, capture_output=True,
                        text=True, timeout=150)
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+_SCRUB_CHILD = r"""
+import ctypes as C, os, sys
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, os.path.join(sys.argv[1], "oracle"))
+import talos_amd as ta, pyoracle as po
+lib = ta.load_library()
+for kind in (po.AES_128_GCM, po.AES_256_GCM, po.CHACHA20_POLY1305):
+    key = bytes(range(1, 1 + po.KEY_LEN[kind]))
+    ctx = ta.EvpAead(kind, key)
+    assert ctx.ok == 1
+    ok, ct, _ = ctx.seal(bytes(12), b"x" * 100, b"")
+    assert ok == 1
+    t, slot = C.c_void_p(), C.c_uint32()
+    assert lib.tlsgpu_evp_context_slot(C.byref(ctx.ctx), C.byref(t), C.byref(slot)) == 0
+    n = 1024 + 4096
+    live = (C.c_uint8 * n)()
+    assert lib.tlsgpu_sessions_debug_read(t, slot.value, live, n) == 0
+    assert any(bytes(live)), "installed slot reads all zero"
+    ctx.cleanup()          # returns before the scrub has run on the device
+    after = (C.c_uint8 * n)()
+    assert lib.tlsgpu_sessions_debug_read(t, slot.value, after, n) == 0
+    assert not any(bytes(after)), (kind, "key material left after cleanup")
+print("SCRUBBED")
+"""
+
+
+def test_evp_cleanup_scrubs_device_key():
+    """EVP_AEAD_CTX_cleanup's asynchronous scrub (explicit_bzero analogue,
+    e_aes.c:1415-1422): once the slot's queued work has finished, the context's
+    DevSession and GCM tables read back as zeros."""
+    r = subprocess.run([sys.executable, "-c", _SCRUB_CHILD, ROOT], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0 and "SCRUBBED" in r.stdout, r.stdout + r.stderr

@@ -241,3 +241,47 @@ def test_host_pipeline_failure_drains(ta, tmp_path):
     r = subprocess.run([sys.executable, "-c", _FAIL_CHILD, ROOT], env=env, capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0 and "DRAINED" in r.stdout, r.stdout + r.stderr
+
+
+_GROUP_FAIL_CHILD = r"""
+import ctypes as C, sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import talos_amd as ta
+g = ta.Group([0, 0])
+gs = ta.GroupSessionTable(g, 1)
+gs.install(0, [ta.SessionParams(ta.AES_128_GCM, bytes(range(16)), bytes(4))])
+eng = g.lib.tlsgpu_group_engine(g.handle, 0)
+n, L = 512, 16384
+keep = []
+def pinned(nb):
+    p = C.c_void_p(); assert g.lib.tlsgpu_host_alloc(eng, nb, C.byref(p)) == 0
+    keep.append(p.value); return p.value
+h_in, h_out, h_recs, h_st = pinned(n * L), pinned(n * (L + 64)), pinned(32 * n), pinned(4 * n)
+d = np.zeros(n, dtype=ta.RECORD_DTYPE)
+d["in_off"] = np.arange(n) * L; d["out_off"] = np.arange(n) * (L + 64); d["seq"] = np.arange(n)
+d["len_type"] = ta.len_type(L, 23)
+C.memmove(h_recs, d.tobytes(), d.nbytes)
+assert g.lib.tlsgpu_host_pipeline(eng, 2, 1 << 20) == 0
+try:   # group-level argument failure
+    gs.seal_host(h_recs, n, h_in, n * L, h_in, n * L, h_st)
+    print("NO-ERROR-1")
+except ta.TlsGpuError as exc:
+    assert "in place" in str(exc), exc
+try:   # a member's failure (on its worker thread) reaches this thread
+    gs.seal_host(h_recs, n, h_in, n * L, h_out, n * (L + 64), h_st)
+    print("NO-ERROR-2")
+except ta.TlsGpuError as exc:
+    assert "group member" in str(exc) and "injected" in str(exc), exc
+    print("REASONS-OK")
+"""
+
+
+@pytest.mark.gpu
+def test_group_errors_reach_caller(ta):
+    """tlsgpu_last_error on the caller's thread carries the reason of a failed
+    group call: a group-level argument check and a member's failure on its
+    worker thread."""
+    env = dict(os.environ, TLSGPU_TEST_HOST_FAIL_CHUNK="2")
+    r = subprocess.run([sys.executable, "-c", _GROUP_FAIL_CHILD, ROOT], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "REASONS-OK" in r.stdout, r.stdout + r.stderr

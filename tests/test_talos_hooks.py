@@ -85,6 +85,43 @@ def test_registry_by_value_and_pointer_lengths(ta):
         del cbs
 
 
+_LEN_MODE_CHILD = r"""
+import ctypes as C, sys
+sys.path.insert(0, sys.argv[1])
+import talos_amd as ta
+lib = ta.load_library()
+seen = []
+def on_read(ssl, data, plen):
+    seen.append(plen[0])
+cbs = ta.talos_register(on_read, None)
+fn = lib.tls_processing_ssl_read
+fn.restype = None
+fn.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+buf = C.create_string_buffer(64)
+n = C.c_uint(16)
+if sys.argv[2] == "value":
+    # by-value length with junk in the upper half of the register: only the low
+    # 32 bits count
+    fn(1, buf, (0xDEADBEEF << 32) | 7)
+    fn(1, buf, 9)
+else:
+    fn(1, buf, C.addressof(n))
+print(seen)
+"""
+
+
+@pytest.mark.parametrize("mode,want", [("value", "[7, 9]"), ("pointer", "[16]")])
+def test_talos_len_mode_setting(mode, want):
+    """TLSGPU_TALOS_LEN=value reads the low 32 bits of the third argument as the
+    length (the patched record layer, any compiler); =pointer always dereferences
+    it (tlsgpu_talos.h, process-wide)."""
+    env = dict(os.environ, TLSGPU_TALOS_LEN=mode)
+    env.pop("LD_PRELOAD", None)
+    r = subprocess.run([sys.executable, "-c", _LEN_MODE_CHILD, ROOT, mode], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip().splitlines()[-1] == want, r.stdout + r.stderr
+
+
 def test_reference_nosgx_build_faults_with_logging_module():
     """The reference's own interface (tls_processing_interface.c:74-77) forwards
     the patched record layer's by-value length as a pointer; the module's *len
