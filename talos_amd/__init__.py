@@ -156,6 +156,8 @@ def load_library(path: str = LIBPATH) -> C.CDLL:
         "tlsgpu_evp_batch_stats": (i32, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "tlsgpu_evp_call_stats": (i32, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "tlsgpu_evp_context_slot": (i32, [vp, C.POINTER(C.c_void_p), C.POINTER(C.c_uint32)]),
+        "tlsgpu_evp_set_doorbell": (i32, [C.c_uint, C.c_uint]),
+        "tlsgpu_evp_doorbell_stats": (i32, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "tlsgpu_sessions_debug_read": (i32, [vp, u32, vp, C.c_size_t]),
         "tlsgpu_evp_device_count": (u32, []),
         "tlsgpu_evp_device_stats": (i32, [u32, C.POINTER(i32), C.POINTER(C.c_uint64),
@@ -689,6 +691,19 @@ def evp_device_stats() -> list[tuple[int, int, int]]:
                "tlsgpu_evp_device_stats")
         out.append((d.value, c.value, n.value))
     return out
+
+
+def evp_set_doorbell(groups: int, lifetime_ms: int = 0) -> None:
+    """Per-call AES-GCM EVP jobs through resident server workgroups
+    (tlsgpu_evp_set_doorbell); before the first EVP call."""
+    _check(load_library().tlsgpu_evp_set_doorbell(groups, lifetime_ms), "tlsgpu_evp_set_doorbell")
+
+
+def evp_doorbell_stats() -> tuple[int, int]:
+    j, l = C.c_uint64(), C.c_uint64()
+    _check(load_library().tlsgpu_evp_doorbell_stats(C.byref(j), C.byref(l)),
+           "tlsgpu_evp_doorbell_stats")
+    return j.value, l.value
 
 
 def evp_batch_stats() -> tuple[int, int]:

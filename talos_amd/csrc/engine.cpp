@@ -24,6 +24,7 @@
 #include <climits>
 #include <deque>
 #include <linux/futex.h>
+#include <sched.h>
 #include <sys/syscall.h>
 #include <thread>
 #include <vector>
@@ -1573,6 +1574,168 @@ static const bool g_evp_zerocopy = [] {
   return !(v && *v == '0');
 }();
 
+// ---------------------------------------------------------------------------
+// Doorbell server (round 4, evp_server.hip): per-call AES-GCM jobs without a
+// kernel launch.  TLSGPU_EVP_DOORBELL=<G> (or tlsgpu_evp_set_doorbell) keeps G
+// server workgroups resident per EVP device while calls arrive; a calling
+// thread owns one slot of kSlotsPerGroup * G (slot k -> workgroup k % G), posts
+// its job number there and spins on the answer.  An instance lives `lifetime`
+// (TLSGPU_EVP_DOORBELL_MS, default 50 ms) and is relaunched by the first post
+// after half of that has passed, on the same stream: a job is only posted
+// while an instance that still polls for at least half a lifetime is queued or
+// running, so every posted job is served, and a process that stops calling
+// leaves nothing spinning.  ChaCha20-Poly1305 contexts keep the launched path.
+constexpr uint32_t kSlotsPerGroup = 8;
+struct EvpServer {
+  int device = -1;
+  uint32_t groups = 0, nslots = 0;
+  uint64_t lifetime_ns = 0;
+  DoorbellSlot* slots = nullptr;  // pinned host
+  DoorbellSlot* d_slots = nullptr;
+  uint32_t* stop = nullptr;       // pinned host word
+  uint32_t* d_stop = nullptr;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  uint64_t deadline_ns = 0;       // post only before this (host clock), else relaunch
+  std::vector<uint32_t> free_slots;
+  std::atomic<uint64_t> jobs{0}, launches{0};
+};
+static EvpServer* g_servers[kMaxEvpDevices] = {};
+static std::mutex g_server_mu;
+static unsigned g_doorbell_groups = [] {
+  const char* v = getenv("TLSGPU_EVP_DOORBELL");
+  return v && *v ? (unsigned)strtoul(v, nullptr, 10) : 0u;
+}();
+static unsigned g_doorbell_ms = [] {
+  const char* v = getenv("TLSGPU_EVP_DOORBELL_MS");
+  const unsigned ms = v && *v ? (unsigned)strtoul(v, nullptr, 10) : 50u;
+  return ms ? ms : 50u;
+}();
+
+static uint64_t mono_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// stop every server at exit: one host store each (no HIP call: the runtime
+// may already be going away); an instance exits within one poll
+static void servers_stop_at_exit() {
+  for (EvpServer* sv : g_servers)
+    if (sv && sv->stop) __atomic_store_n(sv->stop, 1u, __ATOMIC_RELEASE);
+}
+
+// The server of EVP device k (created on first use when the doorbell is on).
+static EvpServer* evp_server(size_t k, tlsgpu_engine* e) {
+  if (!g_doorbell_groups || k >= (size_t)kMaxEvpDevices) return nullptr;
+  std::lock_guard<std::mutex> lk(g_server_mu);
+  if (g_servers[k]) return g_servers[k]->slots ? g_servers[k] : nullptr;
+  auto* sv = new (std::nothrow) EvpServer();
+  if (!sv) return nullptr;
+  g_servers[k] = sv;  // a failed setup stays registered (slots == nullptr): not retried
+  sv->device = e->device;
+  sv->groups = std::min(g_doorbell_groups, 256u);
+  sv->nslots = sv->groups * kSlotsPerGroup;
+  sv->lifetime_ns = (uint64_t)g_doorbell_ms * 1000000ull;
+  DoorbellSlot* h = nullptr;
+  uint32_t* stop = nullptr;
+  if (hipSetDevice(e->device) != hipSuccess ||
+      hipHostMalloc((void**)&h, sizeof(DoorbellSlot) * sv->nslots, hipHostMallocDefault) !=
+          hipSuccess)
+    return nullptr;
+  memset(h, 0, sizeof(DoorbellSlot) * sv->nslots);
+  if (hipHostMalloc((void**)&stop, 128, hipHostMallocDefault) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&sv->d_slots, h, 0) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&sv->d_stop, stop, 0) != hipSuccess ||
+      hipStreamCreateWithFlags(&sv->stream, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipHostFree(h);
+    if (stop) (void)hipHostFree(stop);
+    return nullptr;
+  }
+  *stop = 0;
+  sv->stop = stop;
+  for (uint32_t i = sv->nslots; i-- > 0;) sv->free_slots.push_back(i);
+  sv->slots = h;
+  static std::once_flag once;
+  std::call_once(once, [] { atexit(servers_stop_at_exit); });
+  return sv;
+}
+
+// Launch an instance if the one queued last may stop polling within half a
+// lifetime.  Returns false if the launch failed.
+static bool server_ensure(EvpServer* sv) {
+  const uint64_t now = mono_ns();
+  std::lock_guard<std::mutex> lk(sv->mu);
+  if (now < sv->deadline_ns) return true;
+  if (hipSetDevice(sv->device) != hipSuccess) return false;
+  ServerArgs a;
+  a.slots = sv->d_slots;
+  a.nslots = sv->nslots;
+  a.stop = sv->d_stop;
+  a.lifetime = sv->lifetime_ns / 10;  // 100 MHz realtime ticks
+  if (launch_evp_server(a, (int)sv->groups, sv->stream) != 0) return false;
+  sv->deadline_ns = now + sv->lifetime_ns / 2;
+  sv->launches.fetch_add(1, std::memory_order_relaxed);
+  return true;
+}
+
+// The calling thread's slot on a server (assigned on first use, given back
+// when the thread exits); -1 when all are taken.
+struct ThreadSlots {
+  int slot[kMaxEvpDevices];
+  uint32_t seq[kMaxEvpDevices];
+  ThreadSlots() {
+    for (int& x : slot) x = -2;  // not asked yet
+  }
+  ~ThreadSlots() {
+    for (int k = 0; k < kMaxEvpDevices; k++)
+      if (slot[k] >= 0 && g_servers[k]) {
+        std::lock_guard<std::mutex> lk(g_servers[k]->mu);
+        g_servers[k]->free_slots.push_back((uint32_t)slot[k]);
+      }
+  }
+};
+static thread_local ThreadSlots t_slots;
+
+static DoorbellSlot* thread_slot(EvpServer* sv, size_t k, uint32_t** seq) {
+  int& s = t_slots.slot[k];
+  if (s == -2) {
+    std::lock_guard<std::mutex> lk(sv->mu);
+    if (sv->free_slots.empty()) {
+      s = -1;
+    } else {
+      s = (int)sv->free_slots.back();
+      sv->free_slots.pop_back();
+      // continue the slot's numbering (an earlier thread may have used it)
+      t_slots.seq[k] = __atomic_load_n(&sv->slots[s].done, __ATOMIC_ACQUIRE);
+    }
+  }
+  if (s < 0) return nullptr;
+  *seq = &t_slots.seq[k];
+  return &sv->slots[s];
+}
+
+extern "C" int tlsgpu_evp_set_doorbell(unsigned groups, unsigned lifetime_ms) {
+  std::lock_guard<std::mutex> lk(g_server_mu);
+  for (EvpServer* sv : g_servers)
+    if (sv) return fail(TLSGPU_EINVAL, "the doorbell server is already set up");
+  g_doorbell_groups = groups;
+  if (lifetime_ms) g_doorbell_ms = lifetime_ms;
+  return TLSGPU_OK;
+}
+
+extern "C" int tlsgpu_evp_doorbell_stats(uint64_t* jobs, uint64_t* launches) {
+  uint64_t j = 0, l = 0;
+  for (EvpServer* sv : g_servers)
+    if (sv) {
+      j += sv->jobs.load();
+      l += sv->launches.load();
+    }
+  if (jobs) *jobs = j;
+  if (launches) *launches = l;
+  return TLSGPU_OK;
+}
+
 // One EVP call on the GPU: 1 = success, 0 = authentication failure / rejected
 // by the kernel (output zero-filled), -1 = runtime failure.
 static int gpu_call(const AeadState* st, bool seal, unsigned char* out, size_t* out_len,
@@ -1642,6 +1805,47 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
   // a job the kernel rejects keeps this status (never a stale one)
   *reinterpret_cast<int32_t*>(h + o_status) = TLSGPU_REC_PUBLIC_INVALID;
   if (!zc && hipMemcpyAsync(d, h, o_status + 4, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
+  const bool gcm = st->kind == TLSGPU_AES_128_GCM || st->kind == TLSGPU_AES_256_GCM;
+  // doorbell (zero-copy AES-GCM calls): post the job to a resident server
+  // workgroup instead of launching; the staging buffer is the job's memory
+  if (zc && gcm) {
+    EvpServer* sv = evp_server(st->evp_dev, e);
+    uint32_t* seq = nullptr;
+    DoorbellSlot* slot = sv ? thread_slot(sv, st->evp_dev, &seq) : nullptr;
+    if (slot) {
+      if (st->install_pending.load(std::memory_order_acquire)) {  // the key install
+        if (hipEventSynchronize(st->installed) != hipSuccess) return -1;
+        st->install_pending.store(false, std::memory_order_release);
+      }
+      slot->op = (uint32_t)(seal ? 1 : 0) | ((st->kind == TLSGPU_AES_128_GCM ? 10u : 14u) << 8);
+      slot->n_sessions = st->sess->capacity;
+      slot->job = (uint64_t)d;
+      slot->status = (uint64_t)(d + o_status);
+      slot->sessions = (uint64_t)st->sess->d_sess;
+      slot->gcm_tables = (uint64_t)st->sess->d_gcm;
+      if (!server_ensure(sv)) return -1;
+      const uint32_t n = ++*seq;
+      __atomic_store_n(&slot->post, n, __ATOMIC_RELEASE);
+      const uint64_t t0 = mono_ns();
+      for (uint64_t spins = 1; __atomic_load_n(&slot->done, __ATOMIC_ACQUIRE) != n; spins++) {
+        __builtin_ia32_pause();
+        if ((spins & 1023) == 0) {
+          const uint64_t waited = mono_ns() - t0;
+          if (waited > 10000000000ull) return -1;  // 10 s: the device is gone
+          if (waited > 100000) sched_yield();      // a long job: let others run
+        }
+      }
+      sv->jobs.fetch_add(1, std::memory_order_relaxed);
+      const int32_t status = *reinterpret_cast<const int32_t*>(h + o_status);
+      if (status < 0) {  // the kernel's zero-fill of max_out_len bytes (evp_aead.c:137-143)
+        if (max_out_len) memset(out, 0, max_out_len);
+        return 0;
+      }
+      if (status) memcpy(out, h + o_out, (size_t)status);
+      *out_len = (size_t)status;
+      return 1;
+    }
+  }
   BatchArgs a = {};
   a.sessions = st->sess->d_sess;
   a.gcm_tables = st->sess->d_gcm;
@@ -1650,7 +1854,6 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
   a.records_per_group = 1;
   a.status = reinterpret_cast<int32_t*>(d + o_status);
   a.n_sessions = st->sess->capacity;
-  const bool gcm = st->kind == TLSGPU_AES_128_GCM || st->kind == TLSGPU_AES_256_GCM;
   int rc = gcm ? launch_gcm(a, seal, true, st->kind == TLSGPU_AES_128_GCM ? 10 : 14, 1, s)
                : launch_chacha(a, seal, true, true, true, s);
   if (rc) return -1;

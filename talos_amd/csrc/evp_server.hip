@@ -1,0 +1,112 @@
+// evp_server.hip — persistent "doorbell" server for synchronous per-call
+// EVP_AEAD_CTX_seal/open jobs on AES-GCM contexts.
+//
+// A per-call job (e_aes.c:1424-1510 through evp_aead.c:89-144) is one record,
+// latency-bound: launching a kernel and waiting for it costs 11-12 µs on this
+// box before any cipher work (tools/hip_latency.hip).  With TLSGPU_EVP_DOORBELL
+// set, G workgroups of this kernel stay resident (one per CU, the T-tables
+// loaded into LDS once), each polling the doorbell slots of its calling
+// threads in pinned host memory (slot k belongs to workgroup k % G).  A posted
+// job is the same RawJob the launched path builds in the thread's pinned
+// staging; the workgroup runs it with the launched path's own code
+// (gcm_raw_job, gcm_raw.h), writes output and status straight to the staging
+// buffer and answers in the slot: one PCIe round trip per call, no launch.
+//
+// Coherence: the kernel outlives any one job, so nothing may be served from a
+// cache that a launch would have invalidated.  Session data is read with
+// vector loads (TG_VECTOR_SESSION_LOADS: no scalar-cache copies of a slot's
+// round keys survive the slot's re-keying), and each job starts behind one
+// system-scope acquire fence on wave 0 (vector L1 invalidated) and a barrier.
+// The answer is published by a system-scope release after every wave's
+// stores have completed.
+//
+// Termination: every workgroup exits when the stop word is set or after
+// `lifetime` ticks of the 100 MHz realtime counter, whichever is first; the
+// host relaunches (engine.cpp EvpServer) so that a job is only ever posted
+// while an instance that will poll for at least half a lifetime is queued.
+#define TG_VECTOR_SESSION_LOADS 1
+#include "gcm_raw.h"
+
+namespace tg {
+
+constexpr uint32_t kSrvExit = 0xFFFFFFFFu;
+constexpr uint32_t SRV_SEL_OFF = PLAN_OFF + 16 * 16;  // after gcm_raw_job's part_y words
+
+__device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
+  fill_aes_lds<kThreads>();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t* sel = reinterpret_cast<uint32_t*>(s_lds + SRV_SEL_OFF);
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  // lane l of wave 0 watches slot blockIdx.x + l * gridDim.x; `served` is the
+  // number it last answered (from the slot itself: an earlier instance may
+  // have served it)
+  const uint32_t mine = blockIdx.x + lane * gridDim.x;
+  uint32_t served = 0;
+  if (wave == 0 && mine < s.nslots) served = sys_load(&s.slots[mine].done);
+  for (;;) {
+    if (wave == 0) {
+      uint32_t pick = kSrvExit;
+      for (;;) {
+        const bool ready = mine < s.nslots && sys_load(&s.slots[mine].post) != served;
+        const unsigned long long m = __ballot(ready);
+        if (m) {
+          pick = blockIdx.x + (uint32_t)(__ffsll((long long)m) - 1) * gridDim.x;
+          break;
+        }
+        if (sys_load(s.stop) != 0 || __builtin_amdgcn_s_memrealtime() - t0 > s.lifetime) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (lane == 0) *sel = pick;
+      // the job's fields and data (pinned host memory) and its session (HBM,
+      // installed by another kernel) are read fresh after this
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);
+      __builtin_amdgcn_s_waitcnt(0);
+    }
+    __syncthreads();
+    const uint32_t k = __builtin_amdgcn_readfirstlane(*sel);
+    if (k == kSrvExit) break;
+    DoorbellSlot* sl = s.slots + k;
+    const uint32_t post = __builtin_amdgcn_readfirstlane(sys_load(&sl->post));
+    const uint32_t op = __builtin_amdgcn_readfirstlane(sys_load(&sl->op));
+    BatchArgs a = {};
+    a.sessions = reinterpret_cast<const DevSession*>(__hip_atomic_load(
+        &sl->sessions, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    a.gcm_tables = reinterpret_cast<const DevGcmTables*>(__hip_atomic_load(
+        &sl->gcm_tables, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    a.descs = reinterpret_cast<const void*>(
+        __hip_atomic_load(&sl->job, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    a.status = reinterpret_cast<int32_t*>(
+        __hip_atomic_load(&sl->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    a.n = 1;
+    a.n_sessions = sys_load(&sl->n_sessions);
+    switch (op) {
+      case 10 << 8: gcm_raw_job<false, 10>(a, 0); break;
+      case (10 << 8) | 1: gcm_raw_job<true, 10>(a, 0); break;
+      case 14 << 8: gcm_raw_job<false, 14>(a, 0); break;
+      case (14 << 8) | 1: gcm_raw_job<true, 14>(a, 0); break;
+      default:  // not a job this server runs (the host never posts one)
+        if (threadIdx.x == 0) a.status[0] = TLSGPU_REC_PUBLIC_INVALID;
+        break;
+    }
+    // every wave's output stores complete, then one release publishes them
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __atomic_thread_fence(__ATOMIC_RELEASE);
+      __hip_atomic_store(&sl->done, post, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (wave == 0 && mine == k) served = post;
+  }
+}
+
+int launch_evp_server(const ServerArgs& a, int groups, hipStream_t s) {
+  hipLaunchKernelGGL(evp_server_kernel, dim3(groups), dim3(kThreads), 0, s, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace tg

@@ -43,8 +43,23 @@ constexpr uint32_t LDS_BYTES = PLAN_OFF + 4 * kPlanCap;
 __shared__ __attribute__((aligned(16))) uint8_t s_lds[LDS_BYTES];
 
 // Wave-uniform data (session header, round keys, descriptors) is read through
-// the constant address space so it lands in SGPRs via s_load.
+// the constant address space so it lands in SGPRs via s_load.  A persistent
+// kernel (evp_server.hip: TG_VECTOR_SESSION_LOADS) reads the same data as
+// plain global loads instead: a kernel launch invalidates the scalar cache, a
+// long-running kernel never gets that, and session slots are re-keyed while it
+// runs; its per-job acquire fence invalidates only the vector caches.
+#ifdef TG_VECTOR_SESSION_LOADS
+// a uniform word read by a vector load and moved to an SGPR (readfirstlane)
+struct cu32_word {
+  uint32_t raw;
+  __device__ __forceinline__ operator uint32_t() const {
+    return __builtin_amdgcn_readfirstlane(raw);
+  }
+};
+typedef const cu32_word cu32;
+#else
 typedef __attribute__((address_space(4))) const uint32_t cu32;
+#endif
 template <typename T>
 __device__ __forceinline__ cu32* as_const(const T* p) { return (cu32*)(p); }
 

@@ -26,6 +26,7 @@
 //     block sequence E = [AAD', C_0..C_{nb-1}, lengths] (j = l mod 64), then
 //     y_l = x_l * H^(nb+1-jlast_l) and an XOR butterfly across the wave.
 #include "gcm_device.h"
+#include "gcm_raw.h"
 
 namespace tg {
 
@@ -106,107 +107,11 @@ __global__ __launch_bounds__(kThreads, 1) void gcm_batch_kernel(BatchArgs a) {
   }
 }
 
-// Raw EVP jobs (EVP_AEAD_CTX_seal/open, any nonce / AAD length; TLS = false)
-// or the records of a small TLS batch (TLS = true: tlsgpu_record descriptors,
-// parse_tls): one job per workgroup and the job's blocks split over the 16
-// waves, for latency — a synchronous EVP call waits for its one job, a small
-// batch leaves most CUs idle with one wave per record, and a coalesced batch
-// runs its jobs side by side on as many CUs.  Wave w takes the 64-aligned block range
-// [64 * spw * w, 64 * spw * (w + 1)); its lane chains are the record's chains
-// restricted to that range, so their weights are H^(nb + 1 - jlast) as in the
-// one-wave form: the last range closes with the lengths block as usual, the
-// others raise their chains by (H^64)^q with q extra Horner steps and finish
-// with one Shoup multiply.  The 16 partial GHASH values meet in LDS and wave 0
-// forms / checks the tag (and zero-fills on failure) after the barrier.
+// Raw EVP jobs and small TLS batches: one job per workgroup (gcm_raw.h).
 template <bool SEAL, int ROUNDS, bool TLS = false>
 __global__ __launch_bounds__(kThreads, 1) void gcm_raw_kernel(BatchArgs a) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t laneoff = aes_laneoff(lane);
-  const GhLane gl = gh_lane(lane);
-  const uint32_t r = blockIdx.x;
-  const RawJob* J = reinterpret_cast<const RawJob*>(a.descs) + r;
-  const tlsgpu_record* D = reinterpret_cast<const tlsgpu_record*>(a.descs) + r;
-  const uint32_t sid = __builtin_amdgcn_readfirstlane(TLS ? as_const(D)[6] : J->session);
-  const bool in_range = sid < a.n_sessions;
-  const DevSession* __restrict__ S = a.sessions + (in_range ? sid : 0);
-  const uint32_t kind = as_const(&S->kind)[0];
-  if (!(in_range && is_gcm(kind) && (int)as_const(&S->rounds)[0] == ROUNDS)) {
-    // raw jobs: no per-batch status memset (run_batch); a job no kernel of
-    // this launch set takes (bad or empty session) is publicly invalid here
-    if (!TLS && threadIdx.x == 0 && !(in_range && kind >= TLSGPU_AES_128_GCM &&
-                                       kind <= TLSGPU_CHACHA20_POLY1305_OLD))
-      a.status[r] = TLSGPU_REC_PUBLIC_INVALID;
-    return;
-  }
-  fill_aes_lds<kThreads>();
-  load_session_tables<kThreads>(a.gcm_tables + sid);
-  __syncthreads();
-  RecCtx rc;
-  if (TLS) {
-    // every wave parses (same descriptor): a publicly invalid record returns
-    // from all of them before the barrier below
-    if (!parse_tls<SEAL>(load_desc(D), S, a.in, a.out, a.status + r, lane, rc)) return;
-  } else {
-    parse_raw<SEAL>(*J, S, rc);
-  }
-  cu32* rk = as_const(S->rk);
-  const uint32_t nb = (rc.n + 15) >> 4;
-  const uint32_t nsteps = (nb + kWave - 1) / kWave;
-  const uint32_t spw = nsteps == 0 ? 1 : (nsteps + kWaves - 1) / kWaves;  // steps per wave
-  const uint32_t nwork = nsteps == 0 ? 1 : (nsteps + spw - 1) / spw;
-  uint32_t y[4] = {0, 0, 0, 0};
-  if (wave < nwork) {
-    const CtrConst cc = ctr_setup(rc.j0, rk, laneoff);
-    const RecConsts none = {};
-    const uint32_t s0 = wave * spw * kWave;
-    uint32_t x[4] = {0, 0, 0, 0};
-    if (wave == 0 && rc.aad_len != 0 && lane == 63) {
-      x[0] = bswap32(rc.aad_be[0]); x[1] = bswap32(rc.aad_be[1]);
-      x[2] = bswap32(rc.aad_be[2]); x[3] = bswap32(rc.aad_be[3]);
-    }
-    uint32_t xb[4];
-    uint32_t e;
-    if (wave == nwork - 1) {  // the last range: partial tail, lengths block
-      gcm_blocks<SEAL, ROUNDS, false>(rc, S, none, cc, x, s0, lane, laneoff, gl);
-      e = gcm_close_chain(rc, x, xb, lane, gl);
-    } else {
-      RecCtx part = rc;
-      const uint32_t e1 = s0 + spw * kWave;  // full blocks only
-      part.n = 16u * e1;
-      gcm_blocks<SEAL, ROUNDS, false>(part, S, none, cc, x, s0, lane, laneoff, gl);
-      e = nb + 1 - (e1 - kWave + lane);
-      while (e > (uint32_t)kPowMax) {  // weight (H^64)^q: q more Horner steps
-        uint32_t xk[4];
-        gl.mul64(x, xk);
-        x[0] = xk[0]; x[1] = xk[1]; x[2] = xk[2]; x[3] = xk[3];
-        e -= kWave;
-      }
-      be_from_le(x, xb);
-    }
-    if (e != 0) gl.shoup(xb, e, y);
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-      y[0] ^= __shfl_xor(y[0], m);
-      y[1] ^= __shfl_xor(y[1], m);
-      y[2] ^= __shfl_xor(y[2], m);
-      y[3] ^= __shfl_xor(y[3], m);
-    }
-  }
-  uint4* part_y = reinterpret_cast<uint4*>(s_lds + PLAN_OFF);
-  if (lane == 0) part_y[wave] = make_uint4(y[0], y[1], y[2], y[3]);
-  __syncthreads();
-  if (wave != 0) return;
-  uint32_t t[4] = {0, 0, 0, 0};
-  if (lane == 0) {
-    for (uint32_t w = 0; w < nwork; w++) {
-      const uint4 v = part_y[w];
-      t[0] ^= v.x; t[1] ^= v.y; t[2] ^= v.z; t[3] ^= v.w;
-    }
-  }
-  uint32_t ek0[4] = {rc.j0[0], rc.j0[1], rc.j0[2], rc.j0[3]};
-  aes_block<ROUNDS>(ek0, rk, as_const(S->rk_rot), laneoff);
-  gcm_tag<SEAL>(rc, t, ek0, S, a.status + r, lane);
+  fill_aes_lds<kThreads>();  // the job's barrier after its table load covers this
+  gcm_raw_job<SEAL, ROUNDS, TLS>(a, blockIdx.x);
 }
 
 template <bool SEAL, int ROUNDS, bool TLS = false>

@@ -253,6 +253,32 @@ int launch_gcm_hy14(const BatchArgs& a, const RecPre* pre, bool seal, int bs_wav
 int launch_bs_ecb(const DevSession* sessions, uint32_t session, int rounds, const void* d_in,
                   void* d_out, uint32_t nblocks, hipStream_t s);
 int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, hipStream_t s);
+
+// Doorbell slot of the persistent EVP server (evp_server.hip, engine.cpp): one
+// per calling thread, in pinned host memory, one 128-B line each.  The thread
+// fills the job fields, then stores `post` (its next job number); a server
+// workgroup that sees post != the number it last served runs the job (one
+// RawJob, zero-copy in the thread's pinned staging) and stores `done` = post
+// after the job's output and status are visible to the host.
+struct alignas(128) DoorbellSlot {
+  uint32_t post;        // host: number of the posted job (written last)
+  uint32_t done;        // device: number of the last job finished
+  uint32_t op;          // bit 0: seal; bits 8-15: AES rounds (10 / 14)
+  uint32_t n_sessions;  // capacity of the context's session table
+  uint64_t job;         // device address of the RawJob
+  uint64_t status;      // device address of the job's int32 status
+  uint64_t sessions;    // const DevSession* of the context's table
+  uint64_t gcm_tables;  // const DevGcmTables*
+  uint8_t pad[80];
+};
+static_assert(sizeof(DoorbellSlot) == 128, "DoorbellSlot layout");
+struct ServerArgs {
+  DoorbellSlot* slots;        // device view of the pinned slot array
+  uint32_t nslots;
+  const uint32_t* stop;       // pinned word: non-zero = exit now
+  unsigned long long lifetime;  // s_memrealtime ticks (100 MHz) a workgroup serves at most
+};
+int launch_evp_server(const ServerArgs& a, int groups, hipStream_t s);
 int launch_session_install_arg(DevSession* sessions, DevGcmTables* tables,
                                const tlsgpu_session_params& p, uint32_t id, hipStream_t s);
 int launch_session_install(DevSession* sessions, DevGcmTables* tables,

@@ -1,0 +1,73 @@
+"""The doorbell server for per-call EVP jobs (round 4, talos_amd/csrc/evp_server.hip,
+include/tlsgpu.h tlsgpu_evp_set_doorbell): with TLSGPU_EVP_DOORBELL set, a
+synchronous EVP_AEAD_CTX_seal / _open on an AES-GCM context is posted to a
+resident server workgroup instead of launching a kernel.  Every output must
+be the oracle's (e_aes.c:1424-1510 through evp_aead.c:89-144: tag, zero-fill
+and return 0 on a bad tag, odd nonce lengths, truncated tags), with threads
+cycling init / seal / open / cleanup so session slots are re-keyed while the
+server runs, across server relaunches (short lifetime), and the server must
+stop by itself when the calls stop.  ChaCha20-Poly1305 contexts keep the
+launched path in the same process."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+_CHILD = r"""
+import os, random, sys, threading, time
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, os.path.join(sys.argv[1], "oracle"))
+import talos_amd as ta, pyoracle as po
+ta.load_library()
+orc = po.Oracle()
+kinds = [po.AES_128_GCM, po.AES_256_GCM, po.CHACHA20_POLY1305]
+errors = []
+def worker(t):
+    rnd = random.Random(4100 + t)
+    try:
+        for i in range(30):
+            kind = kinds[(t + i) % len(kinds)]
+            key = bytes(rnd.randrange(256) for _ in range(po.KEY_LEN[kind]))
+            tag_len = rnd.choice([16, 16, 12]) if kind != po.CHACHA20_POLY1305 else 16
+            ctx, octx = ta.EvpAead(kind, key, tag_len), orc.aead(kind, key, tag_len)
+            assert ctx.ok == 1
+            for _ in range(3):
+                nlen = 12 if kind == po.CHACHA20_POLY1305 else rnd.choice([12, 12, 1, 8, 16, 60])
+                nonce = bytes(rnd.randrange(256) for _ in range(nlen))
+                pt = bytes(rnd.randrange(256) for _ in range(rnd.choice([0, 1, 15, 100, 1400, 4096, 16384, 40000])))
+                ad = bytes(rnd.randrange(256) for _ in range(rnd.choice([0, 13, 100])))
+                ok, exp = orc.seal(octx, nonce, pt, ad)
+                ok2, got, ol = ctx.seal(nonce, pt, ad)
+                assert ok == ok2 == 1 and got == exp and ol == len(exp), (t, i, kind, len(pt))
+                ok3, back, _ = ctx.open(nonce, got, ad)
+                assert ok3 == 1 and back == pt, (t, i, kind, len(pt))
+                if got:
+                    bad = bytearray(got); bad[rnd.randrange(len(bad))] ^= 1 << rnd.randrange(8)
+                    ok4, z, _ = ctx.open(nonce, bytes(bad), ad)
+                    assert ok4 == 0 and not any(z), (t, i, "tampered record accepted or not zero-filled")
+            ctx.cleanup()
+            if i % 7 == 3:
+                time.sleep(0.03)   # past half a lifetime: the next call relaunches the server
+    except Exception as exc:
+        errors.append(repr(exc))
+ths = [threading.Thread(target=worker, args=(t,)) for t in range(int(sys.argv[2]))]
+[th.start() for th in ths]; [th.join() for th in ths]
+assert not errors, errors[:3]
+jobs, launches = ta.evp_doorbell_stats()
+assert jobs > 0 and launches >= 2, (jobs, launches)
+time.sleep(0.2)   # every instance has passed its lifetime: none may still be running
+print("OK", jobs, launches)
+"""
+
+
+@pytest.mark.parametrize("threads", [1, 12])
+def test_evp_doorbell_matches_oracle(threads):
+    env = dict(os.environ, TLSGPU_EVP_DOORBELL="4", TLSGPU_EVP_DOORBELL_MS="40")
+    env.pop("TLSGPU_EVP_BATCH_US", None)
+    r = subprocess.run([sys.executable, "-c", _CHILD, ROOT, str(threads)], env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
