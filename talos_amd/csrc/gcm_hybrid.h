@@ -295,7 +295,9 @@ __device__ void gcm_pair_hy(const RecCtx (&rc)[2], const RecPre* pa, const RecPr
 
 }  // namespace tg
 
-#include "gcm_bs16.h"
+#ifdef TG_EXPERIMENTAL  // the packed bitsliced record path (talos_amd/experimental/)
+#include "../experimental/gcm_bs16.h"
+#endif
 
 namespace tg {
 
@@ -323,6 +325,15 @@ __device__ __forceinline__ void hy_tt_record(const BatchArgs& a, const RecPre* _
 // the shared LDS table); anything else through the T-table path.  The reserve
 // keeps the run's last records on T-table waves, so the run-end barrier does
 // not wait for a bitsliced record started late.
+#ifndef TG_EXPERIMENTAL
+// default build: no bitsliced role (B16W = 0 everywhere), never instantiated
+template <bool SEAL, int ROUNDS>
+__device__ __forceinline__ bool hy_b16_record(const BatchArgs&, const RecPre* __restrict__,
+                                              uint32_t, uint32_t, const DevSession* __restrict__,
+                                              uint32_t, uint32_t, const GhLane&) {
+  return false;
+}
+#else
 template <bool SEAL, int ROUNDS>
 __device__ __forceinline__ bool hy_b16_record(const BatchArgs& a, const RecPre* __restrict__ pre,
                                               uint32_t r, uint32_t left,
@@ -340,6 +351,7 @@ __device__ __forceinline__ bool hy_b16_record(const BatchArgs& a, const RecPre* 
   }
   return false;  // the caller's T-table path (one call site of gcm_record_x4: inlined)
 }
+#endif
 
 // ---------------------------------------------------------------------------
 // Short-record packs.  A record's GHASH sequence is

@@ -1,7 +1,7 @@
 // bs_ecb.hip — diagnostic self-test of the bitsliced AES core (bs_aes.h):
 // ECB encryption under a session's key, checked bit-exact against the oracle
 // by tests/test_gpu_parity.py (tlsgpu_aes_ecb_bitsliced).
-#include "gcm_device.h"
+#include "../csrc/gcm_device.h"
 
 namespace tg {
 

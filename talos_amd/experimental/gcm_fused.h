@@ -14,7 +14,7 @@
 // 16 KiB TT record per record pair.  TT record boundaries are handled after a pass's
 // consume step, where the bitsliced state is dead.
 #pragma once
-#include "gcm_hybrid.h"
+#include "../csrc/gcm_hybrid.h"
 
 namespace tg {
 

@@ -1,6 +1,6 @@
 // gcm_hy256.hip — AES-256-GCM instantiations of gcm_hy_kernel with
 // bitsliced waves: 4 of 8 (TLSGPU_GCM_HYBRID) or all 8 (TLSGPU_GCM_BITSLICE).
-#include "gcm_hybrid.h"
+#include "../csrc/gcm_hybrid.h"
 
 namespace tg {
 

@@ -3,7 +3,7 @@
 // pipe busy while the bitsliced waves run AES on the VALU.  Selected by
 // BatchArgs::bs16_min != 0 (env TLSGPU_BS16_MIN); its own translation unit so
 // the bitsliced code compiles in parallel with gcm_queue.hip.
-#include "gcm_hybrid.h"
+#include "../csrc/gcm_hybrid.h"
 
 namespace tg {
 
