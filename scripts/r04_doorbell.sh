@@ -13,7 +13,7 @@ step() {  # name timeout cmd...
   return 0
 }
 step probe 60 tools/doorbell_probe
+step abC 400 bash scripts/ab_bench.sh "$(basename $O)_abC" 3 "variants/libtlsgpu_base.so talos_amd/libtlsgpu.so" --config C
 step doorbell_test 240 python -u -m pytest tests/test_evp_doorbell.py -x -v --timeout 120 --timeout-method thread -m gpu
 step doorbell_bench 400 scripts/evp_doorbell_bench.sh "${O}_doorbell_bench.jsonl"
-step suite 900 python -u -m pytest tests -v --timeout 120 --timeout-method thread -m gpu
-step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
+step copy 120 tools/ubench copy

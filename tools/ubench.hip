@@ -639,6 +639,31 @@ __global__ void __launch_bounds__(256) copy_u(const float4* __restrict__ a4, flo
   for (; i < n; i += stride) b[i] = a[i];
 }
 
+// Copy where each wave streams one contiguous chunk: load k of a wave covers
+// [chunk + k KiB, chunk + (k+1) KiB), so every instruction is one coalesced
+// 1 KiB and a wave's U loads in flight are U consecutive KiB (DRAM pages).
+template <int U, bool NT>
+__global__ void __launch_bounds__(512) copy_chunk(const float4* __restrict__ a4,
+                                                  float4* __restrict__ b4, size_t n) {
+  const v4u_t* a = (const v4u_t*)a4;
+  v4u_t* b = (v4u_t*)b4;
+  const size_t waves = (size_t)gridDim.x * (blockDim.x / 64);
+  const size_t wave = (size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  const size_t lane = threadIdx.x & 63;
+  const size_t per = 64 * U;  // float4 per wave iteration
+  for (size_t base = wave * per; base + per <= n; base += waves * per) {
+    v4u_t x[U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      x[u] = NT ? __builtin_nontemporal_load(a + base + 64 * u + lane) : a[base + 64 * u + lane];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (NT) __builtin_nontemporal_store(x[u], b + base + 64 * u + lane);
+      else b[base + 64 * u + lane] = x[u];
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 static int g_cus = 256;
 static Stamp* g_st;
@@ -802,12 +827,14 @@ static void set4() {
 
 // set3: the vector-memory (L1) lookup pipe, alone and beside the LDS AES round,
 // and the copy variants.
+static bool g_copy_only = false;
 static void set3() {
   uint32_t* gtab;
   CK(hipMalloc(&gtab, 4096));
   CK(hipMemcpy(gtab, g_tab, 4096, hipMemcpyDeviceToDevice));
   for (int W : {8, 16})
     for (int nch : {4, 8}) {
+      if (g_copy_only) break;
       const int iters = 1024;
       Res r = run([&](int th, size_t l) {
         if (nch == 4) ta_chain_kernel<4><<<g_cus, th, l>>>(iters, gtab, g_st, g_out);
@@ -819,7 +846,7 @@ static void set3() {
              W, nch, r.med_cycles / ((double)iters * nch * W), r.clock_ghz);
     }
   for (int nb : {1, 2})
-    for (int tac = 0; tac <= 4; tac++) {
+    for (int tac = 0; tac <= 4 && !g_copy_only; tac++) {
       const int rounds = 1024;
       Res r = run([&](int th, size_t l) {
 #define A(NB, T) if (nb == NB && tac == T) aes_ta_kernel<NB, T><<<g_cus, th, l>>>(rounds, g_tab, gtab, g_rk, g_st, g_out);
@@ -862,6 +889,12 @@ static void set3() {
     CK(hipEventDestroy(e0));
     CK(hipEventDestroy(e1));
   };
+  for (int bpc : {1, 2, 4}) {
+    time_copy("chunk8_512t", bpc, [&](int g) { copy_chunk<8, false><<<g, 512>>>(a, b, n); });
+    time_copy("chunk8_nt_512t", bpc, [&](int g) { copy_chunk<8, true><<<g, 512>>>(a, b, n); });
+    time_copy("chunk16_512t", bpc, [&](int g) { copy_chunk<16, false><<<g, 512>>>(a, b, n); });
+    time_copy("chunk4_512t", bpc, [&](int g) { copy_chunk<4, false><<<g, 512>>>(a, b, n); });
+  }
   for (int bpc : {1, 2}) {
     time_copy("u16_nt", bpc, [&](int g) { copy_u<16, true><<<g, 256>>>(a, b, n); });
     time_copy("u16", bpc, [&](int g) { copy_u<16, false><<<g, 256>>>(a, b, n); });
@@ -1024,6 +1057,12 @@ int main(int argc, char** argv) {
   if (argc > 1 && !strcmp(argv[1], "set4")) {
     set4();
     if (argc > 2) set3();
+    fflush(stdout);
+    return 0;
+  }
+  if (argc > 1 && !strcmp(argv[1], "copy")) {  // the copy variants of set3 only
+    g_copy_only = true;
+    set3();
     fflush(stdout);
     return 0;
   }
