@@ -432,7 +432,7 @@ int tlsgpu_evp_call_stats(uint64_t *seal_calls, uint64_t *open_calls);
  * RawJob the launched path builds) in a slot of pinned host memory and spins
  * on the answer, so a synchronous EVP_AEAD_CTX_seal / _open on an AES-GCM
  * context costs one PCIe round trip instead of a kernel launch + stream sync.
- * Each server instance exits after lifetime_ms (0 = 50 ms) and is relaunched
+ * Each server instance exits after lifetime_ms (0 = 5 ms) and is relaunched
  * by the next call, so an idle process leaves nothing running.  Threads beyond
  * 8 * groups per device, ChaCha20-Poly1305 contexts and pooled (queued)
  * contexts use the other paths.  Same as TLSGPU_EVP_DOORBELL=<groups>

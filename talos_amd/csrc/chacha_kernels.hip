@@ -97,30 +97,14 @@ __device__ __forceinline__ void poly_block(Poly& p, uint32_t m0, uint32_t m1, ui
                 (uint64_t)h3 * p.r0 + (uint64_t)h4 * p.s4;
   uint64_t d4 = (uint64_t)h0 * p.r4 + (uint64_t)h1 * p.r3 + (uint64_t)h2 * p.r2 +
                 (uint64_t)h3 * p.r1 + (uint64_t)h4 * p.r0;
-  // Round 4: the carries in two PARALLEL levels instead of poly1305-donna.c's
-  // serial chain d0 -> d1 -> ... -> d4 -> h0 -> h1 (depth ~20 dependent ops,
-  // the Poly1305 share of config C's dependency stalls): the same integer mod
-  // p = 2^130 - 5, a different limb split.  Bounds, with the clamped r
-  // (r4 < 2^20) and limbs h_i < 2^26 + 45 on entry (so h + m < 2^27.01):
-  //   d0 < 2^57.1, d1 < 2^56.7, d2 < 2^56.3, d3 < 2^55.1, d4 < 2^55.1, so
-  //   c_i = d_i >> 26 < 2^31.1 is exact in 32 bits and 5 c4 < 2^31.5;
-  //   level 1 e_i = (d_i mod 2^26) + c_{i-1} (c4 * 5 into e0) < 2^31.5;
-  //   level 2 h_i = (e_i mod 2^26) + e_{i-1} >> 26 (x5 into h0): e >> 26 <= 44,
-  //   so h_i < 2^26 + 45 again — the invariant holds block after block, and
-  //   poly_finish's full carry (poly1305-donna.c:233-254) starts from limbs in
-  //   the range of the serial form's (< 2^26 + a few), giving the same tag.
-  const uint32_t M = 0x3ffffff;
-  const uint32_t c0 = (uint32_t)(d0 >> 26), c1 = (uint32_t)(d1 >> 26),
-                 c2 = (uint32_t)(d2 >> 26), c3 = (uint32_t)(d3 >> 26),
-                 c4 = (uint32_t)(d4 >> 26);
-  const uint32_t e0 = ((uint32_t)d0 & M) + c4 * 5, e1 = ((uint32_t)d1 & M) + c0,
-                 e2 = ((uint32_t)d2 & M) + c1, e3 = ((uint32_t)d3 & M) + c2,
-                 e4 = ((uint32_t)d4 & M) + c3;
-  p.h0 = (e0 & M) + (e4 >> 26) * 5;
-  p.h1 = (e1 & M) + (e0 >> 26);
-  p.h2 = (e2 & M) + (e1 >> 26);
-  p.h3 = (e3 & M) + (e2 >> 26);
-  p.h4 = (e4 & M) + (e3 >> 26);
+  uint32_t c = (uint32_t)(d0 >> 26); h0 = (uint32_t)d0 & 0x3ffffff;
+  d1 += c; c = (uint32_t)(d1 >> 26); h1 = (uint32_t)d1 & 0x3ffffff;
+  d2 += c; c = (uint32_t)(d2 >> 26); h2 = (uint32_t)d2 & 0x3ffffff;
+  d3 += c; c = (uint32_t)(d3 >> 26); h3 = (uint32_t)d3 & 0x3ffffff;
+  d4 += c; c = (uint32_t)(d4 >> 26); h4 = (uint32_t)d4 & 0x3ffffff;
+  h0 += c * 5; c = h0 >> 26; h0 &= 0x3ffffff;
+  h1 += c;
+  p.h0 = h0; p.h1 = h1; p.h2 = h2; p.h3 = h3; p.h4 = h4;
 }
 
 // poly1305-donna.c:231-321: full carry, conditional subtract, + pad.

@@ -1171,6 +1171,7 @@ struct AeadState {
   EvpBatcher* batcher;    // the queue of the context's device (pooled contexts), or null
   uint32_t evp_dev;       // index of the context's device among the EVP devices
   hipEvent_t installed;   // the slot's event, recorded after the context's key install
+  uint32_t key_id = 0;    // unique per install (doorbell server's LDS table cache)
   mutable std::atomic<bool> install_pending{true};  // no call has waited for it yet
 };
 
@@ -1453,6 +1454,9 @@ extern "C" int EVP_AEAD_CTX_init(EVP_AEAD_CTX* ctx, const EVP_AEAD* aead, const 
   auto* st = new (std::nothrow) AeadState();
   if (!st) return 0;
   st->kind = aead->kind;
+  static std::atomic<uint32_t> g_key_ids{0};
+  do st->key_id = g_key_ids.fetch_add(1, std::memory_order_relaxed) + 1;
+  while (st->key_id == 0);  // 0 means "no key" to the server's table cache
   st->tag_len = (unsigned)tag_len;
   st->batcher = nullptr;
   st->evp_dev = (uint32_t)dk;
@@ -1580,11 +1584,17 @@ static const bool g_evp_zerocopy = [] {
 // server workgroups resident per EVP device while calls arrive; a calling
 // thread owns one slot of kSlotsPerGroup * G (slot k -> workgroup k % G), posts
 // its job number there and spins on the answer.  An instance lives `lifetime`
-// (TLSGPU_EVP_DOORBELL_MS, default 50 ms) and is relaunched by the first post
+// (TLSGPU_EVP_DOORBELL_MS, default 5 ms) and is relaunched by the first post
 // after half of that has passed, on the same stream: a job is only posted
 // while an instance that still polls for at least half a lifetime is queued or
 // running, so every posted job is served, and a process that stops calling
 // leaves nothing spinning.  ChaCha20-Poly1305 contexts keep the launched path.
+// The lifetime is short on purpose: this box runs at most GPU_MAX_HW_QUEUES = 4
+// hardware queues per process, so with more streams than that (engine + 4 call
+// streams + server) the server's queue is shared, and a kernel launched on a
+// stream that shares it waits until the running instance exits
+// (tools/doorbell_probe.hip: 2.7 s behind a 3 s instance with 8 other streams).
+// 5 ms bounds that wait; relaunching every 2.5 ms under load costs one launch.
 constexpr uint32_t kSlotsPerGroup = 8;
 struct EvpServer {
   int device = -1;
@@ -1608,8 +1618,8 @@ static unsigned g_doorbell_groups = [] {
 }();
 static unsigned g_doorbell_ms = [] {
   const char* v = getenv("TLSGPU_EVP_DOORBELL_MS");
-  const unsigned ms = v && *v ? (unsigned)strtoul(v, nullptr, 10) : 50u;
-  return ms ? ms : 50u;
+  const unsigned ms = v && *v ? (unsigned)strtoul(v, nullptr, 10) : 5u;
+  return ms ? ms : 5u;
 }();
 
 static uint64_t mono_ns() {
@@ -1823,6 +1833,7 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
       slot->status = (uint64_t)(d + o_status);
       slot->sessions = (uint64_t)st->sess->d_sess;
       slot->gcm_tables = (uint64_t)st->sess->d_gcm;
+      slot->key_id = st->key_id;
       if (!server_ensure(sv)) return -1;
       const uint32_t n = ++*seq;
       __atomic_store_n(&slot->post, n, __ATOMIC_RELEASE);

@@ -48,18 +48,22 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
   const uint32_t mine = blockIdx.x + lane * gridDim.x;
   uint32_t served = 0;
   if (wave == 0 && mine < s.nslots) served = sys_load(&s.slots[mine].done);
+  uint32_t cached_key = 0;  // key id whose GCM tables are in LDS (0: none)
   for (;;) {
     if (wave == 0) {
       uint32_t pick = kSrvExit;
-      for (;;) {
+      for (uint32_t polls = 0;; polls++) {
         const bool ready = mine < s.nslots && sys_load(&s.slots[mine].post) != served;
         const unsigned long long m = __ballot(ready);
         if (m) {
           pick = blockIdx.x + (uint32_t)(__ffsll((long long)m) - 1) * gridDim.x;
           break;
         }
-        if (sys_load(s.stop) != 0 || __builtin_amdgcn_s_memrealtime() - t0 > s.lifetime) break;
-        __builtin_amdgcn_s_sleep(2);
+        // the stop word and the clock every 16 polls (each poll is a PCIe read)
+        if ((polls & 15) == 15 &&
+            (sys_load(s.stop) != 0 || __builtin_amdgcn_s_memrealtime() - t0 > s.lifetime))
+          break;
+        __builtin_amdgcn_s_sleep(1);
       }
       if (lane == 0) *sel = pick;
       // the job's fields and data (pinned host memory) and its session (HBM,
@@ -84,20 +88,27 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
         __hip_atomic_load(&sl->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     a.n = 1;
     a.n_sessions = sys_load(&sl->n_sessions);
+    const uint32_t key = __builtin_amdgcn_readfirstlane(sys_load(&sl->key_id));
+    const bool hit = key != 0 && key == cached_key;
+    cached_key = key;
     switch (op) {
-      case 10 << 8: gcm_raw_job<false, 10>(a, 0); break;
-      case (10 << 8) | 1: gcm_raw_job<true, 10>(a, 0); break;
-      case 14 << 8: gcm_raw_job<false, 14>(a, 0); break;
-      case (14 << 8) | 1: gcm_raw_job<true, 14>(a, 0); break;
+      case 10 << 8: gcm_raw_job<false, 10>(a, 0, hit); break;
+      case (10 << 8) | 1: gcm_raw_job<true, 10>(a, 0, hit); break;
+      case 14 << 8: gcm_raw_job<false, 14>(a, 0, hit); break;
+      case (14 << 8) | 1: gcm_raw_job<true, 14>(a, 0, hit); break;
       default:  // not a job this server runs (the host never posts one)
         if (threadIdx.x == 0) a.status[0] = TLSGPU_REC_PUBLIC_INVALID;
+        cached_key = 0;
         break;
     }
-    // every wave's output stores complete, then one release publishes them
+    // every wave's output stores complete, then one release publishes them;
+    // the asm wait keeps the flag behind the write-back (MI355X_MICROARCH.md,
+    // compiler hazard: hipcc drops the vmcnt wait after buffer_wbl2 here)
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     if (threadIdx.x == 0) {
       __atomic_thread_fence(__ATOMIC_RELEASE);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_store(&sl->done, post, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (wave == 0 && mine == k) served = post;

@@ -24,8 +24,11 @@ namespace tg {
 // into LDS behind a barrier and returns with nothing of the job left in
 // flight except the tag / status of wave 0, so the persistent EVP server
 // (evp_server.hip) can start its next job after one more barrier.
+// tables_loaded: the session's GCM tables are already in LDS (the server's
+// previous job had the same installed key).
 template <bool SEAL, int ROUNDS, bool TLS = false>
-__device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r) {
+__device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
+                                            bool tables_loaded = false) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t laneoff = aes_laneoff(lane);
@@ -44,7 +47,7 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r) {
       a.status[r] = TLSGPU_REC_PUBLIC_INVALID;
     return;
   }
-  load_session_tables<kThreads>(a.gcm_tables + sid);
+  if (!tables_loaded) load_session_tables<kThreads>(a.gcm_tables + sid);
   __syncthreads();
   RecCtx rc;
   if (TLS) {

@@ -269,7 +269,10 @@ struct alignas(128) DoorbellSlot {
   uint64_t status;      // device address of the job's int32 status
   uint64_t sessions;    // const DevSession* of the context's table
   uint64_t gcm_tables;  // const DevGcmTables*
-  uint8_t pad[80];
+  uint32_t key_id;      // unique per installed key (process-wide): a server
+                        // workgroup keeps the GCM tables of the last key it
+                        // served in LDS and skips reloading them for the same id
+  uint8_t pad[76];
 };
 static_assert(sizeof(DoorbellSlot) == 128, "DoorbellSlot layout");
 struct ServerArgs {
