@@ -29,7 +29,9 @@ run host_B --mode host --no-cpu-baseline --steps 8 --warmup 2 &&
 run pcie --mode pcie &&
 run wire_B --mode wire --no-cpu-baseline &&
 run wire_C --mode wire --config C --no-cpu-baseline &&
-run wire_D --mode wire --config D --no-cpu-baseline || exit $?
+run wire_D --mode wire --config D --no-cpu-baseline &&
+run group_dev0 --split group --devices 0 --no-cpu-baseline &&
+run group_dev00 --split group --devices 0,0 --no-cpu-baseline || exit $?
 [ "$2" = "--no-pmc" ] && exit 0
 for c in B C D; do
   bash scripts/pmc.sh $TAG/pmc$c --config $c || exit $?

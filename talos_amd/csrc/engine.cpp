@@ -1827,9 +1827,17 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
         if (hipEventSynchronize(st->installed) != hipSuccess) return -1;
         st->install_pending.store(false, std::memory_order_release);
       }
-      slot->op = (uint32_t)(seal ? 1 : 0) | ((st->kind == TLSGPU_AES_128_GCM ? 10u : 14u) << 8);
+      // the job travels in the slot (one wave load brings it to the server),
+      // nonce and AAD inline when they fit
+      const bool inl = nonce_len + ad_len <= kDoorbellInline;
+      slot->op = (uint32_t)(seal ? 1 : 0) | ((st->kind == TLSGPU_AES_128_GCM ? 10u : 14u) << 8) |
+                 (inl ? 1u << 16 : 0u);
       slot->n_sessions = st->sess->capacity;
-      slot->job = (uint64_t)d;
+      memcpy(&slot->job, j, sizeof(RawJob));
+      if (inl) {
+        if (nonce_len) memcpy(slot->inl, nonce, nonce_len);
+        if (ad_len) memcpy(slot->inl + nonce_len, ad, ad_len);
+      }
       slot->status = (uint64_t)(d + o_status);
       slot->sessions = (uint64_t)st->sess->d_sess;
       slot->gcm_tables = (uint64_t)st->sess->d_gcm;

@@ -31,6 +31,8 @@ namespace tg {
 
 constexpr uint32_t kSrvExit = 0xFFFFFFFFu;
 constexpr uint32_t SRV_SEL_OFF = PLAN_OFF + 16 * 16;  // after gcm_raw_job's part_y words
+constexpr uint32_t SRV_SLOT_OFF = PLAN_OFF + 512;     // LDS copy of the picked slot (256 B)
+static_assert(SRV_SLOT_OFF + sizeof(DoorbellSlot) <= LDS_BYTES, "server LDS plan");
 
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -66,29 +68,40 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
         __builtin_amdgcn_s_sleep(1);
       }
       if (lane == 0) *sel = pick;
-      // the job's fields and data (pinned host memory) and its session (HBM,
-      // installed by another kernel) are read fresh after this
-      __atomic_thread_fence(__ATOMIC_ACQUIRE);
+      if (pick != kSrvExit) {
+        // the whole slot in one wave load (the job, its nonce and AAD: no
+        // further PCIe round trip for them) into LDS; inline nonce / AAD are
+        // then addressed in that copy
+        DoorbellSlot* sl = s.slots + pick;
+        const uint32_t w = sys_load(reinterpret_cast<const uint32_t*>(sl) + lane);
+        DoorbellSlot* c = reinterpret_cast<DoorbellSlot*>(s_lds + SRV_SLOT_OFF);
+        reinterpret_cast<uint32_t*>(c)[lane] = w;
+        const uint32_t opw = __shfl(w, 2);  // DoorbellSlot::op
+        if (lane == 0 && (opw & (1u << 16))) {
+          c->job.nonce = (uint64_t)(uintptr_t)&c->inl[0];
+          c->job.aad = (uint64_t)(uintptr_t)&c->inl[c->job.nonce_len];
+        }
+        // the job's input (pinned host memory) and its session (HBM, installed
+        // by another kernel) are read fresh after this
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+      }
       __builtin_amdgcn_s_waitcnt(0);
     }
     __syncthreads();
     const uint32_t k = __builtin_amdgcn_readfirstlane(*sel);
     if (k == kSrvExit) break;
     DoorbellSlot* sl = s.slots + k;
-    const uint32_t post = __builtin_amdgcn_readfirstlane(sys_load(&sl->post));
-    const uint32_t op = __builtin_amdgcn_readfirstlane(sys_load(&sl->op));
+    const DoorbellSlot* c = reinterpret_cast<const DoorbellSlot*>(s_lds + SRV_SLOT_OFF);
+    const uint32_t post = __builtin_amdgcn_readfirstlane(c->post);
+    const uint32_t op = __builtin_amdgcn_readfirstlane(c->op) & 0xFFFFu;
     BatchArgs a = {};
-    a.sessions = reinterpret_cast<const DevSession*>(__hip_atomic_load(
-        &sl->sessions, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-    a.gcm_tables = reinterpret_cast<const DevGcmTables*>(__hip_atomic_load(
-        &sl->gcm_tables, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-    a.descs = reinterpret_cast<const void*>(
-        __hip_atomic_load(&sl->job, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-    a.status = reinterpret_cast<int32_t*>(
-        __hip_atomic_load(&sl->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    a.sessions = reinterpret_cast<const DevSession*>(c->sessions);
+    a.gcm_tables = reinterpret_cast<const DevGcmTables*>(c->gcm_tables);
+    a.descs = &c->job;  // LDS, through a generic pointer
+    a.status = reinterpret_cast<int32_t*>(c->status);
     a.n = 1;
-    a.n_sessions = sys_load(&sl->n_sessions);
-    const uint32_t key = __builtin_amdgcn_readfirstlane(sys_load(&sl->key_id));
+    a.n_sessions = __builtin_amdgcn_readfirstlane(c->n_sessions);
+    const uint32_t key = __builtin_amdgcn_readfirstlane(c->key_id);
     const bool hit = key != 0 && key == cached_key;
     cached_key = key;
     switch (op) {

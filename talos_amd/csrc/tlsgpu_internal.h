@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstddef>
+
 #include "../../include/tlsgpu.h"
 
 namespace tg {
@@ -255,26 +257,33 @@ int launch_bs_ecb(const DevSession* sessions, uint32_t session, int rounds, cons
 int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, hipStream_t s);
 
 // Doorbell slot of the persistent EVP server (evp_server.hip, engine.cpp): one
-// per calling thread, in pinned host memory, one 128-B line each.  The thread
-// fills the job fields, then stores `post` (its next job number); a server
-// workgroup that sees post != the number it last served runs the job (one
-// RawJob, zero-copy in the thread's pinned staging) and stores `done` = post
-// after the job's output and status are visible to the host.
-struct alignas(128) DoorbellSlot {
+// per calling thread, in pinned host memory, 256 B.  The thread fills the job
+// (the RawJob itself and, when they fit, its nonce and AAD inline), then
+// stores `post` (its next job number); a server workgroup that sees post != the
+// number it last served copies the slot into LDS with one wave load, runs the
+// job (its input read from and its output and status written to the thread's
+// pinned staging buffer, zero-copy) and stores `done` = post after the output
+// and status are visible to the host.
+struct alignas(256) DoorbellSlot {
   uint32_t post;        // host: number of the posted job (written last)
   uint32_t done;        // device: number of the last job finished
-  uint32_t op;          // bit 0: seal; bits 8-15: AES rounds (10 / 14)
+  uint32_t op;          // bit 0: seal; bits 8-15: AES rounds (10 / 14); bit 16:
+                        // nonce (then AAD) inline in `inl`
   uint32_t n_sessions;  // capacity of the context's session table
-  uint64_t job;         // device address of the RawJob
-  uint64_t status;      // device address of the job's int32 status
-  uint64_t sessions;    // const DevSession* of the context's table
-  uint64_t gcm_tables;  // const DevGcmTables*
   uint32_t key_id;      // unique per installed key (process-wide): a server
                         // workgroup keeps the GCM tables of the last key it
                         // served in LDS and skips reloading them for the same id
-  uint8_t pad[76];
+  uint32_t reserved;
+  uint64_t status;      // device address of the job's int32 status
+  uint64_t sessions;    // const DevSession* of the context's table
+  uint64_t gcm_tables;  // const DevGcmTables*
+  RawJob job;           // 56 B; job.nonce / job.aad ignored when inline
+  uint8_t inl[152];     // inline nonce || AAD
 };
-static_assert(sizeof(DoorbellSlot) == 128, "DoorbellSlot layout");
+static_assert(sizeof(RawJob) == 56, "RawJob layout");
+static_assert(sizeof(DoorbellSlot) == 256 && offsetof(DoorbellSlot, job) == 48,
+              "DoorbellSlot layout");
+constexpr uint32_t kDoorbellInline = 152;
 struct ServerArgs {
   DoorbellSlot* slots;        // device view of the pinned slot array
   uint32_t nslots;
