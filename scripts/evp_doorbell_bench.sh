@@ -1,6 +1,6 @@
 #!/bin/bash
 # Per-call EVP rate, launched path vs the doorbell server (round 4):
-# AES-128-GCM seal through oracle/_ref/cpubench dlopen()ing libtlsgpu.so,
+# AES-128-GCM (and ChaCha20-Poly1305 at 1,400 B) seal through oracle/_ref/cpubench dlopen()ing libtlsgpu.so,
 # 1,400 B and 16 KiB, 1 / 16 / 64 threads; plus connection churn (init).
 # usage: scripts/evp_doorbell_bench.sh OUT.jsonl
 set -o pipefail
@@ -16,6 +16,14 @@ for len in 1400 16384; do
       TLSGPU_EVP_DOORBELL=$db timeout -k 10 60 "$R/oracle/_ref/cpubench" "$R/talos_amd/libtlsgpu.so" \
         aes-128-gcm seal $len $n $t 2 | sed "s/^{/{\"lib\": \"libtlsgpu per call doorbell=$db\", /" >> "$OUT" || exit 1
     done
+  done
+done
+for t in 1 16; do
+  TLSGPU_EVP_SPIN=0 timeout -k 10 60 "$R/oracle/_ref/cpubench" "$R/talos_amd/libtlsgpu.so" \
+    chacha20-poly1305 seal 1400 $((t * 8)) $t 2 | sed "s/^{/{\"lib\": \"libtlsgpu per call launch+eventsync\", /" >> "$OUT" || exit 1
+  for db in 0 16; do
+    TLSGPU_EVP_DOORBELL=$db timeout -k 10 60 "$R/oracle/_ref/cpubench" "$R/talos_amd/libtlsgpu.so" \
+      chacha20-poly1305 seal 1400 $((t * 8)) $t 2 | sed "s/^{/{\"lib\": \"libtlsgpu per call doorbell=$db\", /" >> "$OUT" || exit 1
   done
 done
 for t in 1 16; do

@@ -15,125 +15,11 @@
 // Mapping: one record per lane.  Poly1305 is a serial Horner chain with a
 // per-record key r, so a lane owns the whole chain (no cross-lane combine);
 // the VALU does ARX + 32x32->64 multiplies only, no LDS.
-#include "aes_common.h"
-#include "tlsgpu_internal.h"
+#include "chacha_wave.h"
 
 namespace tg {
 
 typedef __attribute__((address_space(4))) const uint32_t cu32c;
-
-__device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {
-  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
-}
-
-// Zero n bytes at d from one lane (a record whose tag failed,
-// e_chacha20poly1305.c:276-283 + evp_aead.c:137-143): 16-B stores for the
-// aligned bulk instead of one store per byte.
-__device__ __forceinline__ void zero_fill_lane(uint8_t* d, uint64_t n) {
-  uint64_t o = 0;
-  for (; o < n && (((uintptr_t)(d + o)) & 15); o++) d[o] = 0;
-  for (; o + 16 <= n; o += 16) *reinterpret_cast<uint4*>(d + o) = make_uint4(0, 0, 0, 0);
-  for (; o < n; o++) d[o] = 0;
-}
-
-#define CC_QR(a, b, c, d)            \
-  a += b; d = rotl32(d ^ a, 16);     \
-  c += d; b = rotl32(b ^ c, 12);     \
-  a += b; d = rotl32(d ^ a, 8);      \
-  c += d; b = rotl32(b ^ c, 7);
-
-__device__ __forceinline__ void chacha_block(const uint32_t in[16], uint32_t x[16]) {
-#pragma unroll
-  for (int i = 0; i < 16; i++) x[i] = in[i];
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-    CC_QR(x[0], x[4], x[8], x[12]);
-    CC_QR(x[1], x[5], x[9], x[13]);
-    CC_QR(x[2], x[6], x[10], x[14]);
-    CC_QR(x[3], x[7], x[11], x[15]);
-    CC_QR(x[0], x[5], x[10], x[15]);
-    CC_QR(x[1], x[6], x[11], x[12]);
-    CC_QR(x[2], x[7], x[8], x[13]);
-    CC_QR(x[3], x[4], x[9], x[14]);
-  }
-#pragma unroll
-  for (int i = 0; i < 16; i++) x[i] += in[i];
-}
-
-struct Poly {
-  uint32_t r0, r1, r2, r3, r4, s1, s2, s3, s4;
-  uint32_t h0, h1, h2, h3, h4;
-  uint32_t pad0, pad1, pad2, pad3;
-};
-
-__device__ __forceinline__ void poly_init(Poly& p, const uint32_t k[8]) {
-  // clamp r (poly1305-donna.c:59-64) on the key words
-  uint32_t t0 = k[0], t1 = k[1], t2 = k[2], t3 = k[3];
-  p.r0 = t0 & 0x3ffffff;
-  p.r1 = ((t0 >> 26) | (t1 << 6)) & 0x3ffff03;
-  p.r2 = ((t1 >> 20) | (t2 << 12)) & 0x3ffc0ff;
-  p.r3 = ((t2 >> 14) | (t3 << 18)) & 0x3f03fff;
-  p.r4 = (t3 >> 8) & 0x00fffff;
-  p.s1 = p.r1 * 5; p.s2 = p.r2 * 5; p.s3 = p.r3 * 5; p.s4 = p.r4 * 5;
-  p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0;
-  p.pad0 = k[4]; p.pad1 = k[5]; p.pad2 = k[6]; p.pad3 = k[7];
-}
-
-// One 16-byte block m (LE words) with the 2^128 bit given by hibit.
-__device__ __forceinline__ void poly_block(Poly& p, uint32_t m0, uint32_t m1, uint32_t m2,
-                                           uint32_t m3, uint32_t hibit) {
-  uint32_t h0 = p.h0 + (m0 & 0x3ffffff);
-  uint32_t h1 = p.h1 + (((m0 >> 26) | (m1 << 6)) & 0x3ffffff);
-  uint32_t h2 = p.h2 + (((m1 >> 20) | (m2 << 12)) & 0x3ffffff);
-  uint32_t h3 = p.h3 + (((m2 >> 14) | (m3 << 18)) & 0x3ffffff);
-  uint32_t h4 = p.h4 + ((m3 >> 8) | hibit);
-  uint64_t d0 = (uint64_t)h0 * p.r0 + (uint64_t)h1 * p.s4 + (uint64_t)h2 * p.s3 +
-                (uint64_t)h3 * p.s2 + (uint64_t)h4 * p.s1;
-  uint64_t d1 = (uint64_t)h0 * p.r1 + (uint64_t)h1 * p.r0 + (uint64_t)h2 * p.s4 +
-                (uint64_t)h3 * p.s3 + (uint64_t)h4 * p.s2;
-  uint64_t d2 = (uint64_t)h0 * p.r2 + (uint64_t)h1 * p.r1 + (uint64_t)h2 * p.r0 +
-                (uint64_t)h3 * p.s4 + (uint64_t)h4 * p.s3;
-  uint64_t d3 = (uint64_t)h0 * p.r3 + (uint64_t)h1 * p.r2 + (uint64_t)h2 * p.r1 +
-                (uint64_t)h3 * p.r0 + (uint64_t)h4 * p.s4;
-  uint64_t d4 = (uint64_t)h0 * p.r4 + (uint64_t)h1 * p.r3 + (uint64_t)h2 * p.r2 +
-                (uint64_t)h3 * p.r1 + (uint64_t)h4 * p.r0;
-  uint32_t c = (uint32_t)(d0 >> 26); h0 = (uint32_t)d0 & 0x3ffffff;
-  d1 += c; c = (uint32_t)(d1 >> 26); h1 = (uint32_t)d1 & 0x3ffffff;
-  d2 += c; c = (uint32_t)(d2 >> 26); h2 = (uint32_t)d2 & 0x3ffffff;
-  d3 += c; c = (uint32_t)(d3 >> 26); h3 = (uint32_t)d3 & 0x3ffffff;
-  d4 += c; c = (uint32_t)(d4 >> 26); h4 = (uint32_t)d4 & 0x3ffffff;
-  h0 += c * 5; c = h0 >> 26; h0 &= 0x3ffffff;
-  h1 += c;
-  p.h0 = h0; p.h1 = h1; p.h2 = h2; p.h3 = h3; p.h4 = h4;
-}
-
-// poly1305-donna.c:231-321: full carry, conditional subtract, + pad.
-__device__ __forceinline__ void poly_finish(const Poly& p, uint32_t mac[4]) {
-  uint32_t h0 = p.h0, h1 = p.h1, h2 = p.h2, h3 = p.h3, h4 = p.h4, c;
-  c = h1 >> 26; h1 &= 0x3ffffff;
-  h2 += c; c = h2 >> 26; h2 &= 0x3ffffff;
-  h3 += c; c = h3 >> 26; h3 &= 0x3ffffff;
-  h4 += c; c = h4 >> 26; h4 &= 0x3ffffff;
-  h0 += c * 5; c = h0 >> 26; h0 &= 0x3ffffff;
-  h1 += c;
-  uint32_t g0 = h0 + 5; c = g0 >> 26; g0 &= 0x3ffffff;
-  uint32_t g1 = h1 + c; c = g1 >> 26; g1 &= 0x3ffffff;
-  uint32_t g2 = h2 + c; c = g2 >> 26; g2 &= 0x3ffffff;
-  uint32_t g3 = h3 + c; c = g3 >> 26; g3 &= 0x3ffffff;
-  uint32_t g4 = h4 + c - (1u << 26);
-  uint32_t mask = (g4 >> 31) - 1;
-  h0 = (h0 & ~mask) | (g0 & mask);
-  h1 = (h1 & ~mask) | (g1 & mask);
-  h2 = (h2 & ~mask) | (g2 & mask);
-  h3 = (h3 & ~mask) | (g3 & mask);
-  h4 = (h4 & ~mask) | (g4 & mask);
-  uint32_t w0 = h0 | (h1 << 26), w1 = (h1 >> 6) | (h2 << 20), w2 = (h2 >> 12) | (h3 << 14),
-           w3 = (h3 >> 18) | (h4 << 8);
-  uint64_t f = (uint64_t)w0 + p.pad0; mac[0] = (uint32_t)f;
-  f = (uint64_t)w1 + p.pad1 + (f >> 32); mac[1] = (uint32_t)f;
-  f = (uint64_t)w2 + p.pad2 + (f >> 32); mac[2] = (uint32_t)f;
-  f = (uint64_t)w3 + p.pad3 + (f >> 32); mac[3] = (uint32_t)f;
-}
 
 // Byte-stream Poly1305 (poly1305-donna.c:176-212 buffering) for the draft
 // layout, whose segments are not 16-byte aligned.
@@ -588,6 +474,42 @@ __device__ __forceinline__ bool cc_parse_tls(const BatchArgs& a, uint32_t r, CcR
   return true;
 }
 
+// Raw EVP job -> CcRec (e_chacha20poly1305.c:124-286; the host checked
+// nonce_len, in_len >= tag_len and the output room).
+template <bool SEAL>
+__device__ __forceinline__ void cc_parse_raw(const RawJob& j, const DevSession* S, CcRec& rc,
+                                             uint32_t& tag_len) {
+  const uint32_t kind = S->kind;
+  tag_len = S->tag_len;
+  rc.old = kind == TLSGPU_CHACHA20_POLY1305_OLD;
+  const uint8_t* nonce = (const uint8_t*)j.nonce;
+  cc_state(rc.st, S);
+  if (!rc.old) {  // ctr = LE32(nonce[0..3]) << 32 ; iv = nonce + 4
+    rc.st[12] = 0;
+    rc.st[13] = ld_le32(nonce);
+    rc.st[14] = ld_le32(nonce + 4);
+    rc.st[15] = ld_le32(nonce + 8);
+  } else {
+    rc.st[12] = 0; rc.st[13] = 0;
+    rc.st[14] = ld_le32(nonce);
+    rc.st[15] = ld_le32(nonce + 4);
+  }
+  rc.src = (const uint8_t*)j.in;
+  rc.dst = (uint8_t*)j.out;
+  rc.aad_ptr = (const uint8_t*)j.aad;
+  rc.ad_len = j.aad_len;
+  if (SEAL) {
+    rc.n = j.in_len;
+    rc.tag_out = rc.dst + j.in_len;
+    rc.ok_status = (int32_t)(j.in_len + tag_len);
+  } else {
+    rc.n = j.in_len - tag_len;
+    rc.tag_in = rc.src + rc.n;
+    rc.ok_status = (int32_t)rc.n;
+  }
+  rc.zero_len = j.max_out;
+}
+
 // TLS batches: LDS-staged coalesced data path (cc_tls_wave), 4 waves per SIMD.
 template <bool SEAL>
 __global__ __launch_bounds__(kCcThreads) void chacha_tls_kernel(BatchArgs a) {
@@ -620,34 +542,7 @@ __global__ __launch_bounds__(256) void chacha_batch_kernel(BatchArgs a) {
       return;
     }
     if (kind != TLSGPU_CHACHA20_POLY1305 && kind != TLSGPU_CHACHA20_POLY1305_OLD) return;
-    tag_len = S->tag_len;
-    rc.old = kind == TLSGPU_CHACHA20_POLY1305_OLD;
-    const uint8_t* nonce = (const uint8_t*)j.nonce;
-    cc_state(rc.st, S);
-    if (!rc.old) {  // ctr = LE32(nonce[0..3]) << 32 ; iv = nonce + 4
-      rc.st[12] = 0;
-      rc.st[13] = ld_le32(nonce);
-      rc.st[14] = ld_le32(nonce + 4);
-      rc.st[15] = ld_le32(nonce + 8);
-    } else {
-      rc.st[12] = 0; rc.st[13] = 0;
-      rc.st[14] = ld_le32(nonce);
-      rc.st[15] = ld_le32(nonce + 4);
-    }
-    rc.src = (const uint8_t*)j.in;
-    rc.dst = (uint8_t*)j.out;
-    rc.aad_ptr = (const uint8_t*)j.aad;
-    rc.ad_len = j.aad_len;
-    if (SEAL) {
-      rc.n = j.in_len;
-      rc.tag_out = rc.dst + j.in_len;
-      rc.ok_status = (int32_t)(j.in_len + tag_len);
-    } else {
-      rc.n = j.in_len - tag_len;
-      rc.tag_in = rc.src + rc.n;
-      rc.ok_status = (int32_t)rc.n;
-    }
-    rc.zero_len = j.max_out;
+    cc_parse_raw<SEAL>(j, S, rc, tag_len);
   } else {
     if (OLD_ONLY) {  // the staged kernel leaves these records' statuses alone
       const tlsgpu_record d = reinterpret_cast<const tlsgpu_record*>(a.descs)[r];
@@ -657,6 +552,35 @@ __global__ __launch_bounds__(256) void chacha_batch_kernel(BatchArgs a) {
     if (!cc_parse_tls<SEAL>(a, r, rc, tag_len)) return;
   }
   cc_record<SEAL>(rc, tag_len, slot);
+}
+
+// Raw EVP jobs, one wave per job: the RFC 7539 AEAD on the whole wave
+// (chacha_wave.h: per-call latency), the draft AEAD on lane 0 (cc_record).
+template <bool SEAL>
+__global__ __launch_bounds__(kWave) void chacha_raw_wave_kernel(BatchArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage[4096];
+  const uint32_t r = blockIdx.x;
+  const RawJob j = reinterpret_cast<const RawJob*>(a.descs)[r];
+  int32_t* slot = a.status + r;
+  // no per-batch status memset for raw jobs (run_batch): as chacha_batch_kernel
+  if (j.session >= a.n_sessions) {
+    if (threadIdx.x == 0) *slot = TLSGPU_REC_PUBLIC_INVALID;
+    return;
+  }
+  const DevSession* S = a.sessions + j.session;
+  const uint32_t kind = S->kind;
+  if (kind < TLSGPU_AES_128_GCM || kind > TLSGPU_CHACHA20_POLY1305_OLD) {
+    if (threadIdx.x == 0) *slot = TLSGPU_REC_PUBLIC_INVALID;
+    return;
+  }
+  if (kind == TLSGPU_CHACHA20_POLY1305) {
+    cc_wave_job<SEAL>(j, S, slot, stage);
+  } else if (kind == TLSGPU_CHACHA20_POLY1305_OLD && threadIdx.x == 0) {
+    CcRec rc;
+    uint32_t tag_len;
+    cc_parse_raw<SEAL>(j, S, rc, tag_len);
+    cc_record<SEAL>(rc, tag_len, slot);
+  }
 }
 
 // TLSGPU_CHACHA_LEGACY=1 selects the per-lane data path for TLS batches too
@@ -674,6 +598,11 @@ int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, h
   if (a.n == 0) return 0;
   dim3 grid((a.n + 255) / 256), block(256);
   const bool staged = !raw && !getenv_legacy_chacha();
+  if (raw && !getenv_legacy_chacha()) {  // one wave per job
+    if (seal) hipLaunchKernelGGL((chacha_raw_wave_kernel<true>), dim3(a.n), dim3(kWave), 0, s, a);
+    else hipLaunchKernelGGL((chacha_raw_wave_kernel<false>), dim3(a.n), dim3(kWave), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   if (raw || !staged) {
     if (seal) {
       if (raw) hipLaunchKernelGGL((chacha_batch_kernel<true, true>), grid, block, 0, s, a);

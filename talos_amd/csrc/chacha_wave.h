@@ -1,0 +1,285 @@
+// chacha_wave.h — one ChaCha20-Poly1305 EVP job (RFC 7539 layout) on one
+// wave, for latency-bound per-call jobs: the launched raw path
+// (chacha_raw_wave_kernel) and the doorbell server (evp_server.hip).
+//
+// Replaces aead_chacha20_poly1305_seal/open (e_chacha20poly1305.c:124-286)
+// for the 12-byte-nonce AEAD.  The per-lane kernels run a job's keystream
+// blocks and its Poly1305 Horner chain serially on one lane; here the job is
+// spread over the 64 lanes of a wave:
+//
+//   * keystream: lane l computes block counter 64t + l in pass t (counter 0 is
+//     the one-time Poly1305 key, chacha20poly1305.c:178-180), XORs its 64
+//     bytes and stages the ciphertext of the pass in LDS (4 KiB);
+//   * Poly1305 over the N = ceil(|AD|/16) + ceil(|CT|/16) + 1 blocks
+//     c_0..c_{N-1} of AD || pad16 || CT || pad16 || le64 || le64 (:182-190):
+//     tag = (sum_b c_b r^(N-b) mod 2^130-5) + s.  Lane l takes the blocks
+//     b = l (mod 64) in order, Horner with r^64, and multiplies its sum by
+//     r^(N - b_last); the 64 lane sums are added across the wave.  The powers
+//     r^1..r^64 are built by doubling (6 multiplies per lane).
+//
+// The arithmetic is poly1305-donna's 26-bit limbs (chacha_common.h); the
+// result is the same field element as the serial chain's, so the tag is
+// identical (tests/test_evp*.py against the oracle).  Session words are read
+// by vector loads (the server's coherence rule, evp_server.hip).
+#pragma once
+#include "chacha_common.h"
+
+namespace tg {
+
+constexpr uint32_t kM26 = 0x3ffffff;
+
+// An element of GF(2^130-5) in five 26-bit limbs (limbs may exceed 2^26
+// slightly between carries, as in poly1305-donna).
+struct P5 {
+  uint32_t v0, v1, v2, v3, v4;
+};
+
+__device__ __forceinline__ P5 p5_block(uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3,
+                                       uint32_t hibit) {
+  return {m0 & kM26, ((m0 >> 26) | (m1 << 6)) & kM26, ((m1 >> 20) | (m2 << 12)) & kM26,
+          ((m2 >> 14) | (m3 << 18)) & kM26, (m3 >> 8) | hibit};
+}
+
+__device__ __forceinline__ P5 p5_add(const P5& a, const P5& b) {
+  return {a.v0 + b.v0, a.v1 + b.v1, a.v2 + b.v2, a.v3 + b.v3, a.v4 + b.v4};
+}
+
+// One serial carry pass (limbs < 2^31 in, donna's invariant out).
+__device__ __forceinline__ P5 p5_carry(P5 a) {
+  uint32_t c = a.v0 >> 26; a.v0 &= kM26;
+  a.v1 += c; c = a.v1 >> 26; a.v1 &= kM26;
+  a.v2 += c; c = a.v2 >> 26; a.v2 &= kM26;
+  a.v3 += c; c = a.v3 >> 26; a.v3 &= kM26;
+  a.v4 += c; c = a.v4 >> 26; a.v4 &= kM26;
+  a.v0 += c * 5; c = a.v0 >> 26; a.v0 &= kM26;
+  a.v1 += c;
+  return a;
+}
+
+// a * b mod 2^130-5 (poly1305-donna.c:135-172 with a general second operand).
+// Bounds: a's limbs < 2^27.1 (an accumulator plus a block), b's < 2^26.1 (a
+// product of this function or the clamped key): every column sum stays below
+// 2^57.5, the top column (no *5 terms) below 2^55.4, so each carry fits 32 bits.
+__device__ __forceinline__ P5 p5_mul(const P5& a, const P5& b) {
+  const uint32_t s1 = b.v1 * 5, s2 = b.v2 * 5, s3 = b.v3 * 5, s4 = b.v4 * 5;
+  uint64_t d0 = (uint64_t)a.v0 * b.v0 + (uint64_t)a.v1 * s4 + (uint64_t)a.v2 * s3 +
+                (uint64_t)a.v3 * s2 + (uint64_t)a.v4 * s1;
+  uint64_t d1 = (uint64_t)a.v0 * b.v1 + (uint64_t)a.v1 * b.v0 + (uint64_t)a.v2 * s4 +
+                (uint64_t)a.v3 * s3 + (uint64_t)a.v4 * s2;
+  uint64_t d2 = (uint64_t)a.v0 * b.v2 + (uint64_t)a.v1 * b.v1 + (uint64_t)a.v2 * b.v0 +
+                (uint64_t)a.v3 * s4 + (uint64_t)a.v4 * s3;
+  uint64_t d3 = (uint64_t)a.v0 * b.v3 + (uint64_t)a.v1 * b.v2 + (uint64_t)a.v2 * b.v1 +
+                (uint64_t)a.v3 * b.v0 + (uint64_t)a.v4 * s4;
+  uint64_t d4 = (uint64_t)a.v0 * b.v4 + (uint64_t)a.v1 * b.v3 + (uint64_t)a.v2 * b.v2 +
+                (uint64_t)a.v3 * b.v1 + (uint64_t)a.v4 * b.v0;
+  P5 h;
+  uint32_t c = (uint32_t)(d0 >> 26); h.v0 = (uint32_t)d0 & kM26;
+  d1 += c; c = (uint32_t)(d1 >> 26); h.v1 = (uint32_t)d1 & kM26;
+  d2 += c; c = (uint32_t)(d2 >> 26); h.v2 = (uint32_t)d2 & kM26;
+  d3 += c; c = (uint32_t)(d3 >> 26); h.v3 = (uint32_t)d3 & kM26;
+  d4 += c; c = (uint32_t)(d4 >> 26); h.v4 = (uint32_t)d4 & kM26;
+  h.v0 += c * 5; c = h.v0 >> 26; h.v0 &= kM26;
+  h.v1 += c;
+  return h;
+}
+
+__device__ __forceinline__ P5 p5_shfl(const P5& a, int src) {
+  return {(uint32_t)__shfl((int)a.v0, src), (uint32_t)__shfl((int)a.v1, src),
+          (uint32_t)__shfl((int)a.v2, src), (uint32_t)__shfl((int)a.v3, src),
+          (uint32_t)__shfl((int)a.v4, src)};
+}
+
+__device__ __forceinline__ P5 p5_readlane(const P5& a, int src) {
+  return {(uint32_t)__builtin_amdgcn_readlane((int)a.v0, src),
+          (uint32_t)__builtin_amdgcn_readlane((int)a.v1, src),
+          (uint32_t)__builtin_amdgcn_readlane((int)a.v2, src),
+          (uint32_t)__builtin_amdgcn_readlane((int)a.v3, src),
+          (uint32_t)__builtin_amdgcn_readlane((int)a.v4, src)};
+}
+
+// Up to 16 bytes at p (nb < 16: zero padded) as little-endian words.
+__device__ __forceinline__ void cw_load16(const uint8_t* p, uint32_t nb, bool aligned,
+                                          uint32_t w[4]) {
+  if (nb >= 16 && aligned) {
+    const uint4 t = *reinterpret_cast<const uint4*>(p);
+    w[0] = t.x; w[1] = t.y; w[2] = t.z; w[3] = t.w;
+    return;
+  }
+  w[0] = w[1] = w[2] = w[3] = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++)
+    if ((uint32_t)k < nb) w[k >> 2] |= (uint32_t)p[k] << (8 * (k & 3));
+}
+
+__device__ __forceinline__ void cw_store16(uint8_t* p, uint32_t nb, bool aligned,
+                                           const uint32_t w[4]) {
+  if (nb >= 16 && aligned) {
+    *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < 16; k++)
+    if ((uint32_t)k < nb) p[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+}
+
+__device__ __forceinline__ uint32_t cw_mac_byte(const uint32_t mac[4], uint32_t k) {
+  const uint32_t w = k < 4 ? mac[0] : k < 8 ? mac[1] : k < 12 ? mac[2] : mac[3];
+  return (w >> (8 * (k & 3))) & 0xFF;
+}
+
+// Run raw job j of the RFC 7539 AEAD on the calling wave (all 64 lanes).
+// S: the job's session (kind already checked); stage: 4 KiB of LDS, 16-B
+// aligned, owned by this wave.  Writes the output, the tag (seal) and
+// *status (lane 0); on a tag mismatch zero-fills j.max_out bytes
+// (evp_aead.c:137-143).  Host-side checks (nonce_len == 12, open in_len >=
+// tag_len, output room) are the caller's, as for the per-lane kernel.
+template <bool SEAL>
+__device__ void cc_wave_job(const RawJob& j, const DevSession* S, int32_t* status,
+                            uint8_t* stage) {
+  const uint32_t lane = threadIdx.x & 63;
+  // session words 0..7 (kind, rounds, tag_len, ...) and 72..79 (chacha_key)
+  const uint32_t* sw = reinterpret_cast<const uint32_t*>(S);
+  static_assert(offsetof(DevSession, chacha_key) == 72 * 4, "DevSession layout");
+  const uint32_t sv = sw[lane < 8 ? lane : 64 + (lane & 15)];
+  const uint32_t tag_len = __builtin_amdgcn_readlane(sv, 2);
+  uint32_t in[16];
+  in[0] = 0x61707865u; in[1] = 0x3320646eu; in[2] = 0x79622d32u; in[3] = 0x6b206574u;
+#pragma unroll
+  for (int i = 0; i < 8; i++) in[4 + i] = __builtin_amdgcn_readlane(sv, 8 + i);
+  // 12-byte nonce: 64-bit counter words 12-13 = 0 || LE32(nonce[0..3]),
+  // iv = nonce[4..11] (e_chacha20poly1305.c:140-150)
+  const uint8_t* nonce = reinterpret_cast<const uint8_t*>(j.nonce);
+  in[13] = ld_le32(nonce);
+  in[14] = ld_le32(nonce + 4);
+  in[15] = ld_le32(nonce + 8);
+
+  const uint32_t n = SEAL ? j.in_len : j.in_len - tag_len;
+  const uint32_t ad_len = j.aad_len;
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(j.in);
+  uint8_t* dst = reinterpret_cast<uint8_t*>(j.out);
+  const uint8_t* aad = reinterpret_cast<const uint8_t*>(j.aad);
+  const bool aligned = ((((uintptr_t)src) | ((uintptr_t)dst)) & 15) == 0;
+  const uint32_t na = (ad_len + 15) >> 4, nc = (n + 15) >> 4, N = na + nc + 1;
+  const uint32_t nkb = (n + 63) >> 6;            // keystream blocks of data
+  const uint32_t passes = (nkb + 1 + 63) >> 6;   // counters 0..nkb
+
+  P5 acc = {0, 0, 0, 0, 0}, pw = {0, 0, 0, 0, 0}, r64 = {0, 0, 0, 0, 0};
+  uint32_t pad[4] = {0, 0, 0, 0};
+  for (uint32_t t = 0; t < passes; t++) {
+    const uint32_t ctr = 64 * t + lane;
+    uint32_t ks[16];
+    in[12] = ctr;
+    chacha_block(in, ks);
+    if (t == 0) {
+      // one-time key from lane 0's block 0: r (clamped) and s
+      uint32_t k[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) k[i] = __builtin_amdgcn_readlane(ks[i], 0);
+      Poly p;
+      poly_init(p, k);
+      pad[0] = k[4]; pad[1] = k[5]; pad[2] = k[6]; pad[3] = k[7];
+      // lane l: r^(l+1), by doubling
+      pw = {p.r0, p.r1, p.r2, p.r3, p.r4};
+#pragma unroll
+      for (int lev = 0; lev < 6; lev++) {
+        const int step = 1 << lev;
+        const P5 base = p5_readlane(pw, step - 1);          // r^step
+        const P5 lo = p5_shfl(pw, (int)lane - step);        // r^(l-step+1)
+        const P5 m = p5_mul(lo, base);
+        if ((int)lane >= step && (int)lane < 2 * step) pw = m;
+      }
+      r64 = p5_readlane(pw, 63);
+      // AD blocks b = lane, lane + 64, ... (zero padded to 16)
+      for (uint32_t b = lane; b < na; b += 64) {
+        uint32_t w[4];
+        const uint32_t o = 16 * b;
+        cw_load16(aad + o, min(16u, ad_len - o), false, w);
+        acc = p5_add(p5_mul(acc, r64), p5_block(w[0], w[1], w[2], w[3], 1u << 24));
+      }
+    }
+    // data: keystream block kb = ctr - 1 covers bytes [64 kb, 64 kb + 64);
+    // its ciphertext goes to stage[64 lane ..] (data block i at
+    // 16 (i - 256 t + 4))
+    if (ctr >= 1 && ctr - 1 < nkb) {
+      const uint32_t kb = ctr - 1;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t o = 64 * kb + 16 * q;
+        if (o < n) {
+          const uint32_t nb = min(16u, n - o);
+          uint32_t x[4], y[4];
+          cw_load16(src + o, nb, aligned, x);
+#pragma unroll
+          for (int w = 0; w < 4; w++) y[w] = x[w] ^ ks[4 * q + w];
+          if (nb < 16) {  // the MAC sees zero padding
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+              const int32_t b = (int32_t)nb - 4 * w;
+              y[w] &= b >= 4 ? 0xFFFFFFFFu : (b <= 0 ? 0u : ((1u << (8 * b)) - 1u));
+            }
+          }
+          cw_store16(dst + o, nb, aligned, y);
+          const uint32_t* c = SEAL ? y : x;
+          *reinterpret_cast<uint4*>(stage + 64 * lane + 16 * q) = make_uint4(c[0], c[1], c[2], c[3]);
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // this pass's data blocks [lo, hi) in Poly1305 order: block b = na + i
+    // belongs to lane b mod 64
+    const uint32_t lo = t == 0 ? 0u : 256 * t - 4, hi = min(nc, 256 * t + 252);
+    const uint32_t i0 = lo + ((lane - na - lo) & 63);
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+      const uint32_t i = i0 + 64 * s;
+      if (i < hi) {
+        const uint4 c = *reinterpret_cast<const uint4*>(stage + 16 * (i - 256 * t + 4));
+        acc = p5_add(p5_mul(acc, r64), p5_block(c.x, c.y, c.z, c.w, 1u << 24));
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  // le64(|AD|) || le64(|CT|) is block N-1
+  if (lane == ((N - 1) & 63)) acc = p5_add(p5_mul(acc, r64), p5_block(ad_len, 0, n, 0, 1u << 24));
+  // weight r^(N - b_last) for the lane's last block
+  const uint32_t w = lane < N ? N - (lane + 64 * ((N - 1 - lane) >> 6)) : 1u;
+  acc = p5_mul(acc, p5_shfl(pw, (int)w - 1));
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const P5 o = {(uint32_t)__shfl_xor((int)acc.v0, off), (uint32_t)__shfl_xor((int)acc.v1, off),
+                  (uint32_t)__shfl_xor((int)acc.v2, off), (uint32_t)__shfl_xor((int)acc.v3, off),
+                  (uint32_t)__shfl_xor((int)acc.v4, off)};
+    acc = p5_carry(p5_add(acc, o));
+  }
+  Poly p = {};
+  p.h0 = acc.v0; p.h1 = acc.v1; p.h2 = acc.v2; p.h3 = acc.v3; p.h4 = acc.v4;
+  p.pad0 = pad[0]; p.pad1 = pad[1]; p.pad2 = pad[2]; p.pad3 = pad[3];
+  uint32_t mac[4];
+  poly_finish(p, mac);
+  if (SEAL) {
+    if (lane < tag_len) dst[n + lane] = (uint8_t)cw_mac_byte(mac, lane);
+    if (lane == 0) *status = (int32_t)(n + tag_len);
+    return;
+  }
+  const uint8_t* tag_in = src + n;
+  const bool bad = lane < tag_len && (tag_in[lane] ^ cw_mac_byte(mac, lane)) != 0;
+  if (__ballot(bad) == 0) {
+    if (lane == 0) *status = (int32_t)n;
+    return;
+  }
+  // the plaintext stores are ordered before the zero-fill
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  const uint64_t z = j.max_out;
+  const bool zal = (((uintptr_t)dst) & 15) == 0;
+  for (uint64_t o = 16 * (uint64_t)lane; o < z; o += 1024) {
+    const uint32_t zero[4] = {0, 0, 0, 0};
+    cw_store16(dst + o, z - o < 16 ? (uint32_t)(z - o) : 16u, zal, zero);
+  }
+  if (lane == 0) *status = TLSGPU_REC_BAD_MAC;
+}
+
+}  // namespace tg

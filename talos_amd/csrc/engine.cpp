@@ -1835,9 +1835,10 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
   *reinterpret_cast<int32_t*>(h + o_status) = TLSGPU_REC_PUBLIC_INVALID;
   if (!zc && hipMemcpyAsync(d, h, o_status + 4, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
   const bool gcm = st->kind == TLSGPU_AES_128_GCM || st->kind == TLSGPU_AES_256_GCM;
-  // doorbell (zero-copy AES-GCM calls): post the job to a resident server
-  // workgroup instead of launching; the staging buffer is the job's memory
-  if (zc && gcm) {
+  // doorbell (zero-copy AES-GCM and RFC 7539 ChaCha20-Poly1305 calls): post
+  // the job to a resident server workgroup instead of launching; the staging
+  // buffer is the job's memory
+  if (zc && (gcm || st->kind == TLSGPU_CHACHA20_POLY1305)) {
     EvpServer* sv = evp_server(st->evp_dev, e);
     uint32_t* seq = nullptr;
     DoorbellSlot* slot = sv ? thread_slot(sv, st->evp_dev, &seq) : nullptr;
@@ -1849,8 +1850,10 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
       // the job travels in the slot (one wave load brings it to the server),
       // nonce and AAD inline when they fit
       const bool inl = nonce_len + ad_len <= kDoorbellInline;
-      slot->op = (uint32_t)(seal ? 1 : 0) | ((st->kind == TLSGPU_AES_128_GCM ? 10u : 14u) << 8) |
-                 (inl ? 1u << 16 : 0u);
+      const uint32_t kop = st->kind == TLSGPU_AES_128_GCM   ? 10u
+                           : st->kind == TLSGPU_AES_256_GCM ? 14u
+                                                            : 20u;  // ChaCha (evp_server.hip)
+      slot->op = (uint32_t)(seal ? 1 : 0) | (kop << 8) | (inl ? 1u << 16 : 0u);
       slot->n_sessions = st->sess->capacity;
       memcpy(&slot->job, j, sizeof(RawJob));
       if (inl) {

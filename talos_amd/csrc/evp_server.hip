@@ -26,13 +26,35 @@
 // while an instance that will poll for at least half a lifetime is queued.
 #define TG_VECTOR_SESSION_LOADS 1
 #include "gcm_raw.h"
+#include "chacha_wave.h"
 
 namespace tg {
 
 constexpr uint32_t kSrvExit = 0xFFFFFFFFu;
 constexpr uint32_t SRV_SEL_OFF = PLAN_OFF + 16 * 16;  // after gcm_raw_job's part_y words
 constexpr uint32_t SRV_SLOT_OFF = PLAN_OFF + 512;     // LDS copy of the picked slot (256 B)
-static_assert(SRV_SLOT_OFF + sizeof(DoorbellSlot) <= LDS_BYTES, "server LDS plan");
+constexpr uint32_t SRV_STAGE_OFF = PLAN_OFF + 1024;   // ChaCha job: wave 0's 4 KiB stage
+static_assert(SRV_SLOT_OFF + sizeof(DoorbellSlot) <= SRV_STAGE_OFF, "server LDS plan");
+static_assert(SRV_STAGE_OFF + 4096 <= LDS_BYTES, "server LDS plan");
+
+// A ChaCha20-Poly1305 (RFC 7539) job on wave 0 (chacha_wave.h); the session's
+// kind word by a vector load (lane-varying address), as everything else here.
+template <bool SEAL>
+__device__ __forceinline__ void srv_chacha_job(const BatchArgs& a, const RawJob& j) {
+  if (threadIdx.x >= kWave) return;
+  const uint32_t sid = j.session;
+  if (sid >= a.n_sessions) {
+    if (threadIdx.x == 0) a.status[0] = TLSGPU_REC_PUBLIC_INVALID;
+    return;
+  }
+  const DevSession* S = a.sessions + sid;
+  const uint32_t kw = reinterpret_cast<const uint32_t*>(S)[threadIdx.x & 7];
+  if (__builtin_amdgcn_readlane(kw, 0) != TLSGPU_CHACHA20_POLY1305) {
+    if (threadIdx.x == 0) a.status[0] = TLSGPU_REC_PUBLIC_INVALID;
+    return;
+  }
+  cc_wave_job<SEAL>(j, S, a.status, s_lds + SRV_STAGE_OFF);
+}
 
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -103,12 +125,15 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
     a.n_sessions = __builtin_amdgcn_readfirstlane(c->n_sessions);
     const uint32_t key = __builtin_amdgcn_readfirstlane(c->key_id);
     const bool hit = key != 0 && key == cached_key;
+    const uint32_t prev_key = cached_key;  // a ChaCha job leaves the GCM tables alone
     cached_key = key;
     switch (op) {
       case 10 << 8: gcm_raw_job<false, 10>(a, 0, hit); break;
       case (10 << 8) | 1: gcm_raw_job<true, 10>(a, 0, hit); break;
       case 14 << 8: gcm_raw_job<false, 14>(a, 0, hit); break;
       case (14 << 8) | 1: gcm_raw_job<true, 14>(a, 0, hit); break;
+      case 20 << 8: srv_chacha_job<false>(a, c->job); cached_key = prev_key; break;
+      case (20 << 8) | 1: srv_chacha_job<true>(a, c->job); cached_key = prev_key; break;
       default:  // not a job this server runs (the host never posts one)
         if (threadIdx.x == 0) a.status[0] = TLSGPU_REC_PUBLIC_INVALID;
         cached_key = 0;

@@ -1,13 +1,15 @@
 """The doorbell server for per-call EVP jobs (round 4, talos_amd/csrc/evp_server.hip,
 include/tlsgpu.h tlsgpu_evp_set_doorbell): with TLSGPU_EVP_DOORBELL set, a
-synchronous EVP_AEAD_CTX_seal / _open on an AES-GCM context is posted to a
-resident server workgroup instead of launching a kernel.  Every output must
+synchronous EVP_AEAD_CTX_seal / _open on an AES-GCM or RFC 7539
+ChaCha20-Poly1305 context is posted to a resident server workgroup instead of
+launching a kernel.  Every output must
 be the oracle's (e_aes.c:1424-1510 through evp_aead.c:89-144: tag, zero-fill
 and return 0 on a bad tag, odd nonce lengths, truncated tags), with threads
 cycling init / seal / open / cleanup so session slots are re-keyed while the
 server runs, across server relaunches (short lifetime), and the server must
-stop by itself when the calls stop.  ChaCha20-Poly1305 contexts keep the
-launched path in the same process."""
+stop by itself when the calls stop.  ChaCha jobs run on the server's wave 0
+(chacha_wave.h) between GCM jobs, whose LDS table cache they must leave
+intact."""
 import os
 import subprocess
 import sys

@@ -146,6 +146,39 @@ def test_evp_gcm_split_jobs(ta, oracle, name):
         g.cleanup()
 
 
+@pytest.mark.parametrize("name", ["chacha20-poly1305", "chacha20-poly1305-old"])
+def test_evp_chacha_wave_jobs(ta, oracle, name):
+    """Raw ChaCha20-Poly1305 jobs run one per wave (chacha_wave.h for the RFC
+    7539 AEAD: 64 keystream blocks per pass, Poly1305 split over the lanes by
+    block index mod 64 and recombined with r^1..r^64; the draft AEAD on lane
+    0).  Lengths around the pass boundary (63 data blocks in pass 0, 64 after),
+    AD longer than 64 Poly1305 blocks, short tags; seal equals the oracle, open
+    round-trips, a flipped byte anywhere zero-fills the whole max_out."""
+    kind = KINDS[name]
+    rnd = random.Random(93)
+    key = bytes(rnd.randrange(256) for _ in range(32))
+    nlen = 12 if kind == po.CHACHA20_POLY1305 else 8
+    for n, ad_len, tag_len in ((0, 0, 16), (0, 13, 16), (1, 0, 16), (15, 13, 16),
+                               (1400, 13, 16), (4031, 13, 16), (4032, 13, 16), (4033, 13, 12),
+                               (4096, 0, 16), (8128, 17, 16), (8129, 1024, 16),
+                               (16384, 13, 16), (16400, 2049, 13), (70001, 13, 16)):
+        nonce = bytes(rnd.randrange(256) for _ in range(nlen))
+        ad = bytes(rnd.randrange(256) for _ in range(ad_len))
+        pt = np.random.default_rng(n + 7).integers(0, 256, n, dtype=np.uint8).tobytes()
+        octx = oracle.aead(kind, key, tag_len)
+        ok, exp = oracle.seal(octx, nonce, pt, ad)
+        g = ta.EvpAead(kind, key, tag_len)
+        ok2, got, _ = g.seal(nonce, pt, ad)
+        assert ok == ok2 == 1 and got == exp, (n, ad_len, tag_len)
+        ok3, back, ol = g.open(nonce, got, ad)
+        assert ok3 == 1 and back == pt and ol == n, n
+        bad = bytearray(got)
+        bad[rnd.randrange(len(bad))] ^= 0x10
+        ok4, z, ol = g.open(nonce, bytes(bad), ad, max_out=n + 5)
+        assert ok4 == 0 and z == bytes(n + 5) and ol == 0, n
+        g.cleanup()
+
+
 # ------------------------------------------------------------- batch records
 
 def _mk_sessions(ta, rnd, kinds_per_sid):
