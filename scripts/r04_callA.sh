@@ -12,6 +12,7 @@ step() {  # name timeout cmd...
   [ $rc -ge 124 ] && exit $rc
   return 0
 }
+step ubench5 60 tools/ubench set5
 step chacha_wave 200 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread -m gpu -k "chacha_wave or aeadtests"
 step doorbell_test 240 python -u -m pytest tests/test_evp_doorbell.py -x -v --timeout 120 --timeout-method thread -m gpu
 step doorbell_bench 400 scripts/evp_doorbell_bench.sh "${O}_doorbell_bench.jsonl"

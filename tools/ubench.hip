@@ -32,6 +32,8 @@
 #include <cstring>
 #include <vector>
 
+#include "../talos_amd/csrc/chacha_common.h"  // set5: the production ChaCha20 / Poly1305 code
+
 #define CK(x)                                                                   \
   do {                                                                          \
     hipError_t e_ = (x);                                                        \
@@ -806,6 +808,101 @@ static void copy() {
   CK(hipFree(b));
 }
 
+
+// ---------------------------------------------------------------------------
+// set5: config C's compute alone (registers only, no memory): NB ChaCha20
+// blocks per lane per iteration (written interleaved: 4*NB independent
+// quarter rounds per round) and NP Poly1305 blocks (one serial chain),
+// chacha_block / poly_block from talos_amd/csrc/chacha_common.h.  By waves
+// per SIMD: the issue ceiling the staged kernel (4 waves per SIMD) sits under.
+template <int NB, int NP>
+__global__ void cc_compute_kernel(int iters, Stamp* st, uint32_t* out) {
+  using tg::rotl32;
+  extern __shared__ uint32_t pad[];  // occupancy guard only
+  if (iters < 0) pad[threadIdx.x] = 0;
+  uint32_t in[NB][16];
+#pragma unroll
+  for (int b = 0; b < NB; b++)
+#pragma unroll
+    for (int i = 0; i < 16; i++) in[b][i] = threadIdx.x * 2654435761u + 77 * i + b;
+  tg::Poly p;
+  uint32_t k8[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) k8[i] = threadIdx.x * 40503u + i;
+  tg::poly_init(p, k8);
+  uint32_t acc = 0;
+  unsigned long long t0, r0;
+  stamp_begin(st, &t0, &r0);
+  for (int it = 0; it < iters; it++) {
+    uint32_t x[NB][16];
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+      in[b][12] = it;
+#pragma unroll
+      for (int i = 0; i < 16; i++) x[b][i] = in[b][i];
+    }
+#pragma unroll
+    for (int r = 0; r < 10; r++) {
+#pragma unroll
+      for (int b = 0; b < NB; b++) {
+        CC_QR(x[b][0], x[b][4], x[b][8], x[b][12]);
+        CC_QR(x[b][1], x[b][5], x[b][9], x[b][13]);
+        CC_QR(x[b][2], x[b][6], x[b][10], x[b][14]);
+        CC_QR(x[b][3], x[b][7], x[b][11], x[b][15]);
+      }
+#pragma unroll
+      for (int b = 0; b < NB; b++) {
+        CC_QR(x[b][0], x[b][5], x[b][10], x[b][15]);
+        CC_QR(x[b][1], x[b][6], x[b][11], x[b][12]);
+        CC_QR(x[b][2], x[b][7], x[b][8], x[b][13]);
+        CC_QR(x[b][3], x[b][4], x[b][9], x[b][14]);
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; b++)
+#pragma unroll
+      for (int i = 0; i < 16; i++) x[b][i] += in[b][i];
+#pragma unroll
+    for (int q = 0; q < NP; q++) {
+      const uint32_t* m = x[q % NB] + 4 * (q & 3);
+      tg::poly_block(p, m[0], m[1], m[2], m[3], 1u << 24);
+    }
+#pragma unroll
+    for (int b = 0; b < NB; b++) acc ^= x[b][0] ^ x[b][7] ^ x[b][15];
+  }
+  stamp_end(st, t0, r0, acc ^ p.h0 ^ p.h4, out);
+}
+
+static void set5() {
+  // waves per SIMD W: 1,024-thread workgroups (4 waves per SIMD each), one
+  // (96 KiB LDS) or two (64 KiB) per CU; 256 * W threads for W < 4
+  auto one = [&](int nb, int np, int W) {
+    const int iters = 256;
+    const int threads = W >= 4 ? 1024 : 256 * W;
+    const size_t lds = W == 8 ? 64 * 1024 : 96 * 1024;
+    const int groups = W == 8 ? 2 * g_cus : g_cus;
+    auto launch = [&](int th, size_t l) {
+#define K(NB, NP) if (nb == NB && np == NP) cc_compute_kernel<NB, NP><<<groups, th, l>>>(iters, g_st, g_out);
+      K(1, 0) K(1, 4) K(2, 8) K(1, 1)
+#undef K
+    };
+    Res r = run(launch, threads, lds);
+    // every wave runs iters x nb blocks of 64 B per lane; cycles per SIMD per
+    // 4 KiB (one wave-block) with W waves sharing the SIMD
+    const double wave_blocks = (double)iters * nb;
+    const double simd_cycles_per_wave_block = r.med_cycles / (wave_blocks * W);
+    const double chip_bps = 4096.0 * 4 * g_cus * r.clock_ghz * 1e9 / simd_cycles_per_wave_block;
+    printf("{\"bench\": \"cc_compute\", \"chacha_blocks_per_lane\": %d, \"poly_blocks_per_iter\": %d, "
+           "\"waves_per_simd\": %d, \"simd_cycles_per_wave_block\": %.1f, \"chip_GBps_one_direction\": %.0f, "
+           "\"clock_ghz\": %.3f}\n",
+           nb, np, W, simd_cycles_per_wave_block, chip_bps / 1e9, r.clock_ghz);
+  };
+  for (int W : {1, 2, 3, 4, 8}) one(1, 0, W);  // 36 VGPRs: 8 waves per SIMD fit
+  for (int W : {1, 2, 3, 4}) one(1, 4, W);     // 71 VGPRs
+  for (int W : {2, 4}) one(2, 8, W);
+  for (int W : {4}) one(1, 1, W);
+}
+
 static void set4() {
   for (int op : {OP_PERM, OP_BITOP3, OP_ALIGNBIT, OP_ANDOR, OP_PKSWAP, OP_BFE, OP_LSHLOR})
     for (int w : {1, 4}) valu(op, w);
@@ -1054,6 +1151,16 @@ int main(int argc, char** argv) {
         (const void*)aes_v2_kernel<1, 3>, (const void*)aes_v2_kernel<2, 0>, (const void*)aes_v2_kernel<2, 1>,
         (const void*)aes_v2_kernel<2, 2>, (const void*)aes_v2_kernel<2, 3>})
     CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+  for (const void* f :
+       {(const void*)cc_compute_kernel<1, 0>,
+        (const void*)cc_compute_kernel<1, 4>, (const void*)cc_compute_kernel<2, 8>,
+        (const void*)cc_compute_kernel<1, 1>})
+    CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+  if (argc > 1 && !strcmp(argv[1], "set5")) {
+    set5();
+    fflush(stdout);
+    return 0;
+  }
   if (argc > 1 && !strcmp(argv[1], "set4")) {
     set4();
     if (argc > 2) set3();
