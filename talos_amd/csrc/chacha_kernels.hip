@@ -614,8 +614,14 @@ int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, h
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
   if (rfc) {
-    if (seal) hipLaunchKernelGGL((chacha_tls_kernel<true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((chacha_tls_kernel<false>), grid, block, 0, s, a);
+    // TLSGPU_CC_LDS_PAD=<bytes> (A/B only): unused dynamic LDS per 4-wave
+    // workgroup, which lowers the waves per SIMD (40 KiB static: 1 B more = 3)
+    static const unsigned pad = [] {
+      const char* e = getenv("TLSGPU_CC_LDS_PAD");
+      return e ? (unsigned)strtoul(e, nullptr, 10) : 0u;
+    }();
+    if (seal) hipLaunchKernelGGL((chacha_tls_kernel<true>), grid, block, pad, s, a);
+    else hipLaunchKernelGGL((chacha_tls_kernel<false>), grid, block, pad, s, a);
   }
   if (old) {
     if (seal) hipLaunchKernelGGL((chacha_batch_kernel<true, false, true>), grid, block, 0, s, a);

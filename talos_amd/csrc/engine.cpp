@@ -1609,6 +1609,12 @@ struct EvpServer {
   uint64_t deadline_ns = 0;       // post only before this (host clock), else relaunch
   std::vector<uint32_t> free_slots;
   std::atomic<uint64_t> jobs{0}, launches{0};
+  // TLSGPU_EVP_DOORBELL_TRACE=1: per-slot device timestamps (pinned) and their
+  // sums, printed at exit: pick -> slot loaded -> job done -> released (ticks
+  // of 10 ns), and the caller's post -> done-seen wall time (ns)
+  uint64_t* trace = nullptr;
+  uint64_t* d_trace = nullptr;
+  std::atomic<uint64_t> tr_n{0}, tr_load{0}, tr_job{0}, tr_rel{0}, tr_host_ns{0};
 };
 static EvpServer* g_servers[kMaxEvpDevices] = {};
 static std::mutex g_server_mu;
@@ -1630,9 +1636,23 @@ static uint64_t mono_ns() {
 
 // stop every server at exit: one host store each (no HIP call: the runtime
 // may already be going away); an instance exits within one poll
+static const bool g_doorbell_trace = [] {
+  const char* v = getenv("TLSGPU_EVP_DOORBELL_TRACE");
+  return v && *v && *v != '0';
+}();
+
 static void servers_stop_at_exit() {
   for (EvpServer* sv : g_servers)
     if (sv && sv->stop) __atomic_store_n(sv->stop, 1u, __ATOMIC_RELEASE);
+  for (EvpServer* sv : g_servers) {
+    const uint64_t n = sv ? sv->tr_n.load() : 0;
+    if (!n) continue;
+    fprintf(stderr,
+            "{\"doorbell_trace\": {\"jobs\": %llu, \"us_slot_load\": %.2f, \"us_job\": %.2f, "
+            "\"us_release\": %.2f, \"us_host_round_trip\": %.2f}}\n",
+            (unsigned long long)n, sv->tr_load.load() * 0.01 / n, sv->tr_job.load() * 0.01 / n,
+            sv->tr_rel.load() * 0.01 / n, sv->tr_host_ns.load() * 1e-3 / n);
+  }
 }
 
 // The server of EVP device k (created on first use when the doorbell is on).
@@ -1662,6 +1682,10 @@ static EvpServer* evp_server(size_t k, tlsgpu_engine* e) {
     if (stop) (void)hipHostFree(stop);
     return nullptr;
   }
+  if (g_doorbell_trace &&
+      (hipHostMalloc((void**)&sv->trace, 32 * sv->nslots, hipHostMallocDefault) != hipSuccess ||
+       hipHostGetDevicePointer((void**)&sv->d_trace, sv->trace, 0) != hipSuccess))
+    sv->trace = sv->d_trace = nullptr;
   *stop = 0;
   sv->stop = stop;
   for (uint32_t i = sv->nslots; i-- > 0;) sv->free_slots.push_back(i);
@@ -1683,6 +1707,7 @@ static bool server_ensure(EvpServer* sv) {
   a.nslots = sv->nslots;
   a.stop = sv->d_stop;
   a.lifetime = sv->lifetime_ns / 10;  // 100 MHz realtime ticks
+  a.trace = reinterpret_cast<unsigned long long*>(sv->d_trace);
   if (launch_evp_server(a, (int)sv->groups, sv->stream) != 0) return false;
   sv->deadline_ns = now + sv->lifetime_ns / 2;
   sv->launches.fetch_add(1, std::memory_order_relaxed);
@@ -1877,6 +1902,14 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
         }
       }
       sv->jobs.fetch_add(1, std::memory_order_relaxed);
+      if (sv->trace) {
+        const uint64_t* tr = sv->trace + 4 * (size_t)(slot - sv->slots);
+        sv->tr_n.fetch_add(1, std::memory_order_relaxed);
+        sv->tr_load.fetch_add(tr[1] - tr[0], std::memory_order_relaxed);
+        sv->tr_job.fetch_add(tr[2] - tr[1], std::memory_order_relaxed);
+        sv->tr_rel.fetch_add(tr[3] - tr[2], std::memory_order_relaxed);
+        sv->tr_host_ns.fetch_add(mono_ns() - t0, std::memory_order_relaxed);
+      }
       const int32_t status = *reinterpret_cast<const int32_t*>(h + o_status);
       if (status < 0) {  // the kernel's zero-fill of max_out_len bytes (evp_aead.c:137-143)
         if (max_out_len) memset(out, 0, max_out_len);

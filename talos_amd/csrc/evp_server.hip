@@ -73,6 +73,7 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
   uint32_t served = 0;
   if (wave == 0 && mine < s.nslots) served = sys_load(&s.slots[mine].done);
   uint32_t cached_key = 0;  // key id whose GCM tables are in LDS (0: none)
+  unsigned long long t_pick = 0, t_loaded = 0;  // trace (wave 0)
   for (;;) {
     if (wave == 0) {
       uint32_t pick = kSrvExit;
@@ -81,6 +82,7 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
         const unsigned long long m = __ballot(ready);
         if (m) {
           pick = blockIdx.x + (uint32_t)(__ffsll((long long)m) - 1) * gridDim.x;
+          t_pick = __builtin_amdgcn_s_memrealtime();
           break;
         }
         // the stop word and the clock every 16 polls (each poll is a PCIe read)
@@ -108,6 +110,7 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
         __atomic_thread_fence(__ATOMIC_ACQUIRE);
       }
       __builtin_amdgcn_s_waitcnt(0);
+      t_loaded = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();
     const uint32_t k = __builtin_amdgcn_readfirstlane(*sel);
@@ -142,9 +145,18 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
     // every wave's output stores complete, then one release publishes them;
     // the asm wait keeps the flag behind the write-back (MI355X_MICROARCH.md,
     // compiler hazard: hipcc drops the vmcnt wait after buffer_wbl2 here)
+    const unsigned long long t_job = __builtin_amdgcn_s_memrealtime();
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     if (threadIdx.x == 0) {
+      if (s.trace) {  // diagnostic: ordered before `done` by the release below
+        unsigned long long* tr = s.trace + 4 * (size_t)k;
+        __hip_atomic_store(tr + 0, t_pick, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(tr + 1, t_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(tr + 2, t_job, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(tr + 3, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       __atomic_thread_fence(__ATOMIC_RELEASE);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_store(&sl->done, post, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

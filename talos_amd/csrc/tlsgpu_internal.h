@@ -289,6 +289,8 @@ struct ServerArgs {
   uint32_t nslots;
   const uint32_t* stop;       // pinned word: non-zero = exit now
   unsigned long long lifetime;  // s_memrealtime ticks (100 MHz) a workgroup serves at most
+  unsigned long long* trace;    // null, or pinned [nslots][4]: realtime at pick, slot
+                                // loaded, job done, answer released (TLSGPU_EVP_DOORBELL_TRACE)
 };
 int launch_evp_server(const ServerArgs& a, int groups, hipStream_t s);
 int launch_session_install_arg(DevSession* sessions, DevGcmTables* tables,
