@@ -1791,13 +1791,16 @@ static int evp_queue_call(EvpBatcher* b, const AeadState* st, bool seal, unsigne
                           size_t nonce_len, const unsigned char* in, size_t in_len,
                           const unsigned char* ad, size_t ad_len);
 
-// Wait for a per-call event by polling it (round 4): hipEventSynchronize
-// measured 5-6 µs slower per call than a host spin on the kernel's own
-// completion word (tools/doorbell_probe.hip: 15.4 vs 9.6 µs for a 1,400-B
-// job); TLSGPU_EVP_SPIN=0 restores the blocking wait.
+// Wait for a per-call event: blocking (hipEventSynchronize), or with
+// TLSGPU_EVP_SPIN=1 by polling hipEventQuery.  The probe had a host spin on
+// the kernel's own completion word 5-6 µs faster than the blocking wait
+// (tools/doorbell_probe.hip: 9.6 vs 15.4 µs for a 1,400-B job), but polling
+// the event measured no better in the library (profiles/r04h_doorbell_bench:
+// 36.1 vs 37.6 K calls/s at 1 thread, 42.0 vs 45.2 K at 64) and burns a core
+// per waiting thread, so the blocking wait stays the default.
 static const bool g_evp_spin = [] {
   const char* v = getenv("TLSGPU_EVP_SPIN");
-  return !(v && *v == '0');
+  return v && *v && *v != '0';
 }();
 static bool event_spin(hipEvent_t ev) {
   if (!g_evp_spin) return hipEventSynchronize(ev) == hipSuccess;
