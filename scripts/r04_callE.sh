@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round-4 call E: doorbell GCM job phases (TLSGPU_EVP_DOORBELL_TRACE, gcm_raw.h
+# marks) and the config C time split (tools/cc_diag.py, TLSGPU_CC_DIAG bits).
+# usage: scripts/r04_callE.sh TAG
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:-r04k}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd $R
+B="$R/oracle/_ref/cpubench $R/talos_amd/libtlsgpu.so"
+for spec in "aes-128-gcm seal 1400 1 1" "aes-128-gcm seal 1400 8 1" "aes-128-gcm open 1400 1 1" \
+            "aes-128-gcm seal 16384 1 1"; do
+  set -- $spec
+  TLSGPU_EVP_DOORBELL=16 TLSGPU_EVP_DOORBELL_TRACE=1 timeout -k 10 60 $B $1 $2 $3 $4 $5 2 \
+    >> $O/trace.jsonl 2>> $O/trace.err || exit $?
+  echo "trace $spec: $(tail -2 $O/trace.err | tr '\n' ' ')"
+done
+for d in 0 1 2 3 4 7; do
+  TLSGPU_CC_DIAG=$d timeout -k 10 240 python tools/cc_diag.py >> $O/cc_diag.jsonl 2> $O/cc_diag_$d.err || exit $?
+  tail -1 $O/cc_diag.jsonl
+done
+exit 0

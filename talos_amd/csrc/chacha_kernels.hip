@@ -189,6 +189,11 @@ constexpr int kCcR = kWave / kCcP;           // records covered by one load inst
 constexpr int kCcThreads = 256;
 constexpr uint32_t kCcTile = kWave * kCcStep;  // 8 KiB of rows per wave
 constexpr uint32_t kCcKeys = kWave * 32;       // the lanes' ChaCha keys, 2 KiB per wave
+// Diagnostic bits (TLSGPU_CC_DIAG, BatchArgs::hy_flags of the staged launch;
+// tools/cc_diag.py): drop the gather's global loads, the scatter's global
+// stores, or the ChaCha / Poly1305 work, to split the kernel's time.  The
+// results are then wrong; never set outside that harness.
+constexpr uint32_t kCcDiagNoLoads = 1, kCcDiagNoStores = 2, kCcDiagNoCompute = 4;
 
 // tile offset of piece q (0..7) of row r
 __device__ __forceinline__ uint32_t cc_slot(uint32_t r, uint32_t q) {
@@ -304,7 +309,7 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
       // ds_bpermute outside the branch: an inactive source lane reads as 0
       const uint64_t srck = shfl64((uint64_t)(uintptr_t)src, rr);
       v[k] = make_uint4(0, 0, 0, 0);
-      if (off < snk) {
+      if (off < snk && !(a.hy_flags & kCcDiagNoLoads)) {
         const uint8_t* sp = (const uint8_t*)(uintptr_t)srck + off;
         if (((uintptr_t)sp & 15) == 0) {
           v[k] = gload16(sp);  // full or last piece: an aligned 16 B never crosses a page
@@ -326,7 +331,7 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
     if (s + 1 < steps) gather(base + kCcStep, pf);
     lds_wave_sync();
     // en/decrypt + MAC this lane's row: 2 ChaCha blocks
-    if (base < n) {
+    if (base < n && !(a.hy_flags & kCcDiagNoCompute)) {
 #pragma unroll 1
       for (int h = 0; h < (int)(kCcStep / 64); h++) {
         const uint32_t o64 = base + 64u * h;
@@ -367,7 +372,7 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
       const uint32_t off = base + 16u * (((lane % kCcP) - (rr >> 1)) & 7u);
       const uint32_t snk = __shfl(n, (int)rr);
       const uint64_t dstk = shfl64((uint64_t)(uintptr_t)dst, rr);
-      if (off < snk) {
+      if (off < snk && !(a.hy_flags & kCcDiagNoStores)) {
         uint8_t* dp = (uint8_t*)(uintptr_t)dstk + off;
         const uint4 v = *reinterpret_cast<const uint4*>(tile + 1024u * k + 16u * lane);
         if (off + 16 <= snk && ((uintptr_t)dp & 15) == 0) {
@@ -620,8 +625,14 @@ int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, h
       const char* e = getenv("TLSGPU_CC_LDS_PAD");
       return e ? (unsigned)strtoul(e, nullptr, 10) : 0u;
     }();
-    if (seal) hipLaunchKernelGGL((chacha_tls_kernel<true>), grid, block, pad, s, a);
-    else hipLaunchKernelGGL((chacha_tls_kernel<false>), grid, block, pad, s, a);
+    static const uint32_t diag = [] {
+      const char* e = getenv("TLSGPU_CC_DIAG");
+      return e ? (uint32_t)strtoul(e, nullptr, 0) & 7u : 0u;
+    }();
+    BatchArgs b = a;
+    b.hy_flags = diag;
+    if (seal) hipLaunchKernelGGL((chacha_tls_kernel<true>), grid, block, pad, s, b);
+    else hipLaunchKernelGGL((chacha_tls_kernel<false>), grid, block, pad, s, b);
   }
   if (old) {
     if (seal) hipLaunchKernelGGL((chacha_batch_kernel<true, false, true>), grid, block, 0, s, a);

@@ -1615,6 +1615,7 @@ struct EvpServer {
   uint64_t* trace = nullptr;
   uint64_t* d_trace = nullptr;
   std::atomic<uint64_t> tr_n{0}, tr_load{0}, tr_job{0}, tr_rel{0}, tr_host_ns{0};
+  std::atomic<uint64_t> tr_marks_n{0}, tr_phase[8] = {};  // GCM jobs: loaded -> mark 0 .. 6 -> done
 };
 static EvpServer* g_servers[kMaxEvpDevices] = {};
 static std::mutex g_server_mu;
@@ -1652,6 +1653,14 @@ static void servers_stop_at_exit() {
             "\"us_release\": %.2f, \"us_host_round_trip\": %.2f}}\n",
             (unsigned long long)n, sv->tr_load.load() * 0.01 / n, sv->tr_job.load() * 0.01 / n,
             sv->tr_rel.load() * 0.01 / n, sv->tr_host_ns.load() * 1e-3 / n);
+    const uint64_t m = sv->tr_marks_n.load();
+    if (m) {  // gcm_raw.h TG_JOB_MARK phases
+      static const char* names[8] = {"tables+barrier", "parse", "ctr_setup", "blocks",
+                                     "close+shoup", "reduce+barrier", "ek0_aes", "tag"};
+      fprintf(stderr, "{\"doorbell_gcm_phases_us\": {\"jobs\": %llu", (unsigned long long)m);
+      for (int i = 0; i < 8; i++) fprintf(stderr, ", \"%s\": %.2f", names[i], sv->tr_phase[i].load() * 0.01 / m);
+      fprintf(stderr, "}}\n");
+    }
   }
 }
 
@@ -1683,7 +1692,8 @@ static EvpServer* evp_server(size_t k, tlsgpu_engine* e) {
     return nullptr;
   }
   if (g_doorbell_trace &&
-      (hipHostMalloc((void**)&sv->trace, 32 * sv->nslots, hipHostMallocDefault) != hipSuccess ||
+      (hipHostMalloc((void**)&sv->trace, 8 * kTraceWords * sv->nslots, hipHostMallocDefault) !=
+           hipSuccess ||
        hipHostGetDevicePointer((void**)&sv->d_trace, sv->trace, 0) != hipSuccess))
     sv->trace = sv->d_trace = nullptr;
   *stop = 0;
@@ -1906,12 +1916,19 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
       }
       sv->jobs.fetch_add(1, std::memory_order_relaxed);
       if (sv->trace) {
-        const uint64_t* tr = sv->trace + 4 * (size_t)(slot - sv->slots);
+        const uint64_t* tr = sv->trace + kTraceWords * (size_t)(slot - sv->slots);
         sv->tr_n.fetch_add(1, std::memory_order_relaxed);
         sv->tr_load.fetch_add(tr[1] - tr[0], std::memory_order_relaxed);
-        sv->tr_job.fetch_add(tr[2] - tr[1], std::memory_order_relaxed);
-        sv->tr_rel.fetch_add(tr[3] - tr[2], std::memory_order_relaxed);
+        sv->tr_job.fetch_add(tr[9] - tr[1], std::memory_order_relaxed);
+        sv->tr_rel.fetch_add(tr[10] - tr[9], std::memory_order_relaxed);
         sv->tr_host_ns.fetch_add(mono_ns() - t0, std::memory_order_relaxed);
+        bool all = true;
+        for (int i = 2; i < 9; i++) all = all && tr[i] >= tr[i - 1];
+        if (all && tr[9] >= tr[8]) {
+          sv->tr_marks_n.fetch_add(1, std::memory_order_relaxed);
+          for (int i = 0; i < 8; i++)
+            sv->tr_phase[i].fetch_add(tr[i + 2] - tr[i + 1], std::memory_order_relaxed);
+        }
       }
       const int32_t status = *reinterpret_cast<const int32_t*>(h + o_status);
       if (status < 0) {  // the kernel's zero-fill of max_out_len bytes (evp_aead.c:137-143)

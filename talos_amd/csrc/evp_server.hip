@@ -25,6 +25,18 @@
 // host relaunches (engine.cpp EvpServer) so that a job is only ever posted
 // while an instance that will poll for at least half a lifetime is queued.
 #define TG_VECTOR_SESSION_LOADS 1
+// job phase marks (TLSGPU_EVP_DOORBELL_TRACE): wave 0, lane 0 stamps the
+// realtime clock into LDS; the server copies them to the slot's trace row
+#define TG_JOB_MARK(i)                                                          \
+  do {                                                                          \
+    if (threadIdx.x == 0)                                                       \
+      reinterpret_cast<unsigned long long*>(::tg::s_lds + ::tg::SRV_MARK_OFF)[i] = \
+          __builtin_amdgcn_s_memrealtime();                                     \
+  } while (0)
+#include "gcm_device.h"
+namespace tg {
+constexpr uint32_t SRV_MARK_OFF = PLAN_OFF + 5120;  // 8 job marks (after the ChaCha stage)
+}
 #include "gcm_raw.h"
 #include "chacha_wave.h"
 
@@ -35,7 +47,8 @@ constexpr uint32_t SRV_SEL_OFF = PLAN_OFF + 16 * 16;  // after gcm_raw_job's par
 constexpr uint32_t SRV_SLOT_OFF = PLAN_OFF + 512;     // LDS copy of the picked slot (256 B)
 constexpr uint32_t SRV_STAGE_OFF = PLAN_OFF + 1024;   // ChaCha job: wave 0's 4 KiB stage
 static_assert(SRV_SLOT_OFF + sizeof(DoorbellSlot) <= SRV_STAGE_OFF, "server LDS plan");
-static_assert(SRV_STAGE_OFF + 4096 <= LDS_BYTES, "server LDS plan");
+static_assert(SRV_STAGE_OFF + 4096 <= SRV_MARK_OFF, "server LDS plan");
+static_assert(SRV_MARK_OFF + 64 <= LDS_BYTES, "server LDS plan");
 
 // A ChaCha20-Poly1305 (RFC 7539) job on wave 0 (chacha_wave.h); the session's
 // kind word by a vector load (lane-varying address), as everything else here.
@@ -109,6 +122,7 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
         // by another kernel) are read fresh after this
         __atomic_thread_fence(__ATOMIC_ACQUIRE);
       }
+      if (lane < 7) reinterpret_cast<unsigned long long*>(s_lds + SRV_MARK_OFF)[lane] = 0;
       __builtin_amdgcn_s_waitcnt(0);
       t_loaded = __builtin_amdgcn_s_memrealtime();
     }
@@ -150,11 +164,15 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
     __syncthreads();
     if (threadIdx.x == 0) {
       if (s.trace) {  // diagnostic: ordered before `done` by the release below
-        unsigned long long* tr = s.trace + 4 * (size_t)k;
+        unsigned long long* tr = s.trace + kTraceWords * (size_t)k;
+        const unsigned long long* mk =
+            reinterpret_cast<const unsigned long long*>(s_lds + SRV_MARK_OFF);
         __hip_atomic_store(tr + 0, t_pick, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(tr + 1, t_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(tr + 2, t_job, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(tr + 3, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+        for (int i = 0; i < 7; i++)
+          __hip_atomic_store(tr + 2 + i, mk[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(tr + 9, t_job, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(tr + 10, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       __atomic_thread_fence(__ATOMIC_RELEASE);

@@ -4,6 +4,13 @@
 #pragma once
 #include "gcm_device.h"
 
+// Phase marks of one job (diagnostic): the doorbell server defines this to
+// stamp the realtime clock into LDS from wave 0 (TLSGPU_EVP_DOORBELL_TRACE);
+// elsewhere it compiles to nothing.
+#ifndef TG_JOB_MARK
+#define TG_JOB_MARK(i)
+#endif
+
 namespace tg {
 
 // Raw EVP jobs (EVP_AEAD_CTX_seal/open, any nonce / AAD length; TLS = false)
@@ -49,6 +56,7 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
   }
   if (!tables_loaded) load_session_tables<kThreads>(a.gcm_tables + sid);
   __syncthreads();
+  TG_JOB_MARK(0);
   RecCtx rc;
   if (TLS) {
     // every wave parses (same descriptor): a publicly invalid record returns
@@ -57,6 +65,7 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
   } else {
     parse_raw<SEAL>(*J, S, rc);
   }
+  TG_JOB_MARK(1);
   cu32* rk = as_const(S->rk);
   const uint32_t nb = (rc.n + 15) >> 4;
   const uint32_t nsteps = (nb + kWave - 1) / kWave;
@@ -65,6 +74,7 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
   uint32_t y[4] = {0, 0, 0, 0};
   if (wave < nwork) {
     const CtrConst cc = ctr_setup(rc.j0, rk, laneoff);
+    TG_JOB_MARK(2);
     const RecConsts none = {};
     const uint32_t s0 = wave * spw * kWave;
     uint32_t x[4] = {0, 0, 0, 0};
@@ -76,12 +86,14 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
     uint32_t e;
     if (wave == nwork - 1) {  // the last range: partial tail, lengths block
       gcm_blocks<SEAL, ROUNDS, false>(rc, S, none, cc, x, s0, lane, laneoff, gl);
+      TG_JOB_MARK(3);
       e = gcm_close_chain(rc, x, xb, lane, gl);
     } else {
       RecCtx part = rc;
       const uint32_t e1 = s0 + spw * kWave;  // full blocks only
       part.n = 16u * e1;
       gcm_blocks<SEAL, ROUNDS, false>(part, S, none, cc, x, s0, lane, laneoff, gl);
+      TG_JOB_MARK(3);
       e = nb + 1 - (e1 - kWave + lane);
       while (e > (uint32_t)kPowMax) {  // weight (H^64)^q: q more Horner steps
         uint32_t xk[4];
@@ -92,6 +104,7 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
       be_from_le(x, xb);
     }
     if (e != 0) gl.shoup(xb, e, y);
+    TG_JOB_MARK(4);
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) {
       y[0] ^= __shfl_xor(y[0], m);
@@ -104,6 +117,7 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
   if (lane == 0) part_y[wave] = make_uint4(y[0], y[1], y[2], y[3]);
   __syncthreads();
   if (wave != 0) return;
+  TG_JOB_MARK(5);
   uint32_t t[4] = {0, 0, 0, 0};
   if (lane == 0) {
     for (uint32_t w = 0; w < nwork; w++) {
@@ -113,6 +127,7 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
   }
   uint32_t ek0[4] = {rc.j0[0], rc.j0[1], rc.j0[2], rc.j0[3]};
   aes_block<ROUNDS>(ek0, rk, as_const(S->rk_rot), laneoff);
+  TG_JOB_MARK(6);
   gcm_tag<SEAL>(rc, t, ek0, S, a.status + r, lane);
 }
 

@@ -289,9 +289,11 @@ struct ServerArgs {
   uint32_t nslots;
   const uint32_t* stop;       // pinned word: non-zero = exit now
   unsigned long long lifetime;  // s_memrealtime ticks (100 MHz) a workgroup serves at most
-  unsigned long long* trace;    // null, or pinned [nslots][4]: realtime at pick, slot
-                                // loaded, job done, answer released (TLSGPU_EVP_DOORBELL_TRACE)
+  unsigned long long* trace;    // null, or pinned [nslots][kTraceWords]: realtime at pick,
+                                // slot loaded, GCM job marks 0..6, job done, answer
+                                // released (TLSGPU_EVP_DOORBELL_TRACE)
 };
+constexpr int kTraceWords = 12;
 int launch_evp_server(const ServerArgs& a, int groups, hipStream_t s);
 int launch_session_install_arg(DevSession* sessions, DevGcmTables* tables,
                                const tlsgpu_session_params& p, uint32_t id, hipStream_t s);
