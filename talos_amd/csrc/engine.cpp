@@ -1606,7 +1606,7 @@ struct EvpServer {
   uint32_t* d_stop = nullptr;
   hipStream_t stream = nullptr;
   std::mutex mu;
-  uint64_t deadline_ns = 0;       // post only before this (host clock), else relaunch
+  std::atomic<uint64_t> deadline_ns{0};  // post only before this (host clock), else relaunch
   std::vector<uint32_t> free_slots;
   std::atomic<uint64_t> jobs{0}, launches{0};
   // TLSGPU_EVP_DOORBELL_TRACE=1: per-slot device timestamps (pinned) and their
@@ -1618,6 +1618,9 @@ struct EvpServer {
   std::atomic<uint64_t> tr_marks_n{0}, tr_phase[8] = {};  // GCM jobs: loaded -> mark 0 .. 6 -> done
 };
 static EvpServer* g_servers[kMaxEvpDevices] = {};
+// the servers whose setup succeeded, read without the lock on every call (a
+// process-wide mutex per call cost 16 calling threads more than the call)
+static std::atomic<EvpServer*> g_ready_servers[kMaxEvpDevices] = {};
 static std::mutex g_server_mu;
 static unsigned g_doorbell_groups = [] {
   const char* v = getenv("TLSGPU_EVP_DOORBELL");
@@ -1667,6 +1670,7 @@ static void servers_stop_at_exit() {
 // The server of EVP device k (created on first use when the doorbell is on).
 static EvpServer* evp_server(size_t k, tlsgpu_engine* e) {
   if (!g_doorbell_groups || k >= (size_t)kMaxEvpDevices) return nullptr;
+  if (EvpServer* ready = g_ready_servers[k].load(std::memory_order_acquire)) return ready;
   std::lock_guard<std::mutex> lk(g_server_mu);
   if (g_servers[k]) return g_servers[k]->slots ? g_servers[k] : nullptr;
   auto* sv = new (std::nothrow) EvpServer();
@@ -1702,6 +1706,7 @@ static EvpServer* evp_server(size_t k, tlsgpu_engine* e) {
   sv->slots = h;
   static std::once_flag once;
   std::call_once(once, [] { atexit(servers_stop_at_exit); });
+  g_ready_servers[k].store(sv, std::memory_order_release);
   return sv;
 }
 
@@ -1709,8 +1714,9 @@ static EvpServer* evp_server(size_t k, tlsgpu_engine* e) {
 // lifetime.  Returns false if the launch failed.
 static bool server_ensure(EvpServer* sv) {
   const uint64_t now = mono_ns();
+  if (now < sv->deadline_ns.load(std::memory_order_acquire)) return true;  // no lock per call
   std::lock_guard<std::mutex> lk(sv->mu);
-  if (now < sv->deadline_ns) return true;
+  if (now < sv->deadline_ns.load(std::memory_order_relaxed)) return true;
   if (hipSetDevice(sv->device) != hipSuccess) return false;
   ServerArgs a;
   a.slots = sv->d_slots;
@@ -1719,7 +1725,7 @@ static bool server_ensure(EvpServer* sv) {
   a.lifetime = sv->lifetime_ns / 10;  // 100 MHz realtime ticks
   a.trace = reinterpret_cast<unsigned long long*>(sv->d_trace);
   if (launch_evp_server(a, (int)sv->groups, sv->stream) != 0) return false;
-  sv->deadline_ns = now + sv->lifetime_ns / 2;
+  sv->deadline_ns.store(now + sv->lifetime_ns / 2, std::memory_order_release);
   sv->launches.fetch_add(1, std::memory_order_relaxed);
   return true;
 }
