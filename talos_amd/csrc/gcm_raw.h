@@ -72,6 +72,15 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
   const uint32_t spw = nsteps == 0 ? 1 : (nsteps + kWaves - 1) / kWaves;  // steps per wave
   const uint32_t nwork = nsteps == 0 ? 1 : (nsteps + spw - 1) / spw;
   uint32_t y[4] = {0, 0, 0, 0};
+  uint4* part_y = reinterpret_cast<uint4*>(s_lds + PLAN_OFF);
+  // E_K(J0) for the tag: on the last wave when it has no block range (jobs
+  // below 15 steps), in parallel with the blocks, else on wave 0 at the end
+  const bool ek_early = nwork < (uint32_t)kWaves;
+  if (ek_early && wave == (uint32_t)kWaves - 1) {
+    uint32_t ek[4] = {rc.j0[0], rc.j0[1], rc.j0[2], rc.j0[3]};
+    aes_block<ROUNDS>(ek, rk, as_const(S->rk_rot), laneoff);
+    if (lane == 0) part_y[kWaves - 1] = make_uint4(ek[0], ek[1], ek[2], ek[3]);
+  }
   if (wave < nwork) {
     const CtrConst cc = ctr_setup(rc.j0, rk, laneoff);
     TG_JOB_MARK(2);
@@ -113,8 +122,7 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
       y[3] ^= __shfl_xor(y[3], m);
     }
   }
-  uint4* part_y = reinterpret_cast<uint4*>(s_lds + PLAN_OFF);
-  if (lane == 0) part_y[wave] = make_uint4(y[0], y[1], y[2], y[3]);
+  if (lane == 0 && wave < nwork) part_y[wave] = make_uint4(y[0], y[1], y[2], y[3]);
   __syncthreads();
   if (wave != 0) return;
   TG_JOB_MARK(5);
@@ -125,8 +133,14 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
       t[0] ^= v.x; t[1] ^= v.y; t[2] ^= v.z; t[3] ^= v.w;
     }
   }
-  uint32_t ek0[4] = {rc.j0[0], rc.j0[1], rc.j0[2], rc.j0[3]};
-  aes_block<ROUNDS>(ek0, rk, as_const(S->rk_rot), laneoff);
+  uint32_t ek0[4];
+  if (ek_early) {
+    const uint4 v = part_y[kWaves - 1];
+    ek0[0] = v.x; ek0[1] = v.y; ek0[2] = v.z; ek0[3] = v.w;
+  } else {
+    ek0[0] = rc.j0[0]; ek0[1] = rc.j0[1]; ek0[2] = rc.j0[2]; ek0[3] = rc.j0[3];
+    aes_block<ROUNDS>(ek0, rk, as_const(S->rk_rot), laneoff);
+  }
   TG_JOB_MARK(6);
   gcm_tag<SEAL>(rc, t, ek0, S, a.status + r, lane);
 }
