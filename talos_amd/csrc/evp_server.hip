@@ -21,7 +21,8 @@
 // stores have completed.
 //
 // Termination: every workgroup exits when the stop word is set or after
-// `lifetime` ticks of the 100 MHz realtime counter, whichever is first; the
+// `lifetime` ticks of the 100 MHz realtime counter (checked before every poll,
+// so a busy workgroup leaves on time too), whichever is first; the
 // host relaunches (engine.cpp EvpServer) so that a job is only ever posted
 // while an instance that will poll for at least half a lifetime is queued.
 #define TG_VECTOR_SESSION_LOADS 1
@@ -91,6 +92,10 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
     if (wave == 0) {
       uint32_t pick = kSrvExit;
       for (uint32_t polls = 0;; polls++) {
+        // the lifetime first, busy or not: a workgroup that kept serving past
+        // it would hold the next instance (queued on the same stream) off the
+        // GPU, and with it the slots of workgroups that had already exited
+        if (__builtin_amdgcn_s_memrealtime() - t0 > s.lifetime) break;
         const bool ready = mine < s.nslots && sys_load(&s.slots[mine].post) != served;
         const unsigned long long m = __ballot(ready);
         if (m) {
@@ -98,10 +103,8 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
           t_pick = __builtin_amdgcn_s_memrealtime();
           break;
         }
-        // the stop word and the clock every 16 polls (each poll is a PCIe read)
-        if ((polls & 15) == 15 &&
-            (sys_load(s.stop) != 0 || __builtin_amdgcn_s_memrealtime() - t0 > s.lifetime))
-          break;
+        // the stop word every 16 polls (each poll is a PCIe read)
+        if ((polls & 15) == 15 && sys_load(s.stop) != 0) break;
         __builtin_amdgcn_s_sleep(1);
       }
       if (lane == 0) *sel = pick;
