@@ -16,6 +16,14 @@ for spec in "aes-128-gcm seal 1400 1 1" "aes-128-gcm seal 1400 8 1" "aes-128-gcm
     >> $O/trace.jsonl 2>> $O/trace.err || exit $?
   echo "trace $spec: $(tail -2 $O/trace.err | tr '\n' ' ')"
 done
+if [ -f tools/var/libtlsgpu_as1.so ]; then  # A/B: session reads through global pointers
+  for spec in "aes-128-gcm seal 1400 1 1" "aes-128-gcm seal 1400 8 1"; do
+    set -- $spec
+    TLSGPU_EVP_DOORBELL=16 TLSGPU_EVP_DOORBELL_TRACE=1 timeout -k 10 60 $R/oracle/_ref/cpubench \
+      $R/tools/var/libtlsgpu_as1.so $1 $2 $3 $4 $5 2 >> $O/trace_as1.jsonl 2>> $O/trace_as1.err || exit $?
+    echo "trace as1 $spec: $(tail -2 $O/trace_as1.err | tr '\n' ' ')"
+  done
+fi
 for d in 0 1 2 3 4 7; do
   TLSGPU_CC_DIAG=$d timeout -k 10 240 python tools/cc_diag.py >> $O/cc_diag.jsonl 2> $O/cc_diag_$d.err || exit $?
   tail -1 $O/cc_diag.jsonl
