@@ -73,3 +73,46 @@ def test_evp_doorbell_matches_oracle(threads):
     r = subprocess.run([sys.executable, "-c", _CHILD, ROOT, str(threads)], env=env,
                        capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+_BUSY_CHILD = r"""
+import os, sys, threading, time
+sys.path.insert(0, sys.argv[1])
+import talos_amd as ta
+ta.load_library()
+stop = threading.Event()
+lat = []
+def busy():   # keeps its own server workgroup busy far past the 20 ms lifetime
+    ctx = ta.EvpAead(ta.AES_128_GCM, bytes(16))
+    while not stop.is_set():
+        ok, out, _ = ctx.seal(bytes(12), b"x" * 1400, b"")
+        assert ok == 1
+    ctx.cleanup()
+def late():   # starts after the first instance's lifetime has passed
+    time.sleep(0.1)
+    ctx = ta.EvpAead(ta.AES_256_GCM, bytes(32))
+    for _ in range(20):
+        t = time.perf_counter()
+        ok, out, _ = ctx.seal(bytes(12), b"y" * 100, b"")
+        lat.append(time.perf_counter() - t)
+        assert ok == 1
+    ctx.cleanup()
+a, b = threading.Thread(target=busy), threading.Thread(target=late)
+a.start(); b.start(); b.join(); stop.set(); a.join()
+print("OK", max(lat))
+"""
+
+
+def test_evp_doorbell_busy_workgroup_yields_to_next_instance():
+    """A workgroup whose thread never stops calling must still leave at its
+    lifetime (evp_server.hip checks the clock before every poll): otherwise it
+    holds the next instance, queued behind it on the same stream, off the GPU,
+    and a thread whose workgroup has already exited waits for the busy thread
+    to pause.  The late thread's calls must stay far below the 10 s timeout."""
+    env = dict(os.environ, TLSGPU_EVP_DOORBELL="2", TLSGPU_EVP_DOORBELL_MS="20")
+    env.pop("TLSGPU_EVP_BATCH_US", None)
+    r = subprocess.run([sys.executable, "-c", _BUSY_CHILD, ROOT], env=env,
+                       capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+    worst = float(r.stdout.split()[-1])
+    assert worst < 0.5, f"a call waited {worst:.3f} s behind a busy workgroup"
