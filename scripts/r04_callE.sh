@@ -9,6 +9,10 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
 B="$R/oracle/_ref/cpubench $R/talos_amd/libtlsgpu.so"
+timeout -k 10 300 python -u -m pytest tests/test_evp_doorbell.py tests/test_gpu_parity.py -x -v \
+  --timeout 120 --timeout-method thread -m gpu -k "doorbell or split_jobs or chacha_wave or aeadtests" \
+  > $O/tests.log 2>&1 || { echo "tests rc=$?"; tail -30 $O/tests.log; exit 1; }
+echo "tests: $(tail -1 $O/tests.log)"
 for spec in "aes-128-gcm seal 1400 1 1" "aes-128-gcm seal 1400 8 1" "aes-128-gcm open 1400 1 1" \
             "aes-128-gcm seal 16384 1 1"; do
   set -- $spec
