@@ -59,4 +59,21 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) {
   return __builtin_amdgcn_perm(x, x, 0x00010203u);
 }
 
+// XOR of v over the 64 lanes of the wave (every lane active), returned
+// uniform.  DPP row shifts and row broadcasts instead of a 6-level
+// __shfl_xor butterfly: the butterfly is 6 dependent ds_bpermute round trips
+// through the LDS pipe per word, this is 7 VALU ops (gfx9 DPP: row_shr 1-3
+// into a 4-lane window, row_shr 4 / 8 on the upper banks -> lane 15 of each
+// row holds the row's XOR, row_bcast 15 / 31 -> lane 63 holds the total).
+__device__ __forceinline__ uint32_t wave_xor_total(uint32_t v) {
+  uint32_t a = v ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);
+  a ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);
+  a ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x113, 0xf, 0xf, true);
+  a ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, 0x114, 0xf, 0xe, false);
+  a ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, 0x118, 0xf, 0xc, false);
+  a ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, 0x142, 0xa, 0xf, false);
+  a ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, 0x143, 0xc, 0xf, false);
+  return (uint32_t)__builtin_amdgcn_readlane((int)a, 63);
+}
+
 }  // namespace tg

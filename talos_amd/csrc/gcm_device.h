@@ -648,13 +648,10 @@ template <bool SEAL>
 __device__ __forceinline__ void gcm_tag(const RecCtx& rc, uint32_t (&y)[4], const uint32_t ek0[4],
                                         const DevSession* __restrict__ S, int32_t* status_slot,
                                         uint32_t lane) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
-    y[0] ^= __shfl_xor(y[0], m);
-    y[1] ^= __shfl_xor(y[1], m);
-    y[2] ^= __shfl_xor(y[2], m);
-    y[3] ^= __shfl_xor(y[3], m);
-  }
+  y[0] = wave_xor_total(y[0]);
+  y[1] = wave_xor_total(y[1]);
+  y[2] = wave_xor_total(y[2]);
+  y[3] = wave_xor_total(y[3]);
   // tag = GHASH ^ E_K(J0)  (y is BE words, ek0 LE words)
   uint32_t tag[4] = {bswap32(y[0]) ^ ek0[0], bswap32(y[1]) ^ ek0[1], bswap32(y[2]) ^ ek0[2],
                      bswap32(y[3]) ^ ek0[3]};

@@ -114,13 +114,10 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
     }
     if (e != 0) gl.shoup(xb, e, y);
     TG_JOB_MARK(4);
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-      y[0] ^= __shfl_xor(y[0], m);
-      y[1] ^= __shfl_xor(y[1], m);
-      y[2] ^= __shfl_xor(y[2], m);
-      y[3] ^= __shfl_xor(y[3], m);
-    }
+    y[0] = wave_xor_total(y[0]);
+    y[1] = wave_xor_total(y[1]);
+    y[2] = wave_xor_total(y[2]);
+    y[3] = wave_xor_total(y[3]);
   }
   if (lane == 0 && wave < nwork) part_y[wave] = make_uint4(y[0], y[1], y[2], y[3]);
   __syncthreads();
