@@ -14,7 +14,8 @@
 //     c_0..c_{N-1} of AD || pad16 || CT || pad16 || le64 || le64 (:182-190):
 //     tag = (sum_b c_b r^(N-b) mod 2^130-5) + s.  Lane l takes the blocks
 //     b = l (mod 64) in order, Horner with r^64, and multiplies its sum by
-//     r^(N - b_last); the 64 lane sums are added across the wave.  The powers
+//     r^(N - b_last); the 64 lane sums are added across the wave (DPP row
+//     shifts and broadcasts, p5_wave_sum).  The powers
 //     r^1..r^64 are built by doubling (6 multiplies per lane).
 //
 // The arithmetic is poly1305-donna's 26-bit limbs (chacha_common.h); the
@@ -95,6 +96,31 @@ __device__ __forceinline__ P5 p5_readlane(const P5& a, int src) {
           (uint32_t)__builtin_amdgcn_readlane((int)a.v2, src),
           (uint32_t)__builtin_amdgcn_readlane((int)a.v3, src),
           (uint32_t)__builtin_amdgcn_readlane((int)a.v4, src)};
+}
+
+// One DPP step of a wave reduction on all five limbs (update_dpp with old = 0:
+// lanes without a source, or outside row_mask / bank_mask, add nothing).
+template <int CTRL, int ROWS, int BANKS, bool BOUND>
+__device__ __forceinline__ P5 p5_dpp(const P5& a) {
+  return {(uint32_t)__builtin_amdgcn_update_dpp(0, (int)a.v0, CTRL, ROWS, BANKS, BOUND),
+          (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a.v1, CTRL, ROWS, BANKS, BOUND),
+          (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a.v2, CTRL, ROWS, BANKS, BOUND),
+          (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a.v3, CTRL, ROWS, BANKS, BOUND),
+          (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a.v4, CTRL, ROWS, BANKS, BOUND)};
+}
+
+// Sum of a over the 64 lanes (all active) mod 2^130-5, uniform: the row
+// shift / row broadcast pattern of wave_xor_total (aes_common.h) with a
+// carry pass after each level (4 terms < 2^28.1, then 2 terms < 2^27.1 per
+// limb going in; p5_carry takes < 2^31).
+__device__ __forceinline__ P5 p5_wave_sum(const P5& v) {
+  P5 a = p5_carry(p5_add(p5_add(v, p5_dpp<0x111, 0xf, 0xf, true>(v)),
+                         p5_add(p5_dpp<0x112, 0xf, 0xf, true>(v), p5_dpp<0x113, 0xf, 0xf, true>(v))));
+  a = p5_carry(p5_add(a, p5_dpp<0x114, 0xf, 0xe, false>(a)));
+  a = p5_carry(p5_add(a, p5_dpp<0x118, 0xf, 0xc, false>(a)));
+  a = p5_carry(p5_add(a, p5_dpp<0x142, 0xa, 0xf, false>(a)));
+  a = p5_carry(p5_add(a, p5_dpp<0x143, 0xc, 0xf, false>(a)));
+  return p5_readlane(a, 63);
 }
 
 // Up to 16 bytes at p (nb < 16: zero padded) as little-endian words.
@@ -248,13 +274,7 @@ __device__ void cc_wave_job(const RawJob& j, const DevSession* S, int32_t* statu
   // weight r^(N - b_last) for the lane's last block
   const uint32_t w = lane < N ? N - (lane + 64 * ((N - 1 - lane) >> 6)) : 1u;
   acc = p5_mul(acc, p5_shfl(pw, (int)w - 1));
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const P5 o = {(uint32_t)__shfl_xor((int)acc.v0, off), (uint32_t)__shfl_xor((int)acc.v1, off),
-                  (uint32_t)__shfl_xor((int)acc.v2, off), (uint32_t)__shfl_xor((int)acc.v3, off),
-                  (uint32_t)__shfl_xor((int)acc.v4, off)};
-    acc = p5_carry(p5_add(acc, o));
-  }
+  acc = p5_wave_sum(acc);
   Poly p = {};
   p.h0 = acc.v0; p.h1 = acc.v1; p.h2 = acc.v2; p.h3 = acc.v3; p.h4 = acc.v4;
   p.pad0 = pad[0]; p.pad1 = pad[1]; p.pad2 = pad[2]; p.pad3 = pad[3];

@@ -132,11 +132,32 @@ def wave(r, ad_blocks, data_blocks, len_block):
         w = N - (l + 64 * ((N - 1 - l) >> 6)) if l < N else 1
         assert 1 <= w <= 64
         acc[l] = p5_mul(acc[l], pw[w - 1])
-    off = 32
-    while off:
-        acc = [p5_carry(p5_add(acc[l], acc[l ^ off])) for l in range(64)]
-        off //= 2
-    return value(acc[0])
+    return value(wave_sum(acc))
+
+
+def wave_sum(v):
+    """p5_wave_sum: the DPP row-shift / row-broadcast reduction, lane 63."""
+    zero = [0] * 5
+
+    def shr(a, n, banks):  # row_shr:n on the lanes of the enabled banks (4 lanes each)
+        return [a[l - n] if (l % 16) >= n and ((banks >> ((l % 16) // 4)) & 1) else zero
+                for l in range(64)]
+
+    def bcast(a, src, rows):  # row_bcast: lane src's value into the enabled rows
+        return [a[src if src == 31 else (l // 16) * 16 - 1] if (rows >> (l // 16)) & 1 else zero
+                for l in range(64)]
+
+    s1, s2, s3 = shr(v, 1, 0xF), shr(v, 2, 0xF), shr(v, 3, 0xF)
+    a = [p5_carry(p5_add(p5_add(v[l], s1[l]), p5_add(s2[l], s3[l]))) for l in range(64)]
+    t = shr(a, 4, 0xE)
+    a = [p5_carry(p5_add(a[l], t[l])) for l in range(64)]
+    t = shr(a, 8, 0xC)
+    a = [p5_carry(p5_add(a[l], t[l])) for l in range(64)]
+    t = bcast(a, 15, 0xA)
+    a = [p5_carry(p5_add(a[l], t[l])) for l in range(64)]
+    t = bcast(a, 31, 0xC)
+    a = [p5_carry(p5_add(a[l], t[l])) for l in range(64)]
+    return a[63]
 
 
 CASES = [(0, 0), (13, 0), (0, 1), (13, 1400), (13, 4031), (13, 4032), (13, 4033), (0, 4096),
