@@ -169,7 +169,7 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
     a.n_sessions = __builtin_amdgcn_readfirstlane(c->n_sessions);
     const uint32_t key = __builtin_amdgcn_readfirstlane(c->key_id);
     const uint32_t sid = __builtin_amdgcn_readfirstlane(c->job.session);
-    if ((op >> 8) != 20 && sid < a.n_sessions && key != 0)  // GCM: the LDS copy
+    if (((op >> 8) == 10 || (op >> 8) == 14) && sid < a.n_sessions && key != 0)  // GCM: LDS copy
       a.sessions = reinterpret_cast<const DevSession*>(s_lds + SRV_SESS_OFF) - sid;
     const bool hit = key != 0 && key == cached_key;
     const uint32_t prev_key = cached_key;  // a ChaCha job leaves the GCM tables alone
