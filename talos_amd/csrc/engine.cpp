@@ -1616,6 +1616,7 @@ struct EvpServer {
   uint64_t* d_trace = nullptr;
   std::atomic<uint64_t> tr_n{0}, tr_load{0}, tr_job{0}, tr_rel{0}, tr_host_ns{0};
   std::atomic<uint64_t> tr_marks_n{0}, tr_phase[8] = {};  // GCM jobs: loaded -> mark 0 .. 6 -> done
+  std::atomic<uint64_t> tr_last[4] = {};  // since loaded: wave 0 blocks / shoup, last wave blocks / shoup
 };
 static EvpServer* g_servers[kMaxEvpDevices] = {};
 // the servers whose setup succeeded, read without the lock on every call (a
@@ -1662,7 +1663,10 @@ static void servers_stop_at_exit() {
                                      "close+shoup", "reduce+barrier", "ek0_aes", "tag"};
       fprintf(stderr, "{\"doorbell_gcm_phases_us\": {\"jobs\": %llu", (unsigned long long)m);
       for (int i = 0; i < 8; i++) fprintf(stderr, ", \"%s\": %.2f", names[i], sv->tr_phase[i].load() * 0.01 / m);
-      fprintf(stderr, "}}\n");
+      fprintf(stderr, ", \"since_loaded_us\": {\"wave0_blocks\": %.2f, \"wave0_shoup\": %.2f, "
+                      "\"last_wave_blocks\": %.2f, \"last_wave_shoup\": %.2f}}}\n",
+              sv->tr_last[0].load() * 0.01 / m, sv->tr_last[1].load() * 0.01 / m,
+              sv->tr_last[2].load() * 0.01 / m, sv->tr_last[3].load() * 0.01 / m);
     }
   }
 }
@@ -1886,11 +1890,11 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
     EvpServer* sv = evp_server(st->evp_dev, e);
     uint32_t* seq = nullptr;
     DoorbellSlot* slot = sv ? thread_slot(sv, st->evp_dev, &seq) : nullptr;
-    if (slot) {
-      if (st->install_pending.load(std::memory_order_acquire)) {  // the key install
-        if (hipEventSynchronize(st->installed) != hipSuccess) return -1;
-        st->install_pending.store(false, std::memory_order_release);
-      }
+    // a context's first call, its key install still queued, takes the
+    // launched path below (ordered after the install on the device, no host
+    // wait): waiting for the install here halved connection churn at 16
+    // threads (profiles/r04l_doorbell_bench.jsonl: 17.7 vs 43.7 K/s)
+    if (slot && !st->install_pending.load(std::memory_order_acquire)) {
       // the job travels in the slot (one wave load brings it to the server),
       // nonce and AAD inline when they fit
       const bool inl = nonce_len + ad_len <= kDoorbellInline;
@@ -1934,6 +1938,11 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
           sv->tr_marks_n.fetch_add(1, std::memory_order_relaxed);
           for (int i = 0; i < 8; i++)
             sv->tr_phase[i].fetch_add(tr[i + 2] - tr[i + 1], std::memory_order_relaxed);
+          const uint64_t lw_b = tr[11] >= tr[1] ? tr[11] - tr[1] : 0, lw_s = tr[12] >= tr[1] ? tr[12] - tr[1] : 0;
+          sv->tr_last[0].fetch_add(tr[5] - tr[1], std::memory_order_relaxed);
+          sv->tr_last[1].fetch_add(tr[6] - tr[1], std::memory_order_relaxed);
+          sv->tr_last[2].fetch_add(lw_b, std::memory_order_relaxed);
+          sv->tr_last[3].fetch_add(lw_s, std::memory_order_relaxed);
         }
       }
       const int32_t status = *reinterpret_cast<const int32_t*>(h + o_status);

@@ -28,15 +28,16 @@
 #define TG_VECTOR_SESSION_LOADS 1
 // job phase marks (TLSGPU_EVP_DOORBELL_TRACE): wave 0, lane 0 stamps the
 // realtime clock into LDS; the server copies them to the slot's trace row
-#define TG_JOB_MARK(i)                                                          \
+#define TG_JOB_MARK_AT(i, t)                                                    \
   do {                                                                          \
-    if (threadIdx.x == 0)                                                       \
+    if (threadIdx.x == (t))                                                     \
       reinterpret_cast<unsigned long long*>(::tg::s_lds + ::tg::SRV_MARK_OFF)[i] = \
           __builtin_amdgcn_s_memrealtime();                                     \
   } while (0)
+#define TG_JOB_MARK(i) TG_JOB_MARK_AT(i, 0)
 #include "gcm_device.h"
 namespace tg {
-constexpr uint32_t SRV_MARK_OFF = PLAN_OFF + 5120;  // 8 job marks (after the ChaCha stage)
+constexpr uint32_t SRV_MARK_OFF = PLAN_OFF + 5120;  // 9 job marks (after the ChaCha stage)
 }
 #include "gcm_raw.h"
 #include "chacha_wave.h"
@@ -49,11 +50,11 @@ constexpr uint32_t SRV_SLOT_OFF = PLAN_OFF + 512;     // LDS copy of the picked 
 constexpr uint32_t SRV_STAGE_OFF = PLAN_OFF + 1024;   // ChaCha job: wave 0's 4 KiB stage
 static_assert(SRV_SLOT_OFF + sizeof(DoorbellSlot) <= SRV_STAGE_OFF, "server LDS plan");
 static_assert(SRV_STAGE_OFF + 4096 <= SRV_MARK_OFF, "server LDS plan");
-static_assert(SRV_MARK_OFF + 64 <= LDS_BYTES, "server LDS plan");
+static_assert(SRV_MARK_OFF + 80 <= LDS_BYTES, "server LDS plan");
 // the GCM job's DevSession, copied into LDS once per installed key: the job's
 // session reads (kind, rounds, tag_len, round keys) are then LDS reads, not
 // one dependent HBM round trip each (round-4 trace: parse + setup ≈ 2.3 µs)
-constexpr uint32_t SRV_SESS_OFF = SRV_MARK_OFF + 64;
+constexpr uint32_t SRV_SESS_OFF = SRV_MARK_OFF + 128;
 static_assert(SRV_SESS_OFF % 16 == 0 && SRV_SESS_OFF + sizeof(DevSession) <= LDS_BYTES,
               "server LDS plan");
 // slot words the copy needs (DoorbellSlot layout, tlsgpu_internal.h)
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
           sess_key = key;
         }
       }
-      if (lane < 7) reinterpret_cast<unsigned long long*>(s_lds + SRV_MARK_OFF)[lane] = 0;
+      if (lane < 9) reinterpret_cast<unsigned long long*>(s_lds + SRV_MARK_OFF)[lane] = 0;
       __builtin_amdgcn_s_waitcnt(0);
       t_loaded = __builtin_amdgcn_s_memrealtime();
     }
@@ -204,6 +205,8 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
         __hip_atomic_store(tr + 9, t_job, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(tr + 10, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(tr + 11, mk[7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(tr + 12, mk[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       __atomic_thread_fence(__ATOMIC_RELEASE);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

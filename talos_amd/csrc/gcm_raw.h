@@ -9,6 +9,7 @@
 // elsewhere it compiles to nothing.
 #ifndef TG_JOB_MARK
 #define TG_JOB_MARK(i)
+#define TG_JOB_MARK_AT(i, t)
 #endif
 
 namespace tg {
@@ -96,6 +97,7 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
     if (wave == nwork - 1) {  // the last range: partial tail, lengths block
       gcm_blocks<SEAL, ROUNDS, false>(rc, S, none, cc, x, s0, lane, laneoff, gl);
       TG_JOB_MARK(3);
+      TG_JOB_MARK_AT(7, 64 * (nwork - 1));
       e = gcm_close_chain(rc, x, xb, lane, gl);
     } else {
       RecCtx part = rc;
@@ -114,6 +116,7 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
     }
     if (e != 0) gl.shoup(xb, e, y);
     TG_JOB_MARK(4);
+    TG_JOB_MARK_AT(8, 64 * (nwork - 1));
     y[0] = wave_xor_total(y[0]);
     y[1] = wave_xor_total(y[1]);
     y[2] = wave_xor_total(y[2]);

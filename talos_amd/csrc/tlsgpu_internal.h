@@ -293,7 +293,7 @@ struct ServerArgs {
                                 // slot loaded, GCM job marks 0..6, job done, answer
                                 // released (TLSGPU_EVP_DOORBELL_TRACE)
 };
-constexpr int kTraceWords = 12;
+constexpr int kTraceWords = 16;  // + the last working wave's marks 7, 8 at [11], [12]
 int launch_evp_server(const ServerArgs& a, int groups, hipStream_t s);
 int launch_session_install_arg(DevSession* sessions, DevGcmTables* tables,
                                const tlsgpu_session_params& p, uint32_t id, hipStream_t s);
