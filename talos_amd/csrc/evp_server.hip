@@ -38,7 +38,27 @@
 #include "gcm_device.h"
 namespace tg {
 constexpr uint32_t SRV_MARK_OFF = PLAN_OFF + 5120;  // 9 job marks (after the ChaCha stage)
+constexpr uint32_t SRV_STAGE_OFF = PLAN_OFF + 1024;  // 4 KiB: a ChaCha job's stage, a GCM job's input
+constexpr uint32_t kSrvStageMax = 4096;
+constexpr uint32_t kSrvStageWave = 12;  // waves 12..15 copy (idle: a 4 KiB job has <= 4 ranges)
 }
+#define TG_JOB_STAGE 1
+namespace tg {
+__device__ __forceinline__ bool tg_stage_ok(const RawJob* J) {
+  const uint32_t n = J->in_len;
+  return n != 0 && n <= kSrvStageMax && (J->in & 15) == 0;
+}
+// waves 12..15: 256 lanes x 16 B; the staging buffer rounds the input up to
+// 16 B (engine.cpp gpu_call_impl), so a whole 16 B read stays inside it
+__device__ __forceinline__ void tg_stage_issue(const RawJob* J, uint32_t wave, uint32_t lane) {
+  if (wave < kSrvStageWave) return;
+  const uint32_t off = 16 * ((wave - kSrvStageWave) * kWave + lane);
+  if (off < J->in_len)
+    *reinterpret_cast<uint4*>(s_lds + SRV_STAGE_OFF + off) =
+        *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(J->in) + off);
+}
+__device__ __forceinline__ const uint8_t* tg_stage_src() { return s_lds + SRV_STAGE_OFF; }
+}  // namespace tg
 #include "gcm_raw.h"
 #include "chacha_wave.h"
 
@@ -47,7 +67,6 @@ namespace tg {
 constexpr uint32_t kSrvExit = 0xFFFFFFFFu;
 constexpr uint32_t SRV_SEL_OFF = PLAN_OFF + 16 * 16;  // after gcm_raw_job's part_y words
 constexpr uint32_t SRV_SLOT_OFF = PLAN_OFF + 512;     // LDS copy of the picked slot (256 B)
-constexpr uint32_t SRV_STAGE_OFF = PLAN_OFF + 1024;   // ChaCha job: wave 0's 4 KiB stage
 static_assert(SRV_SLOT_OFF + sizeof(DoorbellSlot) <= SRV_STAGE_OFF, "server LDS plan");
 static_assert(SRV_STAGE_OFF + 4096 <= SRV_MARK_OFF, "server LDS plan");
 static_assert(SRV_MARK_OFF + 80 <= LDS_BYTES, "server LDS plan");

@@ -12,6 +12,16 @@
 #define TG_JOB_MARK_AT(i, t)
 #endif
 
+// Input staging (the doorbell server): idle waves copy a short job's input
+// into LDS while the first waves parse, so the block loop reads LDS instead
+// of pinned host memory across PCIe.  Elsewhere: nothing.
+#ifndef TG_JOB_STAGE
+#define TG_JOB_STAGE 0
+__device__ __forceinline__ bool tg_stage_ok(const void*) { return false; }
+__device__ __forceinline__ void tg_stage_issue(const void*, uint32_t, uint32_t) {}
+__device__ __forceinline__ const uint8_t* tg_stage_src() { return nullptr; }
+#endif
+
 namespace tg {
 
 // Raw EVP jobs (EVP_AEAD_CTX_seal/open, any nonce / AAD length; TLS = false)
@@ -58,6 +68,8 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
   if (!tables_loaded) load_session_tables<kThreads>(a.gcm_tables + sid);
   __syncthreads();
   TG_JOB_MARK(0);
+  const bool staged = !TLS && TG_JOB_STAGE && tg_stage_ok(J);
+  if (staged) tg_stage_issue(J, wave, lane);
   RecCtx rc;
   if (TLS) {
     // every wave parses (same descriptor): a publicly invalid record returns
@@ -67,6 +79,10 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
     parse_raw<SEAL>(*J, S, rc);
   }
   TG_JOB_MARK(1);
+  if (staged) {  // the staging waves' LDS writes, before any block is read
+    __syncthreads();
+    rc.src = tg_stage_src();  // the tag (open) was read from the job's own input by parse_raw
+  }
   cu32* rk = as_const(S->rk);
   const uint32_t nb = (rc.n + 15) >> 4;
   const uint32_t nsteps = (nb + kWave - 1) / kWave;
