@@ -524,11 +524,23 @@ __device__ __forceinline__ void mul_shoup2(const uint32_t A[4], uint32_t ea, uin
 // non-96-bit IVs and RAW-mode AAD).  x is big-endian words.  When final_mul
 // is false the last block is only XORed in (no trailing multiply).
 __device__ void ghash_serial(uint32_t x[4], const uint8_t* p, uint64_t len, bool final_mul) {
+  const bool al4 = ((uintptr_t)p & 3) == 0;
   for (uint64_t off = 0; off < len; off += 16) {
     uint32_t b[4] = {0, 0, 0, 0};
+    if (al4) {  // whole words (a 4-B aligned word cannot cross a page), tail bytes masked
 #pragma unroll
-    for (int k = 0; k < 16; k++)
-      if (off + k < len) b[k >> 2] |= (uint32_t)p[off + k] << (24 - 8 * (k & 3));
+      for (int k = 0; k < 4; k++) {
+        const int64_t nb = (int64_t)(len - off) - 4 * k;
+        if (nb > 0) {
+          const uint32_t w = reinterpret_cast<const uint32_t*>(p + off)[k];
+          b[k] = bswap32(nb >= 4 ? w : (w & ((1u << (8 * nb)) - 1u)));
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        if (off + k < len) b[k >> 2] |= (uint32_t)p[off + k] << (24 - 8 * (k & 3));
+    }
     x[0] ^= b[0]; x[1] ^= b[1]; x[2] ^= b[2]; x[3] ^= b[3];
     if (off + 16 < len || final_mul) {
       uint32_t z[4];
@@ -545,6 +557,7 @@ __device__ __forceinline__ void be_from_le(const uint32_t* l, uint32_t* b) {
 // ---------------------------------------------------------------------------
 // Memory helpers (records are byte-aligned in general).
 __device__ __forceinline__ uint32_t load_u32_bytes(const uint8_t* p) {
+  if (((uintptr_t)p & 3) == 0) return *reinterpret_cast<const uint32_t*>(p);  // one load, not four
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
@@ -556,6 +569,16 @@ __device__ __forceinline__ void load_block(const uint8_t* p, uint32_t nbytes, bo
     v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
   } else if (nbytes == 16) {
     load16_any(p, v);
+  } else if (nbytes != 0 && ((uintptr_t)p & 15) == 0) {
+    // a partial last block at a 16-B aligned address: one 16-B load (it cannot
+    // cross a page) with the bytes past the end masked, not up to 15 byte loads
+    const uint4 t = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int32_t b = (int32_t)nbytes - 4 * k;
+      v[k] = w[k] & (b >= 4 ? 0xFFFFFFFFu : (b <= 0 ? 0u : ((1u << (8 * b)) - 1u)));
+    }
   } else {
     v[0] = v[1] = v[2] = v[3] = 0;
 #pragma unroll
