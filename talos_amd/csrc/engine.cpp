@@ -1609,6 +1609,12 @@ struct EvpServer {
   std::atomic<uint64_t> deadline_ns{0};  // post only before this (host clock), else relaunch
   std::vector<uint32_t> free_slots;
   std::atomic<uint64_t> jobs{0}, launches{0};
+  // threads holding a slot, and 1 + the highest slot ever handed out: an
+  // instance is launched with as many workgroups as there are calling
+  // threads (at most `groups`), and enough that its 64 polling lanes per
+  // workgroup cover every slot in use
+  std::atomic<uint32_t> active{0}, hi_slot{0};
+  std::atomic<uint32_t> covered{0};  // slots the last launched instance polls (64 per workgroup)
   // TLSGPU_EVP_DOORBELL_TRACE=1: per-slot device timestamps (pinned) and their
   // sums, printed at exit: pick -> slot loaded -> job done -> released (ticks
   // of 10 ns), and the caller's post -> done-seen wall time (ns)
@@ -1728,7 +1734,10 @@ static bool server_ensure(EvpServer* sv) {
   a.stop = sv->d_stop;
   a.lifetime = sv->lifetime_ns / 10;  // 100 MHz realtime ticks
   a.trace = reinterpret_cast<unsigned long long*>(sv->d_trace);
-  if (launch_evp_server(a, (int)sv->groups, sv->stream) != 0) return false;
+  const uint32_t cover = (sv->hi_slot.load(std::memory_order_acquire) + kWave - 1) / kWave;
+  const uint32_t g = std::min(sv->groups, std::max({1u, sv->active.load(std::memory_order_acquire), cover}));
+  if (launch_evp_server(a, (int)g, sv->stream) != 0) return false;
+  sv->covered.store(g * kWave, std::memory_order_release);
   sv->deadline_ns.store(now + sv->lifetime_ns / 2, std::memory_order_release);
   sv->launches.fetch_add(1, std::memory_order_relaxed);
   return true;
@@ -1747,6 +1756,7 @@ struct ThreadSlots {
       if (slot[k] >= 0 && g_servers[k]) {
         std::lock_guard<std::mutex> lk(g_servers[k]->mu);
         g_servers[k]->free_slots.push_back((uint32_t)slot[k]);
+        g_servers[k]->active.fetch_sub(1, std::memory_order_release);
       }
   }
 };
@@ -1761,6 +1771,13 @@ static DoorbellSlot* thread_slot(EvpServer* sv, size_t k, uint32_t** seq) {
     } else {
       s = (int)sv->free_slots.back();
       sv->free_slots.pop_back();
+      sv->active.fetch_add(1, std::memory_order_release);
+      if ((uint32_t)s + 1 > sv->hi_slot.load(std::memory_order_relaxed))
+        sv->hi_slot.store((uint32_t)s + 1, std::memory_order_release);
+      // a slot the queued instance does not poll: relaunch wider before the
+      // first post (the caller's server_ensure follows)
+      if ((uint32_t)s >= sv->covered.load(std::memory_order_acquire))
+        sv->deadline_ns.store(0, std::memory_order_release);
       // continue the slot's numbering (an earlier thread may have used it)
       t_slots.seq[k] = __atomic_load_n(&sv->slots[s].done, __ATOMIC_ACQUIRE);
     }
