@@ -426,19 +426,20 @@ int tlsgpu_evp_batch_stats(uint64_t *batches, uint64_t *jobs);
  * not), process-wide since load.  Lets a caller that interposed the library
  * under an unchanged libssl check that every TLS record went through it. */
 int tlsgpu_evp_call_stats(uint64_t *seal_calls, uint64_t *open_calls);
-/* Doorbell server for per-call AES-GCM EVP calls (round 4).  groups > 0 keeps
- * that many 1024-thread server workgroups (one CU each) resident on every EVP
- * device while calls arrive: a calling thread posts its job (the same zero-copy
- * RawJob the launched path builds) in a slot of pinned host memory and spins
- * on the answer, so a synchronous EVP_AEAD_CTX_seal / _open on an AES-GCM
- * context costs one PCIe round trip instead of a kernel launch + stream sync.
- * Each server instance exits after lifetime_ms (0 = 5 ms) and is relaunched
- * by the next call, so an idle process leaves nothing running.  Threads beyond
- * 8 * groups per device, ChaCha20-Poly1305 contexts and pooled (queued)
- * contexts use the other paths.  Same as TLSGPU_EVP_DOORBELL=<groups>
- * (TLSGPU_EVP_DOORBELL_MS=<lifetime>) at load; must be called before the
- * first EVP call.  tlsgpu_evp_doorbell_stats: jobs served and instances
- * launched so far. */
+/* Doorbell server for per-call EVP calls (round 4).  groups > 0 keeps up to
+ * that many 1024-thread server workgroups (one CU each, one per calling thread)
+ * resident on every EVP device while calls arrive: a calling thread posts its
+ * job (the same zero-copy RawJob the launched path builds) in a slot of pinned
+ * host memory and spins on the answer, so a synchronous EVP_AEAD_CTX_seal /
+ * _open on an AES-GCM or RFC 7539 ChaCha20-Poly1305 context costs one PCIe
+ * round trip instead of a kernel launch + stream sync.  Each server instance
+ * exits after lifetime_ms (0 = 5 ms) and is relaunched by the next call, so an
+ * idle process leaves nothing running.  Threads beyond 8 * groups per device,
+ * a context's first call (its key install still queued), draft-suite ChaCha
+ * contexts and pooled (queued) contexts use the other paths.  Same as
+ * TLSGPU_EVP_DOORBELL=<groups> (TLSGPU_EVP_DOORBELL_MS=<lifetime>) at load;
+ * must be called before the first EVP call.  tlsgpu_evp_doorbell_stats: jobs
+ * served and instances launched so far. */
 int tlsgpu_evp_set_doorbell(unsigned groups, unsigned lifetime_ms);
 int tlsgpu_evp_doorbell_stats(uint64_t *jobs, uint64_t *launches);
 /* Test support.  tlsgpu_evp_context_slot: the session table and slot that hold
