@@ -1607,6 +1607,8 @@ struct EvpServer {
   hipStream_t stream = nullptr;
   std::mutex mu;
   std::atomic<uint64_t> deadline_ns{0};  // post only before this (host clock), else relaunch
+  uint64_t end_ns = 0;                   // when the last queued instance stops polling, at the
+                                         // earliest (host clock; under mu)
   std::vector<uint32_t> free_slots;
   std::atomic<uint64_t> jobs{0}, launches{0};
   // threads holding a slot, and 1 + the highest slot ever handed out: an
@@ -1738,7 +1740,13 @@ static bool server_ensure(EvpServer* sv) {
   const uint32_t g = std::min(sv->groups, std::max({1u, sv->active.load(std::memory_order_acquire), cover}));
   if (launch_evp_server(a, (int)g, sv->stream) != 0) return false;
   sv->covered.store(g * kWave, std::memory_order_release);
-  sv->deadline_ns.store(now + sv->lifetime_ns / 2, std::memory_order_release);
+  // instances on one stream run one after another: this one starts when the
+  // one queued before it ends (never before now) and polls for a lifetime
+  // from then; post to it until half of that is left.  (Counting from the
+  // launch instead queued a new instance every half lifetime behind ones
+  // that each ran a whole lifetime: the queue grew without bound.)
+  sv->end_ns = std::max(now, sv->end_ns) + sv->lifetime_ns;
+  sv->deadline_ns.store(sv->end_ns - sv->lifetime_ns / 2, std::memory_order_release);
   sv->launches.fetch_add(1, std::memory_order_relaxed);
   return true;
 }
