@@ -9,7 +9,8 @@ cycling init / seal / open / cleanup so session slots are re-keyed while the
 server runs, across server relaunches (short lifetime), and the server must
 stop by itself when the calls stop.  ChaCha jobs run on the server's wave 0
 (chacha_wave.h) between GCM jobs, whose LDS table cache they must leave
-intact."""
+intact; draft-suite ChaCha contexts take the launched path in the same
+threads."""
 import os
 import subprocess
 import sys
@@ -26,7 +27,7 @@ sys.path.insert(0, sys.argv[1]); sys.path.insert(0, os.path.join(sys.argv[1], "o
 import talos_amd as ta, pyoracle as po
 ta.load_library()
 orc = po.Oracle()
-kinds = [po.AES_128_GCM, po.AES_256_GCM, po.CHACHA20_POLY1305]
+kinds = [po.AES_128_GCM, po.AES_256_GCM, po.CHACHA20_POLY1305, po.CHACHA20_POLY1305_OLD]
 errors = []
 def worker(t):
     rnd = random.Random(4100 + t)
@@ -34,11 +35,13 @@ def worker(t):
         for i in range(30):
             kind = kinds[(t + i) % len(kinds)]
             key = bytes(rnd.randrange(256) for _ in range(po.KEY_LEN[kind]))
-            tag_len = rnd.choice([16, 16, 12]) if kind != po.CHACHA20_POLY1305 else 16
+            chacha = kind in (po.CHACHA20_POLY1305, po.CHACHA20_POLY1305_OLD)
+            tag_len = rnd.choice([16, 16, 12]) if not chacha else 16
             ctx, octx = ta.EvpAead(kind, key, tag_len), orc.aead(kind, key, tag_len)
             assert ctx.ok == 1
             for _ in range(3):
-                nlen = 12 if kind == po.CHACHA20_POLY1305 else rnd.choice([12, 12, 1, 8, 16, 60])
+                nlen = (12 if kind == po.CHACHA20_POLY1305 else 8 if kind == po.CHACHA20_POLY1305_OLD
+                        else rnd.choice([12, 12, 1, 8, 16, 60]))
                 nonce = bytes(rnd.randrange(256) for _ in range(nlen))
                 pt = bytes(rnd.randrange(256) for _ in range(rnd.choice([0, 1, 15, 100, 1400, 4096, 16384, 40000])))
                 ad = bytes(rnd.randrange(256) for _ in range(rnd.choice([0, 13, 100])))
