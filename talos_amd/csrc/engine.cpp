@@ -1649,6 +1649,14 @@ static uint64_t mono_ns() {
 
 // stop every server at exit: one host store each (no HIP call: the runtime
 // may already be going away); an instance exits within one poll
+// A waiting caller spins this long before it starts yielding the core
+// (TLSGPU_EVP_DOORBELL_YIELD_US, default 100): with more calling threads than
+// cores, spinners keep the threads that would post from running.
+static const uint64_t g_doorbell_yield_ns = [] {
+  const char* v = getenv("TLSGPU_EVP_DOORBELL_YIELD_US");
+  return (v && *v ? (uint64_t)strtoull(v, nullptr, 10) : 100ull) * 1000ull;
+}();
+
 static const bool g_doorbell_trace = [] {
   const char* v = getenv("TLSGPU_EVP_DOORBELL_TRACE");
   return v && *v && *v != '0';
@@ -1943,10 +1951,10 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
       const uint64_t t0 = mono_ns();
       for (uint64_t spins = 1; __atomic_load_n(&slot->done, __ATOMIC_ACQUIRE) != n; spins++) {
         __builtin_ia32_pause();
-        if ((spins & 1023) == 0) {
+        if ((spins & 127) == 0) {
           const uint64_t waited = mono_ns() - t0;
           if (waited > 10000000000ull) return -1;  // 10 s: the device is gone
-          if (waited > 100000) sched_yield();      // a long job: let others run
+          if (waited > g_doorbell_yield_ns) sched_yield();  // let other callers post
         }
       }
       sv->jobs.fetch_add(1, std::memory_order_relaxed);
