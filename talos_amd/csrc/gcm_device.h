@@ -1248,6 +1248,28 @@ __device__ void load_session_tables(const DevGcmTables* __restrict__ tab) {
   for (uint32_t jj = threadIdx.x >> 6; jj < 16; jj += NT / kWave) {
     const uint32_t j = __builtin_amdgcn_readfirstlane(jj);  // byte position
     uint32_t lo[4] = {0, 0, 0, 0};
+#ifdef TG_VECTOR_SESSION_LOADS
+    // the persistent server: the wave's 8 basis entries in one lane-parallel
+    // load (lane k < 8: x^(8j + 7 - k)), then lane reads — one memory round
+    // trip instead of eight serialised uniform loads (round-4 trace: a key
+    // change cost 4.3 µs)
+    uint4 own = make_uint4(0, 0, 0, 0);
+    if (bl < 8) own = *reinterpret_cast<const uint4*>(tab->basis[8 * j + 7 - bl]);
+    struct LaneWord {
+      uint4 v;
+      __device__ __forceinline__ uint32_t operator()(int k, int c) const {
+        const uint32_t w = c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
+        return (uint32_t)__builtin_amdgcn_readlane((int)w, k);
+      }
+    } bw{own};
+#pragma unroll
+    for (int k = 0; k < 6; k++) {   // bit k of the byte <-> x^(8j + 7 - k)
+      uint32_t msk = 0u - ((bl >> k) & 1u);
+      lo[0] ^= bw(k, 0) & msk; lo[1] ^= bw(k, 1) & msk; lo[2] ^= bw(k, 2) & msk; lo[3] ^= bw(k, 3) & msk;
+    }
+    const uint32_t b6[4] = {bw(6, 0), bw(6, 1), bw(6, 2), bw(6, 3)};  // x^(8j + 1)
+    const uint32_t b7[4] = {bw(7, 0), bw(7, 1), bw(7, 2), bw(7, 3)};  // x^(8j)
+#else
 #pragma unroll
     for (int k = 0; k < 6; k++) {   // bit k of the byte <-> x^(8j + 7 - k)
       uint32_t msk = 0u - ((bl >> k) & 1u);
@@ -1256,6 +1278,7 @@ __device__ void load_session_tables(const DevGcmTables* __restrict__ tab) {
     }
     cu32* b6 = as_const(tab->basis[8 * j + 1]);
     cu32* b7 = as_const(tab->basis[8 * j + 0]);
+#endif
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       uint32_t m6 = (q & 1) ? 0xFFFFFFFFu : 0u, m7 = (q & 2) ? 0xFFFFFFFFu : 0u;
