@@ -1740,14 +1740,18 @@ static bool server_ensure(EvpServer* sv) {
   if (hipSetDevice(sv->device) != hipSuccess) return false;
   ServerArgs a;
   a.slots = sv->d_slots;
-  a.nslots = sv->nslots;
+  // poll the slots handed out so far, rounded up to 16 (so that a burst of new
+  // threads forces few relaunches): every poll is a PCIe read, and at 64
+  // threads polling all 8 G slots was 8x the reads the calls needed
+  const uint32_t hi = std::max(1u, sv->hi_slot.load(std::memory_order_acquire));
+  a.nslots = std::min(sv->nslots, (hi + 15) & ~15u);
   a.stop = sv->d_stop;
   a.lifetime = sv->lifetime_ns / 10;  // 100 MHz realtime ticks
   a.trace = reinterpret_cast<unsigned long long*>(sv->d_trace);
-  const uint32_t cover = (sv->hi_slot.load(std::memory_order_acquire) + kWave - 1) / kWave;
+  const uint32_t cover = (hi + kWave - 1) / kWave;
   const uint32_t g = std::min(sv->groups, std::max({1u, sv->active.load(std::memory_order_acquire), cover}));
   if (launch_evp_server(a, (int)g, sv->stream) != 0) return false;
-  sv->covered.store(g * kWave, std::memory_order_release);
+  sv->covered.store(std::min(g * (uint32_t)kWave, a.nslots), std::memory_order_release);
   // instances on one stream run one after another: this one starts when the
   // one queued before it ends (never before now) and polls for a lifetime
   // from then; post to it until half of that is left.  (Counting from the
