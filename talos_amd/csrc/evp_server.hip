@@ -1,16 +1,20 @@
 // evp_server.hip — persistent "doorbell" server for synchronous per-call
-// EVP_AEAD_CTX_seal/open jobs on AES-GCM contexts.
+// EVP_AEAD_CTX_seal/open jobs on AES-GCM and RFC 7539 ChaCha20-Poly1305
+// contexts.
 //
 // A per-call job (e_aes.c:1424-1510 through evp_aead.c:89-144) is one record,
 // latency-bound: launching a kernel and waiting for it costs 11-12 µs on this
 // box before any cipher work (tools/hip_latency.hip).  With TLSGPU_EVP_DOORBELL
-// set, G workgroups of this kernel stay resident (one per CU, the T-tables
-// loaded into LDS once), each polling the doorbell slots of its calling
-// threads in pinned host memory (slot k belongs to workgroup k % G).  A posted
-// job is the same RawJob the launched path builds in the thread's pinned
-// staging; the workgroup runs it with the launched path's own code
-// (gcm_raw_job, gcm_raw.h), writes output and status straight to the staging
-// buffer and answers in the slot: one PCIe round trip per call, no launch.
+// set, up to G workgroups of this kernel stay resident (one per CU and per
+// calling thread, the T-tables loaded into LDS once), each polling the
+// doorbell slots of its calling threads in pinned host memory (slot k belongs
+// to workgroup k % gridDim.x).  A posted job is the same RawJob the launched
+// path builds in the thread's pinned staging; the workgroup runs it with the
+// launched path's own code (gcm_raw_job, gcm_raw.h; cc_wave_job,
+// chacha_wave.h on wave 0), writes output and status straight to the staging
+// buffer and answers in the slot: no launch per call.  Per installed key the
+// workgroup keeps the GHASH tables and the DevSession in LDS; a short GCM
+// job's input is staged into LDS by idle waves while the first waves parse.
 //
 // Coherence: the kernel outlives any one job, so nothing may be served from a
 // cache that a launch would have invalidated.  Session data is read with
@@ -26,8 +30,9 @@
 // host relaunches (engine.cpp EvpServer) so that a job is only ever posted
 // while an instance that will poll for at least half a lifetime is queued.
 #define TG_VECTOR_SESSION_LOADS 1
-// job phase marks (TLSGPU_EVP_DOORBELL_TRACE): wave 0, lane 0 stamps the
-// realtime clock into LDS; the server copies them to the slot's trace row
+// job phase marks (TLSGPU_EVP_DOORBELL_TRACE): thread t (0: wave 0, lane 0)
+// stamps the realtime clock into LDS; the server copies them to the slot's
+// trace row
 #define TG_JOB_MARK_AT(i, t)                                                    \
   do {                                                                          \
     if (threadIdx.x == (t))                                                     \
