@@ -1665,6 +1665,12 @@ static const bool g_doorbell_trace = [] {
 static void servers_stop_at_exit() {
   for (EvpServer* sv : g_servers)
     if (sv && sv->stop) __atomic_store_n(sv->stop, 1u, __ATOMIC_RELEASE);
+  // the running and queued instances see the stop word within 16 polls (or
+  // after the job they are on): let them drain before the runtime's own exit
+  // handlers (registered before this one, so they run after it) tear down
+  for (EvpServer* sv : g_servers)
+    if (sv && sv->stop && sv->stream && hipSetDevice(sv->device) == hipSuccess)
+      (void)hipStreamSynchronize(sv->stream);
   for (EvpServer* sv : g_servers) {
     const uint64_t n = sv ? sv->tr_n.load() : 0;
     if (!n) continue;
