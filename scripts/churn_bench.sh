@@ -10,7 +10,7 @@ OUT=${1:-$R/gpurun_out/churn.jsonl}
 for t in 1 16 64; do
   timeout -k 10 60 "$R/oracle/_ref/cpubench" "$R/oracle/_ref/libref.so" aes-128-gcm init 1400 $t $t 2 \
     | sed "s/^{/{\"lib\": \"reference\", /" >> "$OUT" || exit 1
-  timeout -k 10 60 "$R/oracle/_ref/cpubench" "$R/talos_amd/libtlsgpu.so" aes-128-gcm init 1400 $t $t 2 \
+  TLSGPU_EVP_DOORBELL=0 timeout -k 10 60 "$R/oracle/_ref/cpubench" "$R/talos_amd/libtlsgpu.so" aes-128-gcm init 1400 $t $t 2 \
     | sed "s/^{/{\"lib\": \"libtlsgpu per call\", /" >> "$OUT" || exit 1
   TLSGPU_EVP_BATCH_US=50 timeout -k 10 60 "$R/oracle/_ref/cpubench" "$R/talos_amd/libtlsgpu.so" aes-128-gcm init 1400 $t $t 2 \
     | sed "s/^{/{\"lib\": \"libtlsgpu queue 50us\", /" >> "$OUT" || exit 1

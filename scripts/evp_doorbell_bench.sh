@@ -10,7 +10,7 @@ OUT=${1:-$R/gpurun_out/evp_doorbell.jsonl}
 for len in 1400 16384; do
   for t in 1 16 64; do
     n=$((t * 8))
-    TLSGPU_EVP_SPIN=1 timeout -k 10 60 "$R/oracle/_ref/cpubench" "$R/talos_amd/libtlsgpu.so" \
+    TLSGPU_EVP_DOORBELL=0 TLSGPU_EVP_SPIN=1 timeout -k 10 60 "$R/oracle/_ref/cpubench" "$R/talos_amd/libtlsgpu.so" \
       aes-128-gcm seal $len $n $t 2 | sed "s/^{/{\"lib\": \"libtlsgpu per call launch+eventspin\", /" >> "$OUT" || exit 1
     for db in 0 16 64; do
       TLSGPU_EVP_DOORBELL=$db timeout -k 10 60 "$R/oracle/_ref/cpubench" "$R/talos_amd/libtlsgpu.so" \
@@ -19,7 +19,7 @@ for len in 1400 16384; do
   done
 done
 for t in 1 16; do
-  TLSGPU_EVP_SPIN=1 timeout -k 10 60 "$R/oracle/_ref/cpubench" "$R/talos_amd/libtlsgpu.so" \
+  TLSGPU_EVP_DOORBELL=0 TLSGPU_EVP_SPIN=1 timeout -k 10 60 "$R/oracle/_ref/cpubench" "$R/talos_amd/libtlsgpu.so" \
     chacha20-poly1305 seal 1400 $((t * 8)) $t 2 | sed "s/^{/{\"lib\": \"libtlsgpu per call launch+eventspin\", /" >> "$OUT" || exit 1
   for db in 0 16; do
     TLSGPU_EVP_DOORBELL=$db timeout -k 10 60 "$R/oracle/_ref/cpubench" "$R/talos_amd/libtlsgpu.so" \

@@ -10,7 +10,7 @@ for len in 1400 16384; do
   for t in 1 16 64; do
     n=$((t * 8))
     for zc in 0 1; do
-      TLSGPU_EVP_ZEROCOPY=$zc timeout -k 10 60 "$R/oracle/_ref/cpubench" "$R/talos_amd/libtlsgpu.so" \
+      TLSGPU_EVP_DOORBELL=0 TLSGPU_EVP_ZEROCOPY=$zc timeout -k 10 60 "$R/oracle/_ref/cpubench" "$R/talos_amd/libtlsgpu.so" \
         aes-128-gcm seal $len $n $t 2 | sed "s/^{/{\"lib\": \"libtlsgpu per call zerocopy=$zc\", /" >> "$OUT" || exit 1
       [ -n "$QUEUE" ] && { TLSGPU_EVP_BATCH_US=50 TLSGPU_EVP_ZEROCOPY=$zc timeout -k 10 60 "$R/oracle/_ref/cpubench" \
         "$R/talos_amd/libtlsgpu.so" aes-128-gcm seal $len $n $t 2 \

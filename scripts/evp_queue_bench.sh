@@ -10,6 +10,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$1
 mkdir -p $O
 B=$R/oracle/_ref/cpubench
+export TLSGPU_EVP_DOORBELL=${TLSGPU_EVP_DOORBELL:-0}  # round-3 semantics: the launched per-call path
 LIB=$R/talos_amd/libtlsgpu.so
 REF=$R/oracle/_ref/libref.so
 out=$O/evp_queue.jsonl

@@ -1631,9 +1631,14 @@ static EvpServer* g_servers[kMaxEvpDevices] = {};
 // process-wide mutex per call cost 16 calling threads more than the call)
 static std::atomic<EvpServer*> g_ready_servers[kMaxEvpDevices] = {};
 static std::mutex g_server_mu;
+// On by default (round 4): up to 64 server workgroups per EVP device, one
+// per calling thread; TLSGPU_EVP_DOORBELL=0 (or tlsgpu_evp_set_doorbell(0,
+// 0)) keeps every per-call job on the launched path.  The GPU suite runs green
+// both ways.
+constexpr unsigned kDoorbellDefaultGroups = 64;
 static unsigned g_doorbell_groups = [] {
   const char* v = getenv("TLSGPU_EVP_DOORBELL");
-  return v && *v ? (unsigned)strtoul(v, nullptr, 10) : 0u;
+  return v && *v ? (unsigned)strtoul(v, nullptr, 10) : kDoorbellDefaultGroups;
 }();
 static unsigned g_doorbell_ms = [] {
   const char* v = getenv("TLSGPU_EVP_DOORBELL_MS");
