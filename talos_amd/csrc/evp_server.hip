@@ -71,7 +71,9 @@ namespace tg {
 
 constexpr uint32_t kSrvExit = 0xFFFFFFFFu;
 constexpr uint32_t SRV_SEL_OFF = PLAN_OFF + 16 * 16;  // after gcm_raw_job's part_y words
+static_assert(SRV_SEL_OFF + 4 <= PLAN_OFF + 272, "gcm_raw_job's E_K(J0) word follows");
 constexpr uint32_t SRV_SLOT_OFF = PLAN_OFF + 512;     // LDS copy of the picked slot (256 B)
+static_assert(PLAN_OFF + 288 <= SRV_SLOT_OFF, "server LDS plan");
 static_assert(SRV_SLOT_OFF + sizeof(DoorbellSlot) <= SRV_STAGE_OFF, "server LDS plan");
 static_assert(SRV_STAGE_OFF + 4096 <= SRV_MARK_OFF, "server LDS plan");
 static_assert(SRV_MARK_OFF + 80 <= LDS_BYTES, "server LDS plan");

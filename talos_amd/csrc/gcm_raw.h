@@ -90,14 +90,20 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
   const uint32_t nwork = nsteps == 0 ? 1 : (nsteps + spw - 1) / spw;
   uint32_t y[4] = {0, 0, 0, 0};
   uint4* part_y = reinterpret_cast<uint4*>(s_lds + PLAN_OFF);
-  // E_K(J0) for the tag: on the last wave when it has no block range (jobs
-  // below 15 steps), in parallel with the blocks, else on wave 0 at the end
+  // E_K(J0) for the tag, off wave 0's path to the barrier: on the last wave
+  // when it has no block range (jobs below 15 steps), beside the blocks; else
+  // on the last working wave after its chain (the wave with the fewest
+  // Horner steps to raise its range by, so it has the slack).  Into LDS
+  // after the 16 partial sums (and the server's selection word).
+  uint4* ek_lds = reinterpret_cast<uint4*>(s_lds + PLAN_OFF + 272);
   const bool ek_early = nwork < (uint32_t)kWaves;
-  if (ek_early && wave == (uint32_t)kWaves - 1) {
+  const uint32_t ek_wave = ek_early ? (uint32_t)kWaves - 1 : nwork - 1;
+  auto form_ek0 = [&]() {
     uint32_t ek[4] = {rc.j0[0], rc.j0[1], rc.j0[2], rc.j0[3]};
     aes_block<ROUNDS>(ek, rk, as_const(S->rk_rot), laneoff);
-    if (lane == 0) part_y[kWaves - 1] = make_uint4(ek[0], ek[1], ek[2], ek[3]);
-  }
+    if (lane == 0) *ek_lds = make_uint4(ek[0], ek[1], ek[2], ek[3]);
+  };
+  if (ek_early && wave == ek_wave) form_ek0();
   if (wave < nwork) {
     const CtrConst cc = ctr_setup(rc.j0, rk, laneoff);
     TG_JOB_MARK(2);
@@ -137,6 +143,7 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
     y[1] = wave_xor_total(y[1]);
     y[2] = wave_xor_total(y[2]);
     y[3] = wave_xor_total(y[3]);
+    if (!ek_early && wave == ek_wave) form_ek0();
   }
   if (lane == 0 && wave < nwork) part_y[wave] = make_uint4(y[0], y[1], y[2], y[3]);
   __syncthreads();
@@ -149,14 +156,8 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
       t[0] ^= v.x; t[1] ^= v.y; t[2] ^= v.z; t[3] ^= v.w;
     }
   }
-  uint32_t ek0[4];
-  if (ek_early) {
-    const uint4 v = part_y[kWaves - 1];
-    ek0[0] = v.x; ek0[1] = v.y; ek0[2] = v.z; ek0[3] = v.w;
-  } else {
-    ek0[0] = rc.j0[0]; ek0[1] = rc.j0[1]; ek0[2] = rc.j0[2]; ek0[3] = rc.j0[3];
-    aes_block<ROUNDS>(ek0, rk, as_const(S->rk_rot), laneoff);
-  }
+  const uint4 ekv = *ek_lds;
+  const uint32_t ek0[4] = {ekv.x, ekv.y, ekv.z, ekv.w};
   TG_JOB_MARK(6);
   gcm_tag<SEAL>(rc, t, ek0, S, a.status + r, lane);
 }
