@@ -438,7 +438,7 @@ int tlsgpu_evp_call_stats(uint64_t *seal_calls, uint64_t *open_calls);
  * a context's first call (its key install still queued), draft-suite ChaCha
  * contexts and pooled (queued) contexts use the other paths.  Same as
  * TLSGPU_EVP_DOORBELL=<groups> (TLSGPU_EVP_DOORBELL_MS=<lifetime>) at load;
- * the default is 64 groups (on), groups = 0 turns it off; must be called
+ * off (0 groups) by default, 64 is the measured setting; must be called
  * before the first EVP call.  tlsgpu_evp_doorbell_stats: jobs
  * served and instances launched so far. */
 int tlsgpu_evp_set_doorbell(unsigned groups, unsigned lifetime_ms);

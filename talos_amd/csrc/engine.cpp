@@ -1631,11 +1631,12 @@ static EvpServer* g_servers[kMaxEvpDevices] = {};
 // process-wide mutex per call cost 16 calling threads more than the call)
 static std::atomic<EvpServer*> g_ready_servers[kMaxEvpDevices] = {};
 static std::mutex g_server_mu;
-// On by default (round 4): up to 64 server workgroups per EVP device, one
-// per calling thread; TLSGPU_EVP_DOORBELL=0 (or tlsgpu_evp_set_doorbell(0,
-// 0)) keeps every per-call job on the launched path.  The GPU suite runs green
-// both ways.
-constexpr unsigned kDoorbellDefaultGroups = 64;
+// Off by default: TLSGPU_EVP_DOORBELL=<G> (64 is the measured setting) or
+// tlsgpu_evp_set_doorbell turns it on.  Round 4 ran it on by default for one
+// suite run and saw one child process of test_evp_multi_device (two engines
+// on one GPU) exit with SIGSEGV after its last call — not understood yet, so
+// the launched path stays the default.
+constexpr unsigned kDoorbellDefaultGroups = 0;
 static unsigned g_doorbell_groups = [] {
   const char* v = getenv("TLSGPU_EVP_DOORBELL");
   return v && *v ? (unsigned)strtoul(v, nullptr, 10) : kDoorbellDefaultGroups;
