@@ -1617,6 +1617,7 @@ struct EvpServer {
   // workgroup cover every slot in use
   std::atomic<uint32_t> active{0}, hi_slot{0};
   std::atomic<uint32_t> covered{0};  // slots the last launched instance polls (64 per workgroup)
+  uint32_t launch_seq = 0, last_g = 0;  // the last launched instance (under mu)
   // TLSGPU_EVP_DOORBELL_TRACE=1: per-slot device timestamps (pinned) and their
   // sums, printed at exit: pick -> slot loaded -> job done -> released (ticks
   // of 10 ns), and the caller's post -> done-seen wall time (ns)
@@ -1630,6 +1631,7 @@ static EvpServer* g_servers[kMaxEvpDevices] = {};
 // the servers whose setup succeeded, read without the lock on every call (a
 // process-wide mutex per call cost 16 calling threads more than the call)
 static std::atomic<EvpServer*> g_ready_servers[kMaxEvpDevices] = {};
+constexpr uint32_t kExitedWord = 32;  // exit marks after the stop word (256 workgroups max)
 static std::mutex g_server_mu;
 // Off by default: TLSGPU_EVP_DOORBELL=<G> (64 is the measured setting) or
 // tlsgpu_evp_set_doorbell turns it on.  Round 4 ran it on by default for one
@@ -1671,12 +1673,18 @@ static const bool g_doorbell_trace = [] {
 static void servers_stop_at_exit() {
   for (EvpServer* sv : g_servers)
     if (sv && sv->stop) __atomic_store_n(sv->stop, 1u, __ATOMIC_RELEASE);
-  // the running and queued instances see the stop word within 16 polls (or
-  // after the job they are on): let them drain before the runtime's own exit
-  // handlers (registered before this one, so they run after it) tear down
-  for (EvpServer* sv : g_servers)
-    if (sv && sv->stop && sv->stream && hipSetDevice(sv->device) == hipSuccess)
-      (void)hipStreamSynchronize(sv->stream);
+  // the running instance sees the stop word within 16 polls (or after the
+  // job it is on), a queued one at its start: wait for the last launched
+  // instance's workgroups to mark their exit, by reading pinned memory only
+  // (no HIP call from an exit handler; bounded at 200 ms)
+  const uint64_t t0 = mono_ns();
+  for (EvpServer* sv : g_servers) {
+    if (!sv || !sv->stop || !sv->launch_seq) continue;
+    for (uint32_t b = 0; b < sv->last_g; b++)
+      while (__atomic_load_n(sv->stop + kExitedWord + b, __ATOMIC_ACQUIRE) != sv->launch_seq &&
+             mono_ns() - t0 < 200000000ull)
+        __builtin_ia32_pause();
+  }
   for (EvpServer* sv : g_servers) {
     const uint64_t n = sv ? sv->tr_n.load() : 0;
     if (!n) continue;
@@ -1719,7 +1727,8 @@ static EvpServer* evp_server(size_t k, tlsgpu_engine* e) {
           hipSuccess)
     return nullptr;
   memset(h, 0, sizeof(DoorbellSlot) * sv->nslots);
-  if (hipHostMalloc((void**)&stop, 128, hipHostMallocDefault) != hipSuccess ||
+  // one pinned page: [0] the stop word, [kExitedWord + b] workgroup b's exit mark
+  if (hipHostMalloc((void**)&stop, 4096, hipHostMallocDefault) != hipSuccess ||
       hipHostGetDevicePointer((void**)&sv->d_slots, h, 0) != hipSuccess ||
       hipHostGetDevicePointer((void**)&sv->d_stop, stop, 0) != hipSuccess ||
       hipStreamCreateWithFlags(&sv->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -1732,7 +1741,7 @@ static EvpServer* evp_server(size_t k, tlsgpu_engine* e) {
            hipSuccess ||
        hipHostGetDevicePointer((void**)&sv->d_trace, sv->trace, 0) != hipSuccess))
     sv->trace = sv->d_trace = nullptr;
-  *stop = 0;
+  memset(stop, 0, 4096);
   sv->stop = stop;
   for (uint32_t i = sv->nslots; i-- > 0;) sv->free_slots.push_back(i);
   sv->slots = h;
@@ -1760,9 +1769,13 @@ static bool server_ensure(EvpServer* sv) {
   a.stop = sv->d_stop;
   a.lifetime = sv->lifetime_ns / 10;  // 100 MHz realtime ticks
   a.trace = reinterpret_cast<unsigned long long*>(sv->d_trace);
+  a.exited = sv->d_stop + kExitedWord;
+  a.seq = sv->launch_seq + 1;
   const uint32_t cover = (hi + kWave - 1) / kWave;
   const uint32_t g = std::min(sv->groups, std::max({1u, sv->active.load(std::memory_order_acquire), cover}));
   if (launch_evp_server(a, (int)g, sv->stream) != 0) return false;
+  sv->launch_seq = a.seq;
+  sv->last_g = g;
   sv->covered.store(std::min(g * (uint32_t)kWave, a.nslots), std::memory_order_release);
   // instances on one stream run one after another: this one starts when the
   // one queued before it ends (never before now) and polls for a lifetime

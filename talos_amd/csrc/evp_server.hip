@@ -113,7 +113,23 @@ __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Leaving: every earlier store of this workgroup completed (the done flags
+// were released job by job), then the launch number into exited[blockIdx.x].
+__device__ __forceinline__ void srv_leave(const ServerArgs& s) {
+  if (threadIdx.x == 0) {
+    __atomic_thread_fence(__ATOMIC_RELEASE);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(s.exited + blockIdx.x, s.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
+  // an instance that only starts after the stop word was set (queued behind
+  // the one the process was using at exit) leaves at once
+  if (__hip_atomic_load(s.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
+    srv_leave(s);
+    return;
+  }
   fill_aes_lds<kThreads>();
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -240,6 +256,7 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
     }
     if (wave == 0 && mine == k) served = post;
   }
+  srv_leave(s);
 }
 
 int launch_evp_server(const ServerArgs& a, int groups, hipStream_t s) {

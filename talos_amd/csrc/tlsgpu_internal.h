@@ -289,6 +289,9 @@ struct ServerArgs {
   uint32_t nslots;
   const uint32_t* stop;       // pinned word: non-zero = exit now
   unsigned long long lifetime;  // s_memrealtime ticks (100 MHz) a workgroup serves at most
+  uint32_t* exited;             // pinned [gridDim.x]: a workgroup stores `seq` here as it
+                                // leaves (the host's exit drain waits on it, no HIP call)
+  uint32_t seq;                 // this instance's launch number (from 1)
   unsigned long long* trace;    // null, or pinned [nslots][kTraceWords]: realtime at pick,
                                 // slot loaded, GCM job marks 0..6, job done, answer
                                 // released (TLSGPU_EVP_DOORBELL_TRACE)
