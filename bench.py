@@ -228,6 +228,10 @@ def main():
     ap.add_argument("--records", type=int, default=0, help="override records per GPU")
     ap.add_argument("--sessions", type=int, default=0,
                     help="override sessions per GPU (SURVEY.md §8d sensitivity: 1 .. #records)")
+    ap.add_argument("--slot-align", type=int, default=16,
+                    help="alignment of every record's plaintext and ciphertext slot in the "
+                         "device buffers (default 16; 128 = each record on its own cache lines, "
+                         "a measurement option: the golden digests use 16)")
     ap.add_argument("--interleave", action="store_true",
                     help="deal records to sessions round-robin (a many-connection server "
                          "batch) instead of grouping each session's records")
@@ -290,6 +294,7 @@ def main():
     lo, hi = shard_by_bytes(glob, shards, rank)
     lengths = None if rec_len else glob[lo:hi]
     wl = Workload(eng, kind, shards * per_gpu, shards * sessions, seed, lengths=lengths,
+                  slot_align=args.slot_align,
                   record_len=rec_len or 0,
                   tamper_every=1024 if op == "open" and args.mode != "wire" else 0,
                   interleave=args.interleave, shard=(lo, hi))
@@ -397,6 +402,7 @@ def main():
                                 if args.config == "E" else ""),
                    "records_per_gpu": per_gpu, "sessions_per_gpu": sessions,
                    "session_order": "interleaved" if args.interleave else "grouped",
+                   "slot_align": args.slot_align,
                    "gcm_impl": ta.get_gcm_impl() if "gcm" in kind_name else None,
                    "batch_hints": args.hints,
                    "payload_bytes_per_gpu": total_len, "parallelism": f"batch split x{world}"},

@@ -97,10 +97,15 @@ class Workload:
 
     def __init__(self, engine, kind: int, n_records: int, n_sessions: int, seed: int,
                  lengths=None, record_len: int = 16384, tamper_every: int = 0,
-                 interleave: bool = False, shard: tuple[int, int] | None = None):
+                 interleave: bool = False, shard: tuple[int, int] | None = None,
+                 slot_align: int = 16):
         """n_records / n_sessions describe the whole batch; `shard` = (lo, hi)
         keeps records [lo, hi) of it on this engine (default: all).  `lengths`
-        are the kept records' lengths."""
+        are the kept records' lengths.  `slot_align` (a multiple of 16): the
+        alignment of every plaintext and ciphertext slot (16 by default; 128
+        puts every record on its own cache lines — a measurement option)."""
+        if slot_align < 16 or slot_align % 16:
+            raise ValueError("slot_align must be a multiple of 16")
         lo, hi = shard if shard is not None else (0, n_records)
         if not 0 <= lo <= hi <= n_records:
             raise ValueError(f"shard {lo}:{hi} outside the {n_records}-record batch")
@@ -116,11 +121,16 @@ class Workload:
         total = n_records
         n_records = hi - lo   # from here on: this shard's records
         eiv = EXPLICIT_NONCE_LEN[kind]
-        pt_slot = (self.lengths + 15) // 16 * 16
-        body_slot = (self.lengths + eiv + TAG_LEN + 15 + 16) // 16 * 16
+        A = slot_align
+        shift = (A - eiv) % A   # the ciphertext (after the explicit nonce) A-B aligned
+        pt_slot = (self.lengths + A - 1) // A * A
+        if A == 16:   # the default layout (golden digests depend on it)
+            body_slot = (self.lengths + eiv + TAG_LEN + 15 + 16) // 16 * 16
+        else:
+            body_slot = (self.lengths + shift + eiv + TAG_LEN + A - 1) // A * A
         self.pt_off = np.concatenate([[0], np.cumsum(pt_slot)[:-1]]).astype(np.uint64)
         body_base = np.concatenate([[0], np.cumsum(body_slot)[:-1]]).astype(np.uint64)
-        self.body_off = body_base + np.uint64((16 - eiv) % 16)   # ciphertext 16-B aligned
+        self.body_off = body_base + np.uint64(shift)
         self.pt_bytes = int(pt_slot.sum())
         self.body_bytes = int(body_slot.sum()) + 16
 
