@@ -10,7 +10,9 @@ server runs, across server relaunches (short lifetime), and the server must
 stop by itself when the calls stop.  ChaCha jobs run on the server's wave 0
 (chacha_wave.h) between GCM jobs, whose LDS table cache they must leave
 intact; draft-suite ChaCha contexts take the launched path in the same
-threads."""
+threads.  Inputs up to 4 KiB travel in the slot's input area (read with the
+slot): the lengths cover both sides of that limit for seal (4,096 B of
+plaintext) and open (4,080 + 16 B of ciphertext and tag)."""
 import os
 import subprocess
 import sys
@@ -43,7 +45,7 @@ def worker(t):
                 nlen = (12 if kind == po.CHACHA20_POLY1305 else 8 if kind == po.CHACHA20_POLY1305_OLD
                         else rnd.choice([12, 12, 1, 8, 16, 60]))
                 nonce = bytes(rnd.randrange(256) for _ in range(nlen))
-                pt = bytes(rnd.randrange(256) for _ in range(rnd.choice([0, 1, 15, 100, 1400, 4096, 16384, 40000])))
+                pt = bytes(rnd.randrange(256) for _ in range(rnd.choice([0, 1, 15, 100, 1400, 4080, 4081, 4096, 16384, 40000])))
                 ad = bytes(rnd.randrange(256) for _ in range(rnd.choice([0, 13, 100])))
                 ok, exp = orc.seal(octx, nonce, pt, ad)
                 ok2, got, ol = ctx.seal(nonce, pt, ad)
