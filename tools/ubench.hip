@@ -21,6 +21,7 @@
 // host reports cycles per wave-instruction per SIMD (VALU) or per CU (LDS),
 // plus the effective shader clock (s_memtime ticks / s_memrealtime at 100 MHz).
 //   set2              VALU/LDS interference: LDS chains with K extra VALU ops
+//   set6              config C's record-stream memory pattern alone (copy_records)
 //                     per read, LDS-only waves beside VALU-only waves, ds_read_b64,
 //                     the AES round with four rotated tables (no alignbit)
 // Prints one JSON line per measurement.   usage: ubench [set2]
@@ -666,6 +667,41 @@ __global__ void __launch_bounds__(512) copy_chunk(const float4* __restrict__ a4,
   }
 }
 
+
+// set6: config C's memory pattern alone.  A wave owns 64 consecutive records
+// and moves STEP bytes of each per step (STEP / 16 lanes per record, so one
+// instruction covers 1024 / STEP records), as chacha_tls_kernel's staged steps
+// do, without the LDS tile or the cipher: which part of C's memory half is
+// the access pattern itself (many concurrent record streams, windows that
+// straddle lines) rather than the kernel.
+template <int STEP>
+__global__ void __launch_bounds__(256) copy_records(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                    uint32_t nrec, uint32_t len, uint32_t in_stride,
+                                                    uint32_t in_off, uint32_t out_stride, uint32_t out_off) {
+  constexpr int LPR = STEP / 16;        // lanes per record
+  constexpr int RPI = 64 / LPR;         // records per instruction
+  constexpr int NI = 64 / RPI;          // instructions per step (64 records)
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  const uint32_t r0 = wave * 64;
+  if (r0 >= nrec) return;
+  const uint32_t piece = 16 * (lane % LPR);
+  for (uint32_t s = 0; s * STEP < len; s++) {
+    v4u_t x[NI];
+#pragma unroll
+    for (int i = 0; i < NI; i++) {
+      const uint32_t r = r0 + i * RPI + lane / LPR;
+      const uint32_t o = s * STEP + piece;
+      x[i] = o < len ? *(const v4u_t*)(in + (size_t)r * in_stride + in_off + o) : v4u_t{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int i = 0; i < NI; i++) {
+      const uint32_t r = r0 + i * RPI + lane / LPR;
+      const uint32_t o = s * STEP + piece;
+      if (o < len) *(v4u_t*)(out + (size_t)r * out_stride + out_off + o) = x[i];
+    }
+  }
+}
 // ---------------------------------------------------------------------------
 static int g_cus = 256;
 static Stamp* g_st;
@@ -873,6 +909,54 @@ __global__ void cc_compute_kernel(int iters, Stamp* st, uint32_t* out) {
   stamp_end(st, t0, r0, acc ^ p.h0 ^ p.h4, out);
 }
 
+
+static void set6() {
+  const uint32_t nrec = 1u << 20, len = 1408;
+  const size_t cap = (size_t)nrec * 1536 + 4096;
+  uint8_t *a, *b;
+  CK(hipMalloc(&a, cap));
+  CK(hipMalloc(&b, cap));
+  CK(hipMemset(a, 1, cap));
+  struct V { const char* name; int step; uint32_t is, io, os, oo; };
+  const V vs[] = {
+      {"seal_like_1408_to_1440+8", 128, 1408, 0, 1440, 8},
+      {"open_like_1440+8_to_1408", 128, 1440, 8, 1408, 0},
+      {"line_aligned_1536", 128, 1536, 0, 1536, 0},
+      {"seal_like_step256", 256, 1408, 0, 1440, 8},
+      {"open_like_step256", 256, 1440, 8, 1408, 0},
+      {"line_aligned_step256", 256, 1536, 0, 1536, 0},
+      {"contiguous_1408", 128, 1408, 0, 1408, 0},
+  };
+  for (const V& v : vs) {
+    auto launch = [&]() {
+      const uint32_t blocks = nrec / 64 / 4;
+      if (v.step == 128)
+        copy_records<128><<<blocks, 256>>>(a, b, nrec, len, v.is, v.io, v.os, v.oo);
+      else
+        copy_records<256><<<blocks, 256>>>(a, b, nrec, len, v.is, v.io, v.os, v.oo);
+    };
+    launch();
+    CK(hipDeviceSynchronize());
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const int reps = 10;
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < reps; i++) launch();
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double gbps = 2.0 * nrec * len * reps / (ms / 1e3) / 1e9;
+    printf("{\"bench\": \"record_copy\", \"pattern\": \"%s\", \"step\": %d, \"records\": %u, "
+           "\"len\": %u, \"ms\": %.4f, \"GBps_read_plus_write\": %.1f, \"frac_of_8TBs\": %.4f}\n",
+           v.name, v.step, nrec, len, ms / reps, gbps, gbps / 8000.0);
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+  }
+  CK(hipFree(a));
+  CK(hipFree(b));
+}
 static void set5() {
   // waves per SIMD W: 1,024-thread workgroups (4 waves per SIMD each), one
   // (96 KiB LDS) or two (64 KiB) per CU; 256 * W threads for W < 4
@@ -1156,6 +1240,10 @@ int main(int argc, char** argv) {
         (const void*)cc_compute_kernel<1, 4>, (const void*)cc_compute_kernel<2, 8>,
         (const void*)cc_compute_kernel<1, 1>})
     CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+  if (argc > 1 && !strcmp(argv[1], "set6")) {
+    set6();
+    return 0;
+  }
   if (argc > 1 && !strcmp(argv[1], "set5")) {
     set5();
     fflush(stdout);
