@@ -674,7 +674,15 @@ __global__ void __launch_bounds__(512) copy_chunk(const float4* __restrict__ a4,
 // do, without the LDS tile or the cipher: which part of C's memory half is
 // the access pattern itself (many concurrent record streams, windows that
 // straddle lines) rather than the kernel.
-template <int STEP>
+// store cache policy of copy_records: 0 default, 1 nt, 2 sc1, 3 sc0 sc1
+template <int POL>
+__device__ __forceinline__ void st16_pol(void* p, v4u_t v) {
+  if constexpr (POL == 0) *(v4u_t*)p = v;
+  else if constexpr (POL == 1) asm volatile("global_store_dwordx4 %0, %1, off nt" :: "v"(p), "v"(v) : "memory");
+  else if constexpr (POL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
+  else asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(p), "v"(v) : "memory");
+}
+template <int STEP, int POL = 0>
 __global__ void __launch_bounds__(256) copy_records(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                     uint32_t nrec, uint32_t len, uint32_t in_stride,
                                                     uint32_t in_off, uint32_t out_stride, uint32_t out_off) {
@@ -698,7 +706,7 @@ __global__ void __launch_bounds__(256) copy_records(const uint8_t* __restrict__ 
     for (int i = 0; i < NI; i++) {
       const uint32_t r = r0 + i * RPI + lane / LPR;
       const uint32_t o = s * STEP + piece;
-      if (o < len) *(v4u_t*)(out + (size_t)r * out_stride + out_off + o) = x[i];
+      if (o < len) st16_pol<POL>(out + (size_t)r * out_stride + out_off + o, x[i]);
     }
   }
 }
@@ -917,7 +925,7 @@ static void set6() {
   CK(hipMalloc(&a, cap));
   CK(hipMalloc(&b, cap));
   CK(hipMemset(a, 1, cap));
-  struct V { const char* name; int step; uint32_t is, io, os, oo; };
+  struct V { const char* name; int step; uint32_t is, io, os, oo; int pol = 0; };
   const V vs[] = {
       {"seal_like_1408_to_1440+8", 128, 1408, 0, 1440, 8},
       {"open_like_1440+8_to_1408", 128, 1440, 8, 1408, 0},
@@ -926,11 +934,21 @@ static void set6() {
       {"open_like_step256", 256, 1440, 8, 1408, 0},
       {"line_aligned_step256", 256, 1536, 0, 1536, 0},
       {"contiguous_1408", 128, 1408, 0, 1408, 0},
+      {"seal_like_store_nt", 128, 1408, 0, 1440, 8, 1},
+      {"seal_like_store_sc1", 128, 1408, 0, 1440, 8, 2},
+      {"seal_like_store_sc0sc1", 128, 1408, 0, 1440, 8, 3},
+      {"seal_like_1408_to_1440+0", 128, 1408, 0, 1440, 0},
   };
   for (const V& v : vs) {
     auto launch = [&]() {
       const uint32_t blocks = nrec / 64 / 4;
-      if (v.step == 128)
+      if (v.step == 128 && v.pol == 1)
+        copy_records<128, 1><<<blocks, 256>>>(a, b, nrec, len, v.is, v.io, v.os, v.oo);
+      else if (v.step == 128 && v.pol == 2)
+        copy_records<128, 2><<<blocks, 256>>>(a, b, nrec, len, v.is, v.io, v.os, v.oo);
+      else if (v.step == 128 && v.pol == 3)
+        copy_records<128, 3><<<blocks, 256>>>(a, b, nrec, len, v.is, v.io, v.os, v.oo);
+      else if (v.step == 128)
         copy_records<128><<<blocks, 256>>>(a, b, nrec, len, v.is, v.io, v.os, v.oo);
       else
         copy_records<256><<<blocks, 256>>>(a, b, nrec, len, v.is, v.io, v.os, v.oo);
@@ -948,9 +966,9 @@ static void set6() {
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
     const double gbps = 2.0 * nrec * len * reps / (ms / 1e3) / 1e9;
-    printf("{\"bench\": \"record_copy\", \"pattern\": \"%s\", \"step\": %d, \"records\": %u, "
+    printf("{\"bench\": \"record_copy\", \"pattern\": \"%s\", \"step\": %d, \"store_policy\": %d, \"records\": %u, "
            "\"len\": %u, \"ms\": %.4f, \"GBps_read_plus_write\": %.1f, \"frac_of_8TBs\": %.4f}\n",
-           v.name, v.step, nrec, len, ms / reps, gbps, gbps / 8000.0);
+           v.name, v.step, v.pol, nrec, len, ms / reps, gbps, gbps / 8000.0);
     CK(hipEventDestroy(e0));
     CK(hipEventDestroy(e1));
   }
