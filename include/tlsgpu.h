@@ -42,6 +42,7 @@ enum tlsgpu_aead {
 #define TLSGPU_ENOMEM (-2)
 #define TLSGPU_EHIP (-3)	/* HIP runtime error (no GPU, launch failure) */
 #define TLSGPU_ERANGE (-4)	/* session id / size out of range */
+#define TLSGPU_ETIMEOUT (-5)	/* a bounded wait expired (tlsgpu_evp_shutdown) */
 
 /* Per-record status written by the batch calls (int32 per record).
  *   >= 0  success: plaintext length (open) or record body length (seal)
@@ -443,6 +444,21 @@ int tlsgpu_evp_call_stats(uint64_t *seal_calls, uint64_t *open_calls);
  * served and instances launched so far. */
 int tlsgpu_evp_set_doorbell(unsigned groups, unsigned lifetime_ms);
 int tlsgpu_evp_doorbell_stats(uint64_t *jobs, uint64_t *launches);
+/* tlsgpu_evp_doorbell_warm: launch a server instance now on every EVP device
+ * whose queued instance would stop polling within half a lifetime (what the
+ * next call would do), e.g. before a burst of calls.  No-op with the doorbell
+ * off or after shutdown.
+ * tlsgpu_evp_shutdown: the doorbell's shutdown contract.  Stops every server,
+ * then waits until every instance ever launched — running or still queued
+ * behind other work — has left, reading pinned memory only (no HIP call);
+ * later EVP calls take the launched path.  TLSGPU_ETIMEOUT if an instance is
+ * still running after TLSGPU_EVP_SHUTDOWN_MS (default 60 s).  Idempotent.
+ * The library runs it itself first thing at process exit (the main thread's
+ * thread-local destructors run before the HIP runtime's exit-time teardown),
+ * from an atexit handler and from its destructor; an application that tears
+ * the runtime down itself (hipDeviceReset) calls it before. */
+int tlsgpu_evp_doorbell_warm(void);
+int tlsgpu_evp_shutdown(void);
 /* Test support.  tlsgpu_evp_context_slot: the session table and slot that hold
  * a live EVP context's device key material.  tlsgpu_sessions_debug_read: after
  * every queued install / scrub of `slot` has finished, copy its first n bytes

@@ -158,6 +158,8 @@ def load_library(path: str = LIBPATH) -> C.CDLL:
         "tlsgpu_evp_context_slot": (i32, [vp, C.POINTER(C.c_void_p), C.POINTER(C.c_uint32)]),
         "tlsgpu_evp_set_doorbell": (i32, [C.c_uint, C.c_uint]),
         "tlsgpu_evp_doorbell_stats": (i32, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+        "tlsgpu_evp_doorbell_warm": (i32, []),
+        "tlsgpu_evp_shutdown": (i32, []),
         "tlsgpu_sessions_debug_read": (i32, [vp, u32, vp, C.c_size_t]),
         "tlsgpu_evp_device_count": (u32, []),
         "tlsgpu_evp_device_stats": (i32, [u32, C.POINTER(i32), C.POINTER(C.c_uint64),
@@ -694,9 +696,23 @@ def evp_device_stats() -> list[tuple[int, int, int]]:
 
 
 def evp_set_doorbell(groups: int, lifetime_ms: int = 0) -> None:
-    """Per-call AES-GCM EVP jobs through resident server workgroups
-    (tlsgpu_evp_set_doorbell); before the first EVP call."""
+    """Per-call AES-GCM and RFC 7539 ChaCha20-Poly1305 EVP jobs through
+    resident server workgroups (tlsgpu_evp_set_doorbell; a short GCM job's
+    input is staged into LDS by the server's idle waves); before the first
+    EVP call."""
     _check(load_library().tlsgpu_evp_set_doorbell(groups, lifetime_ms), "tlsgpu_evp_set_doorbell")
+
+
+def evp_doorbell_warm() -> None:
+    """Launch a server instance now where the next call would (tlsgpu_evp_doorbell_warm)."""
+    _check(load_library().tlsgpu_evp_doorbell_warm(), "tlsgpu_evp_doorbell_warm")
+
+
+def evp_shutdown() -> None:
+    """The doorbell's shutdown contract (tlsgpu_evp_shutdown): stop every
+    server and wait until every launched instance has left; later EVP calls
+    take the launched path."""
+    _check(load_library().tlsgpu_evp_shutdown(), "tlsgpu_evp_shutdown")
 
 
 def evp_doorbell_stats() -> tuple[int, int]:

@@ -22,7 +22,9 @@
 #include <new>
 #include <unistd.h>
 #include <climits>
+#include <csignal>
 #include <deque>
+#include <execinfo.h>
 #include <linux/futex.h>
 #include <sched.h>
 #include <sys/syscall.h>
@@ -1329,9 +1331,16 @@ struct Staging {
   uint8_t* h_dev = nullptr;  // h_buf as the device addresses it (zero-copy calls)
   size_t cap = 0;
   ~Staging() {
+    if (device >= 0) (void)hipSetDevice(device);  // the buffers' and the event's device
     if (d_buf) (void)hipFree(d_buf);
     if (h_buf) (void)hipHostFree(h_buf);
     if (done) (void)hipEventDestroy(done);
+  }
+  // A job that may still run on the device owns the buffers (a doorbell post
+  // nobody answered): forget them without freeing, the next ensure allocates.
+  void abandon() {
+    d_buf = h_buf = h_dev = nullptr;
+    cap = 0;
   }
   bool ensure(int dev, size_t bytes) {
     if (dev < 0 || dev >= kMaxDev || hipSetDevice(dev) != hipSuccess) return false;
@@ -1361,10 +1370,23 @@ struct Staging {
     return true;
   }
 };
+// Staging of exited threads, per device, for the next thread (round 5): a
+// thread's exit makes no HIP call — hipFree / hipHostFree would synchronise
+// the device, i.e. wait behind doorbell server instances that other threads
+// keep relaunching, and at process exit they ran before the servers were
+// stopped.  The buffers live until the runtime's teardown.
+static std::mutex g_stage_pool_mu;
+static std::vector<Staging*> g_stage_pool[kMaxDev];
+static void evp_shutdown_main_thread_exit();
 struct StagingSet {
   Staging* by_dev[kMaxDev] = {};
   ~StagingSet() {
-    for (Staging* st : by_dev) delete st;
+    // the main thread's staging goes at exit(): stop and drain the doorbell
+    // servers first (shutdown contract)
+    evp_shutdown_main_thread_exit();
+    std::lock_guard<std::mutex> lk(g_stage_pool_mu);
+    for (int d = 0; d < kMaxDev; d++)
+      if (by_dev[d]) g_stage_pool[d].push_back(by_dev[d]);
   }
 };
 static thread_local StagingSet t_stages;
@@ -1373,6 +1395,13 @@ static thread_local StagingSet t_stages;
 static Staging* stage_for(int dev) {
   if (dev < 0 || dev >= kMaxDev) return nullptr;
   Staging*& st = t_stages.by_dev[dev];
+  if (!st) {
+    std::lock_guard<std::mutex> lk(g_stage_pool_mu);
+    if (!g_stage_pool[dev].empty()) {
+      st = g_stage_pool[dev].back();
+      g_stage_pool[dev].pop_back();
+    }
+  }
   if (!st) st = new (std::nothrow) Staging();
   return st;
 }
@@ -1579,8 +1608,8 @@ static const bool g_evp_zerocopy = [] {
 }();
 
 // ---------------------------------------------------------------------------
-// Doorbell server (round 4, evp_server.hip): per-call AES-GCM jobs without a
-// kernel launch.  TLSGPU_EVP_DOORBELL=<G> (or tlsgpu_evp_set_doorbell) keeps G
+// Doorbell server (round 4, evp_server.hip): per-call AES-GCM and RFC 7539
+// ChaCha20-Poly1305 jobs without a kernel launch.  TLSGPU_EVP_DOORBELL=<G> (or tlsgpu_evp_set_doorbell) keeps G
 // server workgroups resident per EVP device while calls arrive; a calling
 // thread owns one slot of kSlotsPerGroup * G (slot k -> workgroup k % G), posts
 // its job number there and spins on the answer.  An instance lives `lifetime`
@@ -1588,7 +1617,9 @@ static const bool g_evp_zerocopy = [] {
 // after half of that has passed, on the same stream: a job is only posted
 // while an instance that still polls for at least half a lifetime is queued or
 // running, so every posted job is served, and a process that stops calling
-// leaves nothing spinning.  ChaCha20-Poly1305 contexts keep the launched path.
+// leaves nothing spinning.  Draft ("old") ChaCha20-Poly1305 contexts, pooled
+// (queued) contexts and a context's first call keep the launched path; a short
+// GCM job's input is staged into LDS by the server's idle waves.
 // The lifetime is short on purpose: this box runs at most GPU_MAX_HW_QUEUES = 4
 // hardware queues per process, so with more streams than that (engine + 4 call
 // streams + server) the server's queue is shared, and a kernel launched on a
@@ -1618,6 +1649,9 @@ struct EvpServer {
   std::atomic<uint32_t> active{0}, hi_slot{0};
   std::atomic<uint32_t> covered{0};  // slots the last launched instance polls (64 per workgroup)
   uint32_t launch_seq = 0, last_g = 0;  // the last launched instance (under mu)
+  // every launched instance whose workgroups have not all been seen leaving:
+  // (launch number, workgroups), oldest first (under mu; pruned at each launch)
+  std::vector<std::pair<uint32_t, uint32_t>> outstanding;
   // TLSGPU_EVP_DOORBELL_TRACE=1: per-slot device timestamps (pinned) and their
   // sums, printed at exit: pick -> slot loaded -> job done -> released (ticks
   // of 10 ns), and the caller's post -> done-seen wall time (ns)
@@ -1634,10 +1668,10 @@ static std::atomic<EvpServer*> g_ready_servers[kMaxEvpDevices] = {};
 constexpr uint32_t kExitedWord = 32;  // exit marks after the stop word (256 workgroups max)
 static std::mutex g_server_mu;
 // Off by default: TLSGPU_EVP_DOORBELL=<G> (64 is the measured setting) or
-// tlsgpu_evp_set_doorbell turns it on.  Round 4 ran it on by default for one
-// suite run and saw one child process of test_evp_multi_device (two engines
-// on one GPU) exit with SIGSEGV after its last call — not understood yet, so
-// the launched path stays the default.
+// tlsgpu_evp_set_doorbell turns it on.  The round-4 exit SIGSEGV is explained
+// and fixed by the shutdown contract below; the default is a
+// design choice: a server holds up to G CUs for a lifetime after the last
+// call, which a process that mixes per-call and batch work should opt into.
 constexpr unsigned kDoorbellDefaultGroups = 0;
 static unsigned g_doorbell_groups = [] {
   const char* v = getenv("TLSGPU_EVP_DOORBELL");
@@ -1665,26 +1699,188 @@ static const uint64_t g_doorbell_yield_ns = [] {
   return (v && *v ? (uint64_t)strtoull(v, nullptr, 10) : 100ull) * 1000ull;
 }();
 
+// Test hook (tests/test_evp_doorbell.py): sleep this long between a call's
+// server_ensure and its post, as a caller descheduled there would.
+static const unsigned g_test_post_delay_us = [] {
+  const char* v = getenv("TLSGPU_TEST_DOORBELL_POST_DELAY_US");
+  return v && *v ? (unsigned)strtoul(v, nullptr, 10) : 0u;
+}();
+
 static const bool g_doorbell_trace = [] {
   const char* v = getenv("TLSGPU_EVP_DOORBELL_TRACE");
   return v && *v && *v != '0';
 }();
 
-static void servers_stop_at_exit() {
+// ---------------------------------------------------------------------------
+// Shutdown contract (round 5).
+// A server instance reads and writes pinned host memory (its slots, the stop
+// page, the callers' staging) for as long as it runs, and instances queue on
+// the server's stream (and on whatever shares its hardware queue).  Before
+// the HIP runtime tears down — it frees every pinned allocation — every
+// instance ever launched must have left.  tlsgpu_evp_shutdown():
+//   1. no new instance and no new post from here on (g_evp_shutdown);
+//   2. the stop word of every server: a running instance leaves within 16
+//      polls or after the job it is on, a queued one at its first instruction;
+//   3. waits for EVERY outstanding instance's exit marks (not only the last
+//      one's), reading pinned memory only — no HIP call — with no silent cap:
+//      a note on stderr after 1 s, TLSGPU_ETIMEOUT after TLSGPU_EVP_SHUTDOWN_MS
+//      (default 60,000);
+//   4. callers still spinning on a post see the drain and take the launched
+//      path for that call if no instance served it.
+// It runs at the earliest point of process exit (a thread-local guard of the
+// main thread: thread-local destructors of the exiting thread run before any
+// atexit or static destructor, so before the runtime's), again from an atexit
+// handler (exit from another thread) and from the library destructor
+// (dlclose); it is idempotent.  At exit a drain that timed out ends the
+// process with _exit(70) before the runtime's teardown can free memory a
+// still-running instance uses.
+static std::atomic<int> g_evp_shutdown{0};  // 0 running, 1 stopping, 2 drained
+static std::mutex g_shutdown_mu;
+static const uint64_t g_shutdown_cap_ns = [] {
+  const char* v = getenv("TLSGPU_EVP_SHUTDOWN_MS");
+  const uint64_t ms = v && *v ? strtoull(v, nullptr, 10) : 60000ull;
+  return (ms ? ms : 60000ull) * 1000000ull;
+}();
+static const bool g_shutdown_verbose = [] {
+  const char* v = getenv("TLSGPU_EVP_SHUTDOWN_VERBOSE");
+  return v && *v && *v != '0';
+}();
+
+// Every workgroup of instance `seq` (g workgroups) has left.  A workgroup
+// stores its instance's launch number into exited[b] as its last act;
+// instances of one server run one after another on its stream, so a mark
+// >= seq (wrapping compare) means workgroup b of this instance or of a later
+// one — which only started after this one ended — has left.
+static bool instance_left(const EvpServer* sv, uint32_t seq, uint32_t g) {
+  for (uint32_t b = 0; b < g; b++)
+    if ((int32_t)(__atomic_load_n(sv->stop + kExitedWord + b, __ATOMIC_ACQUIRE) - seq) < 0)
+      return false;
+  return true;
+}
+
+static void print_doorbell_trace();
+
+extern "C" int tlsgpu_evp_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_shutdown_mu);
+  if (g_evp_shutdown.load(std::memory_order_acquire) == 2) return TLSGPU_OK;
+  g_evp_shutdown.store(1, std::memory_order_seq_cst);
   for (EvpServer* sv : g_servers)
-    if (sv && sv->stop) __atomic_store_n(sv->stop, 1u, __ATOMIC_RELEASE);
-  // the running instance sees the stop word within 16 polls (or after the
-  // job it is on), a queued one at its start: wait for the last launched
-  // instance's workgroups to mark their exit, by reading pinned memory only
-  // (no HIP call from an exit handler; bounded at 200 ms)
+    if (sv && sv->stop) __atomic_store_n(sv->stop, 1u, __ATOMIC_SEQ_CST);
   const uint64_t t0 = mono_ns();
+  bool noted = false;
+  uint32_t waited = 0;
   for (EvpServer* sv : g_servers) {
-    if (!sv || !sv->stop || !sv->launch_seq) continue;
-    for (uint32_t b = 0; b < sv->last_g; b++)
-      while (__atomic_load_n(sv->stop + kExitedWord + b, __ATOMIC_ACQUIRE) != sv->launch_seq &&
-             mono_ns() - t0 < 200000000ull)
+    if (!sv || !sv->stop) continue;
+    std::vector<std::pair<uint32_t, uint32_t>> pend;
+    {
+      // server_ensure checks g_evp_shutdown under this lock: no instance is
+      // launched after this copy
+      std::lock_guard<std::mutex> lk2(sv->mu);
+      pend = sv->outstanding;
+    }
+    for (const auto& inst : pend) {
+      waited++;
+      while (!instance_left(sv, inst.first, inst.second)) {
         __builtin_ia32_pause();
+        const uint64_t t = mono_ns() - t0;
+        if (!noted && t > 1000000000ull) {
+          fprintf(stderr,
+                  "tlsgpu: waiting for doorbell server instance %u (%u workgroups) on device %d "
+                  "to leave\n",
+                  inst.first, inst.second, sv->device);
+          noted = true;
+        }
+        if (t > g_shutdown_cap_ns)
+          return fail(TLSGPU_ETIMEOUT,
+                      "doorbell server instance %u on device %d still running after %llu ms",
+                      inst.first, sv->device, (unsigned long long)(g_shutdown_cap_ns / 1000000));
+      }
+    }
+    std::lock_guard<std::mutex> lk2(sv->mu);
+    sv->outstanding.clear();
   }
+  g_evp_shutdown.store(2, std::memory_order_release);
+  if (g_shutdown_verbose)
+    fprintf(stderr, "{\"evp_shutdown\": {\"instances_waited\": %u, \"ms\": %.3f}}\n", waited,
+            (mono_ns() - t0) * 1e-6);
+  print_doorbell_trace();
+  return TLSGPU_OK;
+}
+
+// Which exit hook is running (TLSGPU_CRASH_TRACE names it in a fault report):
+// 0 running, 1 the main thread's exit guard, 2 atexit, 3 library destructor.
+static volatile sig_atomic_t g_exit_phase = 0;
+
+// TLSGPU_CRASH_TRACE=1: a fatal signal prints the exit phase and a native
+// backtrace before the default action (Python's faulthandler, when enabled
+// after the library loaded, chains to this handler after its own dump).
+static void crash_report(int sig) {
+  char buf[192];
+  const int n = snprintf(buf, sizeof buf,
+                         "tlsgpu: fatal signal %d in exit phase %d (0 running, 1 main-thread exit "
+                         "guard, 2 atexit, 3 library destructor)\n",
+                         sig, (int)g_exit_phase);
+  if (n > 0) (void)!write(2, buf, (size_t)n);
+  void* fr[64];
+  backtrace_symbols_fd(fr, backtrace(fr, 64), 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+__attribute__((constructor)) static void install_crash_report() {
+  const char* v = getenv("TLSGPU_CRASH_TRACE");
+  if (!v || !*v || *v == '0') return;
+  struct sigaction sa;
+  memset(&sa, 0, sizeof sa);
+  sa.sa_handler = crash_report;
+  sa.sa_flags = SA_RESETHAND;
+  for (int sig : {SIGSEGV, SIGBUS, SIGABRT, SIGILL, SIGFPE}) sigaction(sig, &sa, nullptr);
+}
+
+static void evp_shutdown_at_exit() {
+  bool any = false;
+  for (EvpServer* sv : g_servers) any = any || (sv && sv->stop);
+  if (!any || tlsgpu_evp_shutdown() == TLSGPU_OK) return;
+  fprintf(stderr, "tlsgpu: %s; leaving before the runtime's teardown (exit status 70)\n",
+          tlsgpu_last_error());
+  fflush(stderr);
+  _exit(70);
+}
+
+// The main thread's exit guard: armed by the library constructor when it runs
+// on the main thread (LD_PRELOAD, or a dlopen from the main thread), so its
+// destructor runs among the main thread's thread-local destructors, first
+// thing in exit().
+namespace {
+struct MainExitGuard {
+  ~MainExitGuard() {
+    g_exit_phase = 1;
+    evp_shutdown_at_exit();
+  }
+};
+}  // namespace
+// The main thread's own staging set is destroyed among its thread-local
+// destructors at exit(), before the guard (constructed at load, so destroyed
+// later): drain there first.
+static void evp_shutdown_main_thread_exit() {
+  if ((pid_t)syscall(SYS_gettid) != getpid()) return;
+  g_exit_phase = 1;
+  evp_shutdown_at_exit();
+}
+__attribute__((constructor)) static void arm_main_exit_guard() {
+  if ((pid_t)syscall(SYS_gettid) != getpid()) return;
+  static thread_local MainExitGuard guard;
+  (void)&guard;
+}
+__attribute__((destructor)) static void evp_shutdown_at_unload() {
+  g_exit_phase = 3;
+  evp_shutdown_at_exit();
+}
+static void evp_shutdown_atexit() {
+  g_exit_phase = 2;
+  evp_shutdown_at_exit();
+}
+
+static void print_doorbell_trace() {
   for (EvpServer* sv : g_servers) {
     const uint64_t n = sv ? sv->tr_n.load() : 0;
     if (!n) continue;
@@ -1709,7 +1905,9 @@ static void servers_stop_at_exit() {
 
 // The server of EVP device k (created on first use when the doorbell is on).
 static EvpServer* evp_server(size_t k, tlsgpu_engine* e) {
-  if (!g_doorbell_groups || k >= (size_t)kMaxEvpDevices) return nullptr;
+  if (!g_doorbell_groups || k >= (size_t)kMaxEvpDevices ||
+      g_evp_shutdown.load(std::memory_order_acquire) != 0)
+    return nullptr;
   if (EvpServer* ready = g_ready_servers[k].load(std::memory_order_acquire)) return ready;
   std::lock_guard<std::mutex> lk(g_server_mu);
   if (g_servers[k]) return g_servers[k]->slots ? g_servers[k] : nullptr;
@@ -1746,7 +1944,7 @@ static EvpServer* evp_server(size_t k, tlsgpu_engine* e) {
   for (uint32_t i = sv->nslots; i-- > 0;) sv->free_slots.push_back(i);
   sv->slots = h;
   static std::once_flag once;
-  std::call_once(once, [] { atexit(servers_stop_at_exit); });
+  std::call_once(once, [] { atexit(evp_shutdown_atexit); });
   g_ready_servers[k].store(sv, std::memory_order_release);
   return sv;
 }
@@ -1758,7 +1956,16 @@ static bool server_ensure(EvpServer* sv) {
   if (now < sv->deadline_ns.load(std::memory_order_acquire)) return true;  // no lock per call
   std::lock_guard<std::mutex> lk(sv->mu);
   if (now < sv->deadline_ns.load(std::memory_order_relaxed)) return true;
+  // the shutdown contract copies `outstanding` under this lock: nothing is
+  // launched after it
+  if (g_evp_shutdown.load(std::memory_order_acquire) != 0) return false;
   if (hipSetDevice(sv->device) != hipSuccess) return false;
+  // forget instances that have left (the list stays a few entries long)
+  sv->outstanding.erase(std::remove_if(sv->outstanding.begin(), sv->outstanding.end(),
+                                       [sv](const std::pair<uint32_t, uint32_t>& i) {
+                                         return instance_left(sv, i.first, i.second);
+                                       }),
+                        sv->outstanding.end());
   ServerArgs a;
   a.slots = sv->d_slots;
   // poll the slots handed out so far, rounded up to 16 (so that a burst of new
@@ -1776,6 +1983,7 @@ static bool server_ensure(EvpServer* sv) {
   if (launch_evp_server(a, (int)g, sv->stream) != 0) return false;
   sv->launch_seq = a.seq;
   sv->last_g = g;
+  sv->outstanding.emplace_back(a.seq, g);
   sv->covered.store(std::min(g * (uint32_t)kWave, a.nslots), std::memory_order_release);
   // instances on one stream run one after another: this one starts when the
   // one queued before it ends (never before now) and polls for a lifetime
@@ -1838,6 +2046,17 @@ extern "C" int tlsgpu_evp_set_doorbell(unsigned groups, unsigned lifetime_ms) {
     if (sv) return fail(TLSGPU_EINVAL, "the doorbell server is already set up");
   g_doorbell_groups = groups;
   if (lifetime_ms) g_doorbell_ms = lifetime_ms;
+  return TLSGPU_OK;
+}
+
+extern "C" int tlsgpu_evp_doorbell_warm(void) {
+  if (!g_doorbell_groups || g_evp_shutdown.load(std::memory_order_acquire) != 0) return TLSGPU_OK;
+  for (size_t k = 0; k < evp_device_count() && k < (size_t)kMaxEvpDevices; k++) {
+    tlsgpu_engine* e = evp_engine(k);
+    EvpServer* sv = e ? evp_server(k, e) : nullptr;
+    if (sv && !server_ensure(sv) && g_evp_shutdown.load() == 0)
+      return fail(TLSGPU_EHIP, "doorbell server launch on EVP device %zu", k);
+  }
   return TLSGPU_OK;
 }
 
@@ -1974,16 +2193,40 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
       slot->sessions = (uint64_t)st->sess->d_sess;
       slot->gcm_tables = (uint64_t)st->sess->d_gcm;
       slot->key_id = st->key_id;
-      if (!server_ensure(sv)) return -1;
+      if (!server_ensure(sv)) {
+        if (g_evp_shutdown.load(std::memory_order_acquire) == 0) return -1;  // launch failed
+        goto launched;  // shutting down: nothing was posted
+      }
       const uint32_t n = ++*seq;
-      __atomic_store_n(&slot->post, n, __ATOMIC_RELEASE);
       const uint64_t t0 = mono_ns();
-      for (uint64_t spins = 1; __atomic_load_n(&slot->done, __ATOMIC_ACQUIRE) != n; spins++) {
-        __builtin_ia32_pause();
-        if ((spins & 127) == 0) {
-          const uint64_t waited = mono_ns() - t0;
-          if (waited > 10000000000ull) return -1;  // 10 s: the device is gone
-          if (waited > g_doorbell_yield_ns) sched_yield();  // let other callers post
+      {
+        if (g_test_post_delay_us) usleep(g_test_post_delay_us);  // test hook: a descheduled caller
+        __atomic_store_n(&slot->post, n, __ATOMIC_RELEASE);
+        for (uint64_t spins = 1; __atomic_load_n(&slot->done, __ATOMIC_ACQUIRE) != n; spins++) {
+          __builtin_ia32_pause();
+          if ((spins & 127) == 0) {
+            // the instance the post was meant for may have left before the
+            // post landed (this thread descheduled between server_ensure and
+            // the store for more than half a lifetime): past the deadline,
+            // relaunch — the new instance picks the post up
+            const int sd = g_evp_shutdown.load(std::memory_order_acquire);
+            if (sd == 0 && !server_ensure(sv) && g_evp_shutdown.load() == 0) return -1;
+            if (sd == 2) {  // drained: no instance will ever serve it
+              if (__atomic_load_n(&slot->done, __ATOMIC_ACQUIRE) == n) break;
+              t_slots.slot[st->evp_dev] = -1;  // this thread posts no more
+              goto launched;
+            }
+            const uint64_t waited = mono_ns() - t0;
+            if (waited > 10000000000ull) {  // 10 s: the device is gone
+              // the post stays outstanding: retire the slot (never handed out
+              // again) and leave the staging buffer to the job that may still
+              // run (never freed, never reused)
+              t_slots.slot[st->evp_dev] = -1;
+              stg->abandon();
+              return -1;
+            }
+            if (waited > g_doorbell_yield_ns) sched_yield();  // let other callers post
+          }
         }
       }
       sv->jobs.fetch_add(1, std::memory_order_relaxed);
@@ -2017,6 +2260,7 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
       return 1;
     }
   }
+launched:
   BatchArgs a = {};
   a.sessions = st->sess->d_sess;
   a.gcm_tables = st->sess->d_gcm;

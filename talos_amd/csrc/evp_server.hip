@@ -215,15 +215,17 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
     if (((op >> 8) == 10 || (op >> 8) == 14) && sid < a.n_sessions && key != 0)  // GCM: LDS copy
       a.sessions = reinterpret_cast<const DevSession*>(s_lds + SRV_SESS_OFF) - sid;
     const bool hit = key != 0 && key == cached_key;
-    const uint32_t prev_key = cached_key;  // a ChaCha job leaves the GCM tables alone
-    cached_key = key;
+    // the table cache is keyed only on a job that really loaded (or kept)
+    // its session's tables; a job rejected by the session check before the
+    // load leaves LDS without valid tables; a ChaCha job leaves
+    // the GCM tables alone
     switch (op) {
-      case 10 << 8: gcm_raw_job<false, 10>(a, 0, hit); break;
-      case (10 << 8) | 1: gcm_raw_job<true, 10>(a, 0, hit); break;
-      case 14 << 8: gcm_raw_job<false, 14>(a, 0, hit); break;
-      case (14 << 8) | 1: gcm_raw_job<true, 14>(a, 0, hit); break;
-      case 20 << 8: srv_chacha_job<false>(a, c->job); cached_key = prev_key; break;
-      case (20 << 8) | 1: srv_chacha_job<true>(a, c->job); cached_key = prev_key; break;
+      case 10 << 8: cached_key = gcm_raw_job<false, 10>(a, 0, hit) ? key : 0; break;
+      case (10 << 8) | 1: cached_key = gcm_raw_job<true, 10>(a, 0, hit) ? key : 0; break;
+      case 14 << 8: cached_key = gcm_raw_job<false, 14>(a, 0, hit) ? key : 0; break;
+      case (14 << 8) | 1: cached_key = gcm_raw_job<true, 14>(a, 0, hit) ? key : 0; break;
+      case 20 << 8: srv_chacha_job<false>(a, c->job); break;
+      case (20 << 8) | 1: srv_chacha_job<true>(a, c->job); break;
       default:  // not a job this server runs (the host never posts one)
         if (threadIdx.x == 0) a.status[0] = TLSGPU_REC_PUBLIC_INVALID;
         cached_key = 0;

@@ -43,9 +43,11 @@ namespace tg {
 // flight except the tag / status of wave 0, so the persistent EVP server
 // (evp_server.hip) can start its next job after one more barrier.
 // tables_loaded: the session's GCM tables are already in LDS (the server's
-// previous job had the same installed key).
+// previous job had the same installed key).  Returns whether the LDS holds
+// the job's session tables afterwards (false: the session check failed before
+// any table was loaded, so the server must not key its table cache on it).
 template <bool SEAL, int ROUNDS, bool TLS = false>
-__device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
+__device__ __forceinline__ bool gcm_raw_job(const BatchArgs& a, uint32_t r,
                                             bool tables_loaded = false) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -63,7 +65,7 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
     if (!TLS && threadIdx.x == 0 && !(in_range && kind >= TLSGPU_AES_128_GCM &&
                                        kind <= TLSGPU_CHACHA20_POLY1305_OLD))
       a.status[r] = TLSGPU_REC_PUBLIC_INVALID;
-    return;
+    return false;
   }
   if (!tables_loaded) load_session_tables<kThreads>(a.gcm_tables + sid);
   __syncthreads();
@@ -74,7 +76,7 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
   if (TLS) {
     // every wave parses (same descriptor): a publicly invalid record returns
     // from all of them before the barrier below
-    if (!parse_tls<SEAL>(load_desc(D), S, a.in, a.out, a.status + r, lane, rc)) return;
+    if (!parse_tls<SEAL>(load_desc(D), S, a.in, a.out, a.status + r, lane, rc)) return true;
   } else {
     parse_raw<SEAL>(*J, S, rc);
   }
@@ -147,7 +149,7 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
   }
   if (lane == 0 && wave < nwork) part_y[wave] = make_uint4(y[0], y[1], y[2], y[3]);
   __syncthreads();
-  if (wave != 0) return;
+  if (wave != 0) return true;
   TG_JOB_MARK(5);
   uint32_t t[4] = {0, 0, 0, 0};
   if (lane == 0) {
@@ -160,6 +162,7 @@ __device__ __forceinline__ void gcm_raw_job(const BatchArgs& a, uint32_t r,
   const uint32_t ek0[4] = {ekv.x, ekv.y, ekv.z, ekv.w};
   TG_JOB_MARK(6);
   gcm_tag<SEAL>(rc, t, ek0, S, a.status + r, lane);
+  return true;
 }
 
 }  // namespace tg

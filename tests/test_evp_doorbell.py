@@ -10,9 +10,10 @@ server runs, across server relaunches (short lifetime), and the server must
 stop by itself when the calls stop.  ChaCha jobs run on the server's wave 0
 (chacha_wave.h) between GCM jobs, whose LDS table cache they must leave
 intact; draft-suite ChaCha contexts take the launched path in the same
-threads.  Inputs up to 4 KiB travel in the slot's input area (read with the
-slot): the lengths cover both sides of that limit for seal (4,096 B of
-plaintext) and open (4,080 + 16 B of ciphertext and tag)."""
+threads.  A GCM job's input up to 4 KiB is staged into LDS by the server's
+idle waves 12-15 while waves 0-1 parse: the lengths cover both sides of that
+limit for seal (4,096 B of plaintext) and open (4,080 + 16 B of ciphertext
+and tag)."""
 import os
 import subprocess
 import sys
@@ -24,6 +25,7 @@ from conftest import ROOT
 pytestmark = pytest.mark.gpu
 
 _CHILD = r"""
+import faulthandler; faulthandler.enable()
 import os, random, sys, threading, time
 sys.path.insert(0, sys.argv[1]); sys.path.insert(0, os.path.join(sys.argv[1], "oracle"))
 import talos_amd as ta, pyoracle as po
@@ -73,7 +75,7 @@ print("OK", jobs, launches)
 
 @pytest.mark.parametrize("threads", [1, 12])
 def test_evp_doorbell_matches_oracle(threads):
-    env = dict(os.environ, TLSGPU_EVP_DOORBELL="4", TLSGPU_EVP_DOORBELL_MS="40")
+    env = dict(os.environ, TLSGPU_EVP_DOORBELL="4", TLSGPU_EVP_DOORBELL_MS="40", TLSGPU_CRASH_TRACE="1")
     env.pop("TLSGPU_EVP_BATCH_US", None)
     r = subprocess.run([sys.executable, "-c", _CHILD, ROOT, str(threads)], env=env,
                        capture_output=True, text=True, timeout=110)
@@ -81,6 +83,7 @@ def test_evp_doorbell_matches_oracle(threads):
 
 
 _BUSY_CHILD = r"""
+import faulthandler; faulthandler.enable()
 import os, sys, threading, time
 sys.path.insert(0, sys.argv[1])
 import talos_amd as ta
@@ -114,7 +117,7 @@ def test_evp_doorbell_busy_workgroup_yields_to_next_instance():
     holds the next instance, queued behind it on the same stream, off the GPU,
     and a thread whose workgroup has already exited waits for the busy thread
     to pause.  The late thread's calls must stay far below the 10 s timeout."""
-    env = dict(os.environ, TLSGPU_EVP_DOORBELL="2", TLSGPU_EVP_DOORBELL_MS="20")
+    env = dict(os.environ, TLSGPU_EVP_DOORBELL="2", TLSGPU_EVP_DOORBELL_MS="20", TLSGPU_CRASH_TRACE="1")
     env.pop("TLSGPU_EVP_BATCH_US", None)
     r = subprocess.run([sys.executable, "-c", _BUSY_CHILD, ROOT], env=env,
                        capture_output=True, text=True, timeout=100)

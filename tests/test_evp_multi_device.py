@@ -20,6 +20,7 @@ from conftest import ROOT
 pytestmark = pytest.mark.gpu
 
 _CHILD = r"""
+import faulthandler; faulthandler.enable()
 import os, random, sys, threading
 sys.path.insert(0, sys.argv[1]); sys.path.insert(0, os.path.join(sys.argv[1], "oracle"))
 import talos_amd as ta, pyoracle as po
@@ -66,7 +67,7 @@ print("OK", st, b, j)
 
 @pytest.mark.parametrize("batch_us", [None, "200"])
 def test_evp_two_devices(batch_us):
-    env = dict(os.environ, TLSGPU_DEVICES="0,0")
+    env = dict(os.environ, TLSGPU_DEVICES="0,0", TLSGPU_CRASH_TRACE="1")
     env.pop("TLSGPU_DEVICE", None)
     if batch_us:
         env["TLSGPU_EVP_BATCH_US"] = batch_us
