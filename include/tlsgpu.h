@@ -458,6 +458,11 @@ int tlsgpu_evp_doorbell_stats(uint64_t *jobs, uint64_t *launches);
  * from an atexit handler and from its destructor; an application that tears
  * the runtime down itself (hipDeviceReset) calls it before. */
 int tlsgpu_evp_doorbell_warm(void);
+/* Test support: the device image of one session as EVP_AEAD_CTX_init builds it
+ * on the host (DevSession, 1 KiB, then the GCM tables: basis, Shoup tables of
+ * H^1..H^65, bitsliced masks; zero for ChaCha) into out[0..n), n >= 27,392.
+ * tests/test_session_image.py checks it against the device install kernel. */
+int tlsgpu_session_image(const tlsgpu_session_params *p, uint8_t *out, size_t n);
 int tlsgpu_evp_shutdown(void);
 /* Test support.  tlsgpu_evp_context_slot: the session table and slot that hold
  * a live EVP context's device key material.  tlsgpu_sessions_debug_read: after

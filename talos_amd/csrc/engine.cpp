@@ -269,6 +269,8 @@ extern "C" int tlsgpu_sessions_install(tlsgpu_sessions* t, uint32_t first, uint3
   int rc = err == hipSuccess
                ? launch_session_install(t->d_sess, t->d_gcm, d_params, first, n, t->eng->stream)
                : -1;
+  // the raw keys do not outlive the install in device memory
+  (void)hipMemsetAsync(d_params, 0, sizeof(tlsgpu_session_params) * n, t->eng->stream);
   hipError_t serr = hipStreamSynchronize(t->eng->stream);
   (void)hipFree(d_params);
   if (err != hipSuccess || rc != 0 || serr != hipSuccess)
@@ -421,6 +423,11 @@ static uint32_t g_pws = []() {
   return *v == '0' ? 1u : 2u;
 }();
 
+static const bool g_fused = [] {
+  const char* v = getenv("TLSGPU_FUSED");
+  return !(v && *v == '0');
+}();
+
 // bounds: {in_bytes, out_bytes} of a caller's TLS batch (checked by a pre-pass
 // that hands the kernels a sanitized copy of the descriptors), or null for
 // descriptors the engine built itself (raw EVP jobs, wire framing).
@@ -476,6 +483,17 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   a.hy_flags = sane_hy_flags(g_hy_flags, impl);
   const bool gcm_pre = impl != TLSGPU_GCM_TTABLE && impl != TLSGPU_GCM_SPLIT &&
                        (have[TLSGPU_AES_128_GCM] || have[TLSGPU_AES_256_GCM]);
+  // Fused (round 5): one queue kernel is the batch's only kernel — one AES key
+  // size installed, no ChaCha, the hints rule out the per-wave-session kernel,
+  // and they decide the variant (TLSGPU_HINT_NO_SHORT_RECORDS: no-pack, else
+  // the pack variant, which also runs long records) — so it checks bounds,
+  // writes the initial statuses and computes the per-record constants of its
+  // own records in its prologue: no check_record_bounds, no gcm_prep_kernel, no
+  // checked-descriptor copy, no variant that exits at once (TLSGPU_FUSED=0
+  // keeps the launch sequence with the device-side selection).
+  const bool fused = g_fused && bounds && impl == TLSGPU_GCM_QUEUE && a.pws == 1 &&
+                     (have[TLSGPU_AES_128_GCM] != have[TLSGPU_AES_256_GCM]) &&
+                     !have[TLSGPU_CHACHA20_POLY1305] && !have[TLSGPU_CHACHA20_POLY1305_OLD];
   // per-stream scratch: [RecPre x n (queue kernels) | ctl_bytes control words |
   // checked descriptors x n].  Control words per key size k (0: AES-128, 1:
   // AES-256): selection words (kSelSlots x 64 B) at 1024 k, then one uint32
@@ -484,11 +502,11 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   static_assert(kSelSlots * kSelWords * 4 <= 1024, "selection words exceed their slot");
   const size_t cnt_bytes = ((size_t)groups * 4 + 255) & ~(size_t)255;
   const size_t ctl_bytes = 2048 + 2 * cnt_bytes;
-  const size_t pre_bytes = gcm_pre ? sizeof(RecPre) * (size_t)n + ctl_bytes : 0;
+  const size_t pre_bytes = gcm_pre ? sizeof(RecPre) * (size_t)n + (fused ? 0 : ctl_bytes) : 0;
   uint8_t* scratch = nullptr;
   uint8_t* pool_scratch = nullptr;
   if (pre_bytes || bounds) {
-    const size_t sbytes = pre_bytes + (bounds ? sizeof(tlsgpu_record) * (size_t)n : 0);
+    const size_t sbytes = pre_bytes + (bounds && !fused ? sizeof(tlsgpu_record) * (size_t)n : 0);
     if (g_pre_pool) {  // diagnostic only (DESIGN.md §4.1 pool scratch): stream-ordered pool
       if (hipMallocAsync((void**)&scratch, sbytes, s) != hipSuccess) scratch = nullptr;
       pool_scratch = scratch;
@@ -501,10 +519,14 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   uint8_t* ctl = nullptr;
   if (gcm_pre) {
     pre = reinterpret_cast<RecPre*>(scratch);
-    ctl = reinterpret_cast<uint8_t*>(pre + n);
+    ctl = fused ? nullptr : reinterpret_cast<uint8_t*>(pre + n);
   }
   uint8_t* const ctl_zero = impl == TLSGPU_GCM_QUEUE ? ctl : nullptr;
-  if (bounds) {
+  if (fused) {
+    a.fused = 1;
+    a.in_bytes = bounds->in_bytes;
+    a.out_bytes = bounds->out_bytes;
+  } else if (bounds) {
     // one setup launch: sanitized descriptors, every record's initial status
     // (records whose session is empty / invalid keep TLSGPU_REC_PUBLIC_INVALID)
     // and the zeroed control words
@@ -537,7 +559,7 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
     } else if (impl == TLSGPU_GCM_SPLIT) {
       rc = launch_gcm_split(a, seal, rounds, s);
     } else {
-      rc = launch_gcm_prep(a, pre, seal, rounds, s);
+      rc = fused ? 0 : launch_gcm_prep(a, pre, seal, rounds, s);
       if (rc == 0) {
         if (impl == TLSGPU_GCM_QUEUE)
           rc = launch_gcm_queue(a, pre, seal, rounds, groups, s);
@@ -1330,6 +1352,51 @@ struct Staging {
   uint8_t* h_buf = nullptr;
   uint8_t* h_dev = nullptr;  // h_buf as the device addresses it (zero-copy calls)
   size_t cap = 0;
+  // pinned key areas (round 5): EVP_AEAD_CTX_init builds the slot's image here
+  // (session_host.cpp) and one kernel copies it into the slot; `dirty` until
+  // the copy is known done (its event), then zeroed (explicit_bzero analogue)
+  struct KeyArea {
+    uint8_t* h = nullptr;
+    uint8_t* dev = nullptr;
+    hipEvent_t ev = nullptr;
+    bool dirty = false;
+  };
+  static constexpr int kKeyAreas = 4;
+  static constexpr size_t kKeyAreaBytes = sizeof(DevSession) + sizeof(DevGcmTables);
+  KeyArea keys[kKeyAreas];
+  uint32_t key_next = 0;
+  // the next key area (waiting for and zeroing its previous image if needed)
+  KeyArea* take_key_area() {
+    KeyArea& k = keys[key_next++ % kKeyAreas];
+    if (!k.h) {
+      if (hipHostMalloc((void**)&k.h, kKeyAreaBytes, hipHostMallocDefault) != hipSuccess ||
+          hipHostGetDevicePointer((void**)&k.dev, k.h, 0) != hipSuccess ||
+          hipEventCreateWithFlags(&k.ev, hipEventDisableTiming) != hipSuccess) {
+        if (k.h) (void)hipHostFree(k.h);
+        k.h = nullptr;
+        return nullptr;
+      }
+    }
+    if (k.dirty) {
+      if (hipEventSynchronize(k.ev) != hipSuccess) return nullptr;
+      explicit_bzero(k.h, kKeyAreaBytes);
+      k.dirty = false;
+    }
+    return &k;
+  }
+  // zero every key area whose copy has finished (no wait)
+  void sweep_key_areas() {
+    for (KeyArea& k : keys)
+      if (k.dirty && hipEventQuery(k.ev) == hipSuccess) {
+        explicit_bzero(k.h, kKeyAreaBytes);
+        k.dirty = false;
+      }
+  }
+  bool any_dirty_key_area() const {
+    for (const KeyArea& k : keys)
+      if (k.dirty) return true;
+    return false;
+  }
   ~Staging() {
     if (device >= 0) (void)hipSetDevice(device);  // the buffers' and the event's device
     if (d_buf) (void)hipFree(d_buf);
@@ -1422,6 +1489,18 @@ static hipEvent_t slot_event(tlsgpu_sessions* t, uint32_t slot) {
 // first call waits for that event on the device (gpu_call_impl).  A
 // connection's key install at ChangeCipherSpec (t1_enc.c:444-495) then costs
 // no device round trip of its own.
+// Round 5 (hygiene): the image is built on the
+// calling thread (session_host.cpp: key schedule, H, the GHASH power tables —
+// the ~25 µs of one wave install_session_arg spent) into a pinned key area,
+// and one short kernel copies it into the slot: no key material in kernel
+// arguments, and the area is zeroed once its copy has finished
+// (sweep_key_areas after the thread's next synchronised call, or when the
+// area is reused).  TLSGPU_EVP_DEVICE_INSTALL=1 keeps the device install.
+static const bool g_device_install = [] {
+  const char* v = getenv("TLSGPU_EVP_DEVICE_INSTALL");
+  return v && *v && *v != '0';
+}();
+
 static int install_one(tlsgpu_sessions* t, uint32_t slot, const tlsgpu_session_params& p,
                        hipEvent_t* installed) {
   if (!valid_params(p) || slot >= t->capacity) return fail(TLSGPU_EINVAL, "bad session");
@@ -1429,9 +1508,24 @@ static int install_one(tlsgpu_sessions* t, uint32_t slot, const tlsgpu_session_p
   if (!stg || !stg->ensure(t->eng->device, 16)) return fail(TLSGPU_ENOMEM, "staging");
   const hipEvent_t ev = slot_event(t, slot);  // on the slot's device (ensure set it)
   if (!ev) return fail(TLSGPU_EHIP, "slot event");
-  const bool ok = hipStreamWaitEvent(stg->stream, ev, 0) == hipSuccess &&
-                  launch_session_install_arg(t->d_sess, t->d_gcm, p, slot, stg->stream) == 0 &&
-                  hipEventRecord(ev, stg->stream) == hipSuccess;
+  bool ok;
+  if (g_device_install) {
+    ok = hipStreamWaitEvent(stg->stream, ev, 0) == hipSuccess &&
+         launch_session_install_arg(t->d_sess, t->d_gcm, p, slot, stg->stream) == 0 &&
+         hipEventRecord(ev, stg->stream) == hipSuccess;
+  } else {
+    Staging::KeyArea* ka = stg->take_key_area();
+    if (!ka) return fail(TLSGPU_ENOMEM, "key area");
+    auto* img_s = reinterpret_cast<DevSession*>(ka->h);
+    auto* img_t = reinterpret_cast<DevGcmTables*>(ka->h + sizeof(DevSession));
+    const bool tables = host_session_image(p, img_s, img_t);
+    ka->dirty = true;
+    ok = hipStreamWaitEvent(stg->stream, ev, 0) == hipSuccess &&
+         launch_upload_session(ka->dev, t->d_sess + slot, t->d_gcm + slot,
+                               tables ? kGcmTableUploadBytes : 0u, stg->stream) == 0 &&
+         hipEventRecord(ka->ev, stg->stream) == hipSuccess &&
+         hipEventRecord(ev, stg->stream) == hipSuccess;
+  }
   if (!ok) return fail(TLSGPU_EHIP, "session install: %s", hipGetErrorString(hipGetLastError()));
   *installed = ev;
   std::lock_guard<std::mutex> lk(t->mu);
@@ -1451,10 +1545,11 @@ static void scrub_slot(tlsgpu_sessions* t, uint32_t slot) {
   // after the slot's install (a context cleaned up before any call, from
   // another thread, may still have its install queued on another stream)
   if (ev && hipStreamWaitEvent(stg->stream, ev, 0) == hipSuccess &&
-      hipMemsetAsync(t->d_sess + slot, 0, sizeof(DevSession), stg->stream) == hipSuccess &&
-      hipMemsetAsync(t->d_gcm + slot, 0, sizeof(DevGcmTables), stg->stream) == hipSuccess &&
-      hipEventRecord(ev, stg->stream) == hipSuccess)
+      launch_scrub_session(t->d_sess + slot, t->d_gcm + slot, stg->stream) == 0 &&
+      hipEventRecord(ev, stg->stream) == hipSuccess) {
+    stg->sweep_key_areas();
     return;
+  }
   (void)hipSetDevice(t->eng->device);  // fall back to the synchronous form
   (void)hipDeviceSynchronize();
   (void)hipMemset(t->d_sess + slot, 0, sizeof(DevSession));
@@ -2279,6 +2374,7 @@ launched:
       hipEventRecord(stg->done, s) != hipSuccess || !event_spin(stg->done))
     return -1;
   st->install_pending.store(false, std::memory_order_release);  // done before this call's work
+  if (stg->any_dirty_key_area()) stg->sweep_key_areas();  // this context's image, copied by now
   const int32_t status = *reinterpret_cast<const int32_t*>(h + o_status);
   if (status < 0) {  // the kernel's zero-fill of max_out_len bytes (evp_aead.c:137-143)
     if (max_out_len) memset(out, 0, max_out_len);

@@ -301,13 +301,47 @@ __device__ void gcm_pair_hy(const RecCtx (&rc)[2], const RecPre* pa, const RecPr
 
 namespace tg {
 
+// The bounds rule of check_record_bounds (session_kernels.hip): the record's
+// input span and output span lie inside the caller's buffers.
+__device__ __forceinline__ bool rec_in_bounds(const tlsgpu_record& d, const DevSession* S,
+                                              uint64_t in_bytes, uint64_t out_bytes, bool seal) {
+  const uint64_t eiv = as_const(&S->nonce_in_record)[0] ? 8u : 0u, tag = as_const(&S->tag_len)[0];
+  const uint64_t len = d.len_type & 0xFFFFFFu;
+  const uint64_t out_len = seal ? len + eiv + tag : (len >= eiv + tag ? len - eiv - tag : 0);
+  return !(d.in_off > in_bytes || len > in_bytes - d.in_off || d.out_off > out_bytes ||
+           out_len > out_bytes - d.out_off);
+}
+
+// RecPre written by this kernel's own prologue (fused): vector loads (the
+// scalar cache, shared by neighbouring CUs, could hold a line of it from
+// before the prologue's stores), made wave-uniform.
+__device__ __forceinline__ RecConsts rec_consts_fresh(const RecPre* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  const uint4 a = q[0], b = q[1], c = q[2];
+  RecConsts rc;
+  rc.ek0[0] = __builtin_amdgcn_readfirstlane(a.x);
+  rc.ek0[1] = __builtin_amdgcn_readfirstlane(a.y);
+  rc.ek0[2] = __builtin_amdgcn_readfirstlane(a.z);
+  rc.ek0[3] = __builtin_amdgcn_readfirstlane(a.w);
+  rc.k1a = __builtin_amdgcn_readfirstlane(b.x);
+  rc.k1b = __builtin_amdgcn_readfirstlane(b.y);
+  rc.k2[0] = __builtin_amdgcn_readfirstlane(b.z);
+  rc.k2[1] = __builtin_amdgcn_readfirstlane(b.w);
+  rc.k2[2] = __builtin_amdgcn_readfirstlane(c.x);
+  rc.k2[3] = __builtin_amdgcn_readfirstlane(c.y);
+  return rc;
+}
+
 template <bool SEAL, int ROUNDS, int NB = 4>
 __device__ __forceinline__ void hy_tt_record(const BatchArgs& a, const RecPre* __restrict__ pre,
                                              uint32_t r, const DevSession* __restrict__ S,
                                              uint32_t lane, uint32_t laneoff, const GhLane& gl) {
   const tlsgpu_record* D = reinterpret_cast<const tlsgpu_record*>(a.descs);
   RecCtx rc;
-  if (!parse_tls<SEAL>(load_desc(D + r), S, a.in, a.out, a.status + r, lane, rc)) return;
+  const tlsgpu_record d = load_desc(D + r);
+  // fused: an out-of-bounds record's status was written by the prologue
+  if (a.fused && !rec_in_bounds(d, S, a.in_bytes, a.out_bytes, SEAL)) return;
+  if (!parse_tls<SEAL>(d, S, a.in, a.out, a.status + r, lane, rc)) return;
 #ifdef TG_BS16  // packed bitsliced path (experimental build)
   if (a.bs16_min != 0 && rc.n >= a.bs16_min && rc.n <= 16384u &&
       ((((uintptr_t)rc.src) | ((uintptr_t)rc.dst)) & 15) == 0) {
@@ -315,7 +349,7 @@ __device__ __forceinline__ void hy_tt_record(const BatchArgs& a, const RecPre* _
     return;
   }
 #endif
-  const RecConsts rcc = rec_consts_of(pre + r);
+  const RecConsts rcc = rec_consts_fresh(pre + r);
   gcm_record_x4<SEAL, ROUNDS, NB>(rc, S, rcc, a.status + r, lane, laneoff, gl, a.dbg);
 }
 
@@ -540,6 +574,101 @@ __device__ __forceinline__ SelSums sel_sums(const uint32_t* sel) {
   return t;
 }
 
+// Per-record constants of one record (the body of gcm_prep_kernel; rec_consts
+// in gcm_device.h): E_K(J0), the round-1 columns 0, 1 and the round-2
+// constants.  T0 / T1 / SB: Te0, Te1 and S-box lookups of byte b of w.
+template <bool SEAL, int ROUNDS, typename RK, typename T0F, typename T1F, typename SBF>
+__device__ __forceinline__ RecPre rec_pre(const uint32_t j0[4], RK rk, T0F T0, T1F T1, SBF SB) {
+  uint32_t s[4] = {j0[0] ^ rk[0], j0[1] ^ rk[1], j0[2] ^ rk[2], j0[3] ^ rk[3]};
+#pragma unroll
+  for (int rr = 1; rr < ROUNDS; rr++) {
+    uint32_t t[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+      t[c] = T0(s[c], 0) ^ T1(s[(c + 1) & 3], 1) ^
+             rotl32(T0(s[(c + 2) & 3], 2) ^ T1(s[(c + 3) & 3], 3), 16) ^ rk[4 * rr + c];
+#pragma unroll
+    for (int c = 0; c < 4; c++) s[c] = t[c];
+  }
+  RecPre o;
+#pragma unroll
+  for (int c = 0; c < 4; c++)
+    o.ek0[c] = (SB(s[c], 0) | (SB(s[(c + 1) & 3], 1) << 8) | (SB(s[(c + 2) & 3], 2) << 16) |
+                (SB(s[(c + 3) & 3], 3) << 24)) ^ rk[4 * ROUNDS + c];
+  const uint32_t s0 = j0[0] ^ rk[0], s1 = j0[1] ^ rk[1], s2 = j0[2] ^ rk[2];
+  uint32_t k1[4];
+  k1[0] = T0(s0, 0) ^ T1(s1, 1) ^ rotl32(T0(s2, 2), 16) ^ rk[4];
+  k1[1] = T0(s1, 0) ^ T1(s2, 1) ^ rotl32(T1(s0, 3), 16) ^ rk[5];
+  k1[2] = T0(s2, 0) ^ rotl32(T0(s0, 2) ^ T1(s1, 3), 16) ^ rk[6];
+  k1[3] = T1(s0, 1) ^ rotl32(T0(s1, 2) ^ T1(s2, 3), 16) ^ rk[7];
+  const uint32_t v0 = rk[3];
+  const uint32_t c2 = k1[2] ^ T1(v0, 1), c3 = k1[3] ^ T0(v0, 0);  // round-1 columns 2, 3
+  o.k1a = k1[0];
+  o.k1b = k1[1];
+  o.k2[0] = rotl32(T0(c2, 2) ^ T1(c3, 3), 16) ^ rk[8];
+  o.k2[1] = T1(c2, 1) ^ rotl32(T0(c3, 2), 16) ^ rk[9];
+  o.k2[2] = T0(c2, 0) ^ T1(c3, 1) ^ rk[10];
+  o.k2[3] = T0(c3, 0) ^ rotl32(T1(c2, 3), 16) ^ rk[11];
+  o.sb2[0] = SB(c2, 0) | (SB(c2, 1) << 8) | (SB(c2, 2) << 16) | (SB(c2, 3) << 24);
+  o.sb2[1] = SB(c3, 0) | (SB(c3, 1) << 8) | (SB(c3, 2) << 16) | (SB(c3, 3) << 24);
+  return o;
+}
+
+// Fused prologue (round 5): what check_record_bounds
+// and gcm_prep_kernel did in two launches before this kernel, for the
+// workgroup's own records [rlo, rhi), one thread per record: the bounds check
+// and initial status (TLSGPU_REC_OUT_OF_BOUNDS / _PUBLIC_INVALID, the status of
+// a record no kernel takes), and the per-record constants of every record this
+// kernel will run, into `pre`.  The T-tables are already in LDS (fill_aes_lds:
+// row x = 32 bank copies of Te0[x], then 32 of Te1[x]).  Only used when this
+// kernel is the batch's only one (one AES key size installed, no ChaCha, no
+// pack / per-wave-session variants: engine.cpp run_batch), so every status
+// write here precedes this workgroup's own final one (barrier below).
+template <bool SEAL, int ROUNDS, int NT>
+__device__ void fused_prologue(const BatchArgs& a, RecPre* __restrict__ pre, uint32_t rlo,
+                               uint32_t rhi) {
+  const tlsgpu_record* D = reinterpret_cast<const tlsgpu_record*>(a.descs);
+  const uint32_t* te = reinterpret_cast<const uint32_t*>(s_lds + AES_OFF);
+  const uint32_t l32 = threadIdx.x & 31;
+  auto T0 = [&](uint32_t w, int b) { return te[(((w >> (8 * b)) & 0xFF) << 6) | l32]; };
+  auto T1 = [&](uint32_t w, int b) { return te[(((w >> (8 * b)) & 0xFF) << 6) | 32 | l32]; };
+  auto SB = [&](uint32_t w, int b) { return (T0(w, b) >> 8) & 0xFF; };
+  for (uint32_t base = rlo; base < rhi; base += NT) {  // wave-uniform trip count
+    const uint32_t r = base + threadIdx.x;
+    bool mine = false;
+    tlsgpu_record d = {};
+    const DevSession* S = nullptr;
+    if (r < rhi) {
+      d = D[r];
+      int32_t st = TLSGPU_REC_PUBLIC_INVALID;
+      if (d.session < a.n_sessions) {
+        S = a.sessions + d.session;
+        if (!rec_in_bounds(d, S, a.in_bytes, a.out_bytes, SEAL)) st = TLSGPU_REC_OUT_OF_BOUNDS;
+        else mine = is_gcm(S->kind) && (int)S->rounds == ROUNDS;
+      }
+      a.status[r] = st;
+    }
+    const uint32_t sid0 = __builtin_amdgcn_readfirstlane(mine ? d.session : 0xFFFFFFFFu);
+    const bool uniform = !__any(mine && d.session != sid0);
+    if (!mine) continue;
+    uint32_t j0[4];
+    j0[0] = *reinterpret_cast<const uint32_t*>(S->fixed_nonce);
+    j0[1] = j0[2] = 0;
+    j0[3] = 0x01000000u;
+    if (SEAL) {
+      j0[1] = bswap32((uint32_t)(d.seq >> 32));
+      j0[2] = bswap32((uint32_t)d.seq);
+    } else if ((d.len_type & 0xFFFFFFu) >= 8) {
+      const uint8_t* p = a.in + d.in_off;
+      j0[1] = load_u32_bytes(p);
+      j0[2] = load_u32_bytes(p + 4);
+    }
+    pre[r] = uniform ? rec_pre<SEAL, ROUNDS>(j0, as_const(a.sessions[sid0].rk), T0, T1, SB)
+                     : rec_pre<SEAL, ROUNDS>(j0, S->rk, T0, T1, SB);
+  }
+  __threadfence_block();  // the statuses and constants before this workgroup's main loop
+}
+
 // NT threads, the first BSW waves bitsliced (0: a pure T-table queue kernel,
 // 16 waves of <= 128 VGPRs), T-table waves NB blocks wide; B16W > 0: the first
 // B16W waves take the packed bitsliced role (hy_b16_record, one per SIMD for
@@ -554,7 +683,9 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
     const SelSums f = sel_sums(a.sel);
     if (pws_selected(a.pws, f.runs, f.recs)) return;
     if ((a.pack != 0 && f.pack != 0) != PACK) return;
-  } else if (PACK) {
+  } else if (PACK != (a.fused != 0 && a.pack != 0)) {
+    // no selection words: the no-pack variant, or (fused, packs allowed by the
+    // hints) only the pack variant is launched
     return;
   }
   const uint32_t lane = threadIdx.x & 63;
@@ -573,6 +704,10 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
 
   const uint32_t rlo = blockIdx.x * a.records_per_group;
   const uint32_t rhi = min(a.n, rlo + a.records_per_group);
+  if (BSW == 0 && B16W == 0 && a.fused) {
+    __syncthreads();  // the T-tables
+    fused_prologue<SEAL, ROUNDS, NT>(a, const_cast<RecPre*>(pre), rlo, rhi);
+  }
   uint32_t cur = 0xFFFFFFFFu;
   uint32_t pos = rlo;
   // short-record packs (gcm_pack): T-table waves only, planned per run in LDS
@@ -617,7 +752,10 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
         for (uint32_t c = wave * kWave; c < run_len; c += NT) {  // ballot compaction per wave
           const uint32_t t = c + lane;
           const uint32_t nd = t < run_len ? pack_need<SEAL>(D[pos + t].len_type, tag_len) : 0u;
-          const bool sh = t < run_len && nd <= kPackMaxNeed;
+          // fused: an out-of-bounds record takes the long-record path, which
+          // skips it (its status was written by the prologue)
+          const bool sh = t < run_len && nd <= kPackMaxNeed &&
+                          (!a.fused || rec_in_bounds(D[pos + t], S, a.in_bytes, a.out_bytes, SEAL));
           const uint64_t lm = __ballot(t < run_len && !sh), sm = __ballot(sh);
           uint32_t fb = 0, bb = 0;
           if (lane == 0) {
@@ -811,43 +949,7 @@ __global__ __launch_bounds__(kPrepThreads) void gcm_prep_kernel(BatchArgs a,
     j0[1] = load_u32_bytes(p);
     j0[2] = load_u32_bytes(p + 4);
   }
-  auto body = [&](auto rk) {
-    // E_K(J0)
-    uint32_t s[4] = {j0[0] ^ rk[0], j0[1] ^ rk[1], j0[2] ^ rk[2], j0[3] ^ rk[3]};
-#pragma unroll
-    for (int rr = 1; rr < ROUNDS; rr++) {
-      uint32_t t[4];
-#pragma unroll
-      for (int c = 0; c < 4; c++)
-        t[c] = T0(s[c], 0) ^ T1(s[(c + 1) & 3], 1) ^
-               rotl32(T0(s[(c + 2) & 3], 2) ^ T1(s[(c + 3) & 3], 3), 16) ^ rk[4 * rr + c];
-#pragma unroll
-      for (int c = 0; c < 4; c++) s[c] = t[c];
-    }
-    RecPre o;
-#pragma unroll
-    for (int c = 0; c < 4; c++)
-      o.ek0[c] = (SB(s[c], 0) | (SB(s[(c + 1) & 3], 1) << 8) | (SB(s[(c + 2) & 3], 2) << 16) |
-                  (SB(s[(c + 3) & 3], 3) << 24)) ^ rk[4 * ROUNDS + c];
-    // round-1 constants (ctr_setup) and round-2 constants (rec_consts)
-    const uint32_t s0 = j0[0] ^ rk[0], s1 = j0[1] ^ rk[1], s2 = j0[2] ^ rk[2];
-    uint32_t k1[4];
-    k1[0] = T0(s0, 0) ^ T1(s1, 1) ^ rotl32(T0(s2, 2), 16) ^ rk[4];
-    k1[1] = T0(s1, 0) ^ T1(s2, 1) ^ rotl32(T1(s0, 3), 16) ^ rk[5];
-    k1[2] = T0(s2, 0) ^ rotl32(T0(s0, 2) ^ T1(s1, 3), 16) ^ rk[6];
-    k1[3] = T1(s0, 1) ^ rotl32(T0(s1, 2) ^ T1(s2, 3), 16) ^ rk[7];
-    const uint32_t v0 = rk[3];
-    const uint32_t c2 = k1[2] ^ T1(v0, 1), c3 = k1[3] ^ T0(v0, 0);  // round-1 columns 2, 3
-    o.k1a = k1[0];
-    o.k1b = k1[1];
-    o.k2[0] = rotl32(T0(c2, 2) ^ T1(c3, 3), 16) ^ rk[8];
-    o.k2[1] = T1(c2, 1) ^ rotl32(T0(c3, 2), 16) ^ rk[9];
-    o.k2[2] = T0(c2, 0) ^ T1(c3, 1) ^ rk[10];
-    o.k2[3] = T0(c3, 0) ^ rotl32(T1(c2, 3), 16) ^ rk[11];
-    o.sb2[0] = SB(c2, 0) | (SB(c2, 1) << 8) | (SB(c2, 2) << 16) | (SB(c2, 3) << 24);
-    o.sb2[1] = SB(c3, 0) | (SB(c3, 1) << 8) | (SB(c3, 2) << 16) | (SB(c3, 3) << 24);
-    pre[r] = o;
-  };
+  auto body = [&](auto rk) { pre[r] = rec_pre<SEAL, ROUNDS>(j0, rk, T0, T1, SB); };
   if (uniform)
     body(as_const(a.sessions[sid0].rk));  // wave-uniform: round keys in SGPRs
   else

@@ -31,14 +31,16 @@ int launch_gcm_queue(const BatchArgs& a, const RecPre* pre, bool seal, int round
     if (launch_gcm_queue_b16(a, pre, seal, rounds, groups, s)) return -1;
   } else
 #endif
-  if (rounds == 10) {
+  if (a.fused && a.pack) {
+    // fused (engine.cpp run_batch): only the pack variant runs, with its own prologue
+  } else if (rounds == 10) {
     if (seal) hipLaunchKernelGGL((gcm_hy_kernel<true, 10, 1024, 0, TG_QUEUE_NB>), g, b, 0, s, a, pre);
     else hipLaunchKernelGGL((gcm_hy_kernel<false, 10, 1024, 0, TG_QUEUE_NB>), g, b, 0, s, a, pre);
   } else {
     if (seal) hipLaunchKernelGGL((gcm_hy_kernel<true, 14, 1024, 0, TG_QUEUE_NB>), g, b, 0, s, a, pre);
     else hipLaunchKernelGGL((gcm_hy_kernel<false, 14, 1024, 0, TG_QUEUE_NB>), g, b, 0, s, a, pre);
   }
-  if (a.sel && a.pack) {  // the pack variant: runs instead when the prep pass saw a short record
+  if ((a.sel || a.fused) && a.pack) {  // the pack variant: runs instead when the prep pass saw a short record
     if (rounds == 10) {
       if (seal) hipLaunchKernelGGL((gcm_hy_kernel<true, 10, 1024, 0, TG_QUEUE_NB, true>), g, b, 0, s, a, pre);
       else hipLaunchKernelGGL((gcm_hy_kernel<false, 10, 1024, 0, TG_QUEUE_NB, true>), g, b, 0, s, a, pre);

@@ -398,6 +398,47 @@ int launch_session_install_arg(DevSession* sessions, DevGcmTables* tables,
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// EVP_AEAD_CTX_init's install (round 5): the calling thread built the slot's
+// image on the host (session_host.cpp) in its pinned key area; one 256-thread
+// workgroup copies it into the slot (zero-copy reads of the pinned image), the
+// GCM tables only when `table_bytes` != 0.  Kernel arguments carry pointers
+// only — no key material.
+__global__ __launch_bounds__(256) void upload_session(const uint4* __restrict__ img,
+                                                      DevSession* __restrict__ sess,
+                                                      DevGcmTables* __restrict__ tab,
+                                                      uint32_t table_bytes) {
+  constexpr uint32_t kS = sizeof(DevSession) / 16;
+  const uint32_t n = kS + table_bytes / 16;
+  for (uint32_t i = threadIdx.x; i < n; i += 256) {
+    const uint4 v = img[i];
+    if (i < kS) reinterpret_cast<uint4*>(sess)[i] = v;
+    else reinterpret_cast<uint4*>(tab)[i - kS] = v;
+  }
+}
+
+// EVP_AEAD_CTX_cleanup's scrub (e_aes.c:1415-1422 explicit_bzero analogue):
+// the slot's DevSession and GCM tables zeroed in one launch.
+__global__ __launch_bounds__(256) void scrub_session(DevSession* __restrict__ sess,
+                                                     DevGcmTables* __restrict__ tab) {
+  constexpr uint32_t kS = sizeof(DevSession) / 16, kT = sizeof(DevGcmTables) / 16;
+  for (uint32_t i = threadIdx.x; i < kS + kT; i += 256) {
+    if (i < kS) reinterpret_cast<uint4*>(sess)[i] = make_uint4(0, 0, 0, 0);
+    else reinterpret_cast<uint4*>(tab)[i - kS] = make_uint4(0, 0, 0, 0);
+  }
+}
+
+int launch_upload_session(const void* img, DevSession* sess, DevGcmTables* tab,
+                          uint32_t table_bytes, hipStream_t s) {
+  hipLaunchKernelGGL(upload_session, dim3(1), dim3(256), 0, s,
+                     reinterpret_cast<const uint4*>(img), sess, tab, table_bytes);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_scrub_session(DevSession* sess, DevGcmTables* tab, hipStream_t s) {
+  hipLaunchKernelGGL(scrub_session, dim3(1), dim3(256), 0, s, sess, tab);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_fill_synthetic(uint8_t* d_out, uint64_t stride, uint32_t span_len, uint32_t n,
                           uint64_t seed, uint64_t index0, hipStream_t s) {
   if (n == 0 || span_len == 0) return 0;

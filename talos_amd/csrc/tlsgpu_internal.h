@@ -204,6 +204,12 @@ struct BatchArgs {
   uint32_t pws;                     // per-wave-session kernel: 0 auto (runs shorter than
                                     // kPwsRun records on average), 1 never, 2 always
   uint32_t* wg_next;                // per-wave-session kernel: one record counter per workgroup
+  uint32_t fused;                   // queue no-pack kernel (round 5): the bounds check, the
+                                    // initial statuses and the per-record constants of the
+                                    // workgroup's records run in its own prologue (no
+                                    // check_record_bounds / gcm_prep_kernel launches); descs
+                                    // are the caller's, checked against in_bytes / out_bytes
+  uint64_t in_bytes, out_bytes;     // fused: sizes of the caller's in / out buffers
 };
 
 // Average session-run length below which the per-wave-session kernel (gcm_pw.hip)
@@ -315,6 +321,18 @@ int launch_wire_finish(uint32_t n_streams, tlsgpu_wire_result* results, int32_t*
                        hipStream_t s);
 int launch_fill_synthetic(uint8_t* d_out, uint64_t stride, uint32_t span_len,
                           uint32_t n, uint64_t seed, uint64_t index0, hipStream_t s);
+int launch_upload_session(const void* img, DevSession* sess, DevGcmTables* tab,
+                          uint32_t table_bytes, hipStream_t s);
+int launch_scrub_session(DevSession* sess, DevGcmTables* tab, hipStream_t s);
+// session_host.cpp: the image install_body writes, built on the host
+bool host_session_image(const tlsgpu_session_params& p, DevSession* s, DevGcmTables* t);
+// GCM table bytes the default kernels read (basis + Shoup tables; the
+// bitsliced masks only in the experimental build)
+#ifdef TG_EXPERIMENTAL
+constexpr uint32_t kGcmTableUploadBytes = sizeof(DevGcmTables);
+#else
+constexpr uint32_t kGcmTableUploadBytes = offsetof(DevGcmTables, bsrk);
+#endif
 int launch_check_bounds(const tlsgpu_record* recs, tlsgpu_record* safe, uint32_t n,
                         const DevSession* sessions, uint32_t n_sessions, uint64_t in_bytes,
                         uint64_t out_bytes, bool seal, int32_t* status, uint32_t* ctl,

@@ -39,6 +39,19 @@ int g_ndev = [] {
 }();
 thread_local int t_dev = 0;
 
+// The runtime's own per-thread state (libamdhip64 registers a thread-local
+// destructor at a thread's first HIP call; tools/exit_order_probe.hip): here a
+// sentinel created at the thread's first stub call.  A HIP call after it was
+// destroyed — from a thread-local destructor of ours that runs later — is the
+// hazard of the round-4 exit SIGSEGV and a violation.
+struct RuntimeTls {
+  bool alive = true;
+  ~RuntimeTls() { alive = false; }
+};
+thread_local RuntimeTls t_rt;
+thread_local bool t_rt_seen = false;
+void rt_enter(const char* what);
+
 struct Alloc {
   size_t size;
   int dev;
@@ -123,6 +136,17 @@ hipError_t release(void* p, bool pinned, const char* what) {
   return hipSuccess;
 }
 
+void rt_enter(const char* what) {
+  if (!t_rt_seen) {
+    t_rt_seen = true;
+    (void)&t_rt;  // constructed now: its destructor is registered at this point
+  } else if (!t_rt.alive) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    violation("%s: HIP call from a thread-exit destructor after the runtime's thread state "
+              "was destroyed", what);
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -130,64 +154,79 @@ hipError_t release(void* p, bool pinned, const char* what) {
 extern "C" {
 
 hipError_t hipSetDevice(int d) {
+  rt_enter("hipSetDevice");
   if (d < 0 || d >= g_ndev) return hipErrorInvalidDevice;
   t_dev = d;
   return hipSuccess;
 }
 hipError_t hipGetDeviceCount(int* c) {
+  rt_enter("hipGetDeviceCount");
   *c = g_ndev;
   return hipSuccess;
 }
 hipError_t hipDeviceGetAttribute(int* v, hipDeviceAttribute_t, int d) {
+  rt_enter("hipDeviceGetAttribute");
   if (d < 0 || d >= g_ndev) return hipErrorInvalidDevice;
   *v = 256;
   return hipSuccess;
 }
-hipError_t hipDeviceSynchronize(void) { return hipSuccess; }
-hipError_t hipGetLastError(void) { return hipSuccess; }
-const char* hipGetErrorString(hipError_t) { return "devstub"; }
+hipError_t hipDeviceSynchronize(void) {
+  rt_enter("hipDeviceSynchronize"); return hipSuccess; }
+hipError_t hipGetLastError(void) {
+  rt_enter("hipGetLastError"); return hipSuccess; }
+const char* hipGetErrorString(hipError_t) {
+  rt_enter("hipGetErrorString"); return "devstub"; }
 
 hipError_t hipMalloc(void** p, size_t n) {
+  rt_enter("hipMalloc");
   std::lock_guard<std::mutex> lk(g_mu);
   *p = alloc(n, false);
   return *p ? hipSuccess : hipErrorOutOfMemory;
 }
 hipError_t hipMallocAsync(void** p, size_t n, hipStream_t s) {
+  rt_enter("hipMallocAsync");
   std::lock_guard<std::mutex> lk(g_mu);
   stream_dev("hipMallocAsync", s);
   *p = alloc(n, false);
   return *p ? hipSuccess : hipErrorOutOfMemory;
 }
 hipError_t hipFree(void* p) {
+  rt_enter("hipFree");
   std::lock_guard<std::mutex> lk(g_mu);
   return release(p, false, "hipFree");
 }
 hipError_t hipFreeAsync(void* p, hipStream_t s) {
+  rt_enter("hipFreeAsync");
   std::lock_guard<std::mutex> lk(g_mu);
   stream_dev("hipFreeAsync", s);
   return release(p, false, "hipFreeAsync");
 }
 hipError_t hipHostMalloc(void** p, size_t n, unsigned int) {
+  rt_enter("hipHostMalloc");
   std::lock_guard<std::mutex> lk(g_mu);
   *p = alloc(n, true);
   return *p ? hipSuccess : hipErrorOutOfMemory;
 }
 hipError_t hipHostFree(void* p) {
+  rt_enter("hipHostFree");
   std::lock_guard<std::mutex> lk(g_mu);
   return release(p, true, "hipHostFree");
 }
 hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned int) {
+  rt_enter("hipHostGetDevicePointer");
   *d = h;
   return hipSuccess;
 }
 
 hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned int) {
+  rt_enter("hipStreamCreateWithFlags");
   std::lock_guard<std::mutex> lk(g_mu);
   *s = reinterpret_cast<hipStream_t>(new char);
   g_streams[*s] = t_dev;
   return hipSuccess;
 }
 hipError_t hipStreamDestroy(hipStream_t s) {
+  rt_enter("hipStreamDestroy");
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_streams.find(s);
   if (it == g_streams.end()) return hipErrorInvalidHandle;
@@ -195,8 +234,10 @@ hipError_t hipStreamDestroy(hipStream_t s) {
   delete reinterpret_cast<char*>(s);
   return hipSuccess;
 }
-hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+hipError_t hipStreamSynchronize(hipStream_t) {
+  rt_enter("hipStreamSynchronize"); return hipSuccess; }
 hipError_t hipStreamWaitEvent(hipStream_t s, hipEvent_t e, unsigned int) {
+  rt_enter("hipStreamWaitEvent");
   std::lock_guard<std::mutex> lk(g_mu);
   stream_dev("hipStreamWaitEvent", s);
   if (!g_events.count(e)) violation("hipStreamWaitEvent: unknown event");
@@ -204,19 +245,23 @@ hipError_t hipStreamWaitEvent(hipStream_t s, hipEvent_t e, unsigned int) {
 }
 
 hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned int) {
+  rt_enter("hipEventCreateWithFlags");
   std::lock_guard<std::mutex> lk(g_mu);
   *e = reinterpret_cast<hipEvent_t>(new char);
   g_events[*e] = t_dev;
   return hipSuccess;
 }
-hipError_t hipEventCreate(hipEvent_t* e) { return hipEventCreateWithFlags(e, 0); }
+hipError_t hipEventCreate(hipEvent_t* e) {
+  rt_enter("hipEventCreate"); return hipEventCreateWithFlags(e, 0); }
 hipError_t hipEventDestroy(hipEvent_t e) {
+  rt_enter("hipEventDestroy");
   std::lock_guard<std::mutex> lk(g_mu);
   if (!g_events.erase(e)) return hipErrorInvalidHandle;
   delete reinterpret_cast<char*>(e);
   return hipSuccess;
 }
 hipError_t hipEventRecord(hipEvent_t e, hipStream_t s) {
+  rt_enter("hipEventRecord");
   std::lock_guard<std::mutex> lk(g_mu);
   const int d = stream_dev("hipEventRecord", s);
   auto it = g_events.find(e);
@@ -225,18 +270,23 @@ hipError_t hipEventRecord(hipEvent_t e, hipStream_t s) {
     violation("hipEventRecord: event of device %d recorded on a stream of device %d", it->second, d);
   return hipSuccess;
 }
-hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
-hipError_t hipEventQuery(hipEvent_t) { return hipSuccess; }
+hipError_t hipEventSynchronize(hipEvent_t) {
+  rt_enter("hipEventSynchronize"); return hipSuccess; }
+hipError_t hipEventQuery(hipEvent_t) {
+  rt_enter("hipEventQuery"); return hipSuccess; }
 hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) {
+  rt_enter("hipEventElapsedTime");
   *ms = 1.0f;
   return hipSuccess;
 }
 
 hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind) {
+  rt_enter("hipMemcpy");
   if (n) memmove(d, s, n);
   return hipSuccess;
 }
 hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipStream_t st) {
+  rt_enter("hipMemcpyAsync");
   {
     std::lock_guard<std::mutex> lk(g_mu);
     const int dev = stream_dev("hipMemcpyAsync", st);
@@ -247,6 +297,7 @@ hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipSt
   return hipSuccess;
 }
 hipError_t hipMemset(void* p, int v, size_t n) {
+  rt_enter("hipMemset");
   {
     std::lock_guard<std::mutex> lk(g_mu);
     mem_on("hipMemset", "dst", p, t_dev);
@@ -255,6 +306,7 @@ hipError_t hipMemset(void* p, int v, size_t n) {
   return hipSuccess;
 }
 hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t s) {
+  rt_enter("hipMemsetAsync");
   {
     std::lock_guard<std::mutex> lk(g_mu);
     mem_on("hipMemsetAsync", "dst", p, stream_dev("hipMemsetAsync", s));
@@ -263,6 +315,7 @@ hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t s) {
   return hipSuccess;
 }
 hipError_t hipMemsetD32Async(hipDeviceptr_t p, int v, size_t n, hipStream_t s) {
+  rt_enter("hipMemsetD32Async");
   {
     std::lock_guard<std::mutex> lk(g_mu);
     mem_on("hipMemsetD32Async", "dst", p, stream_dev("hipMemsetD32Async", s));
@@ -337,6 +390,16 @@ int launch_session_install_arg(DevSession* sessions, DevGcmTables* tables, const
 int launch_session_install(DevSession* sessions, DevGcmTables* tables, const tlsgpu_session_params* p,
                            uint32_t, uint32_t, hipStream_t s) {
   return launch("launch_session_install", s, {{"sessions", sessions}, {"tables", tables}, {"params", p}});
+}
+int launch_upload_session(const void* img, DevSession* sess, DevGcmTables* tab, uint32_t table_bytes,
+                          hipStream_t s) {
+  launch("launch_upload_session", s, {{"img", img}, {"sessions", sess}, {"tables", tab}});
+  memcpy(sess, img, sizeof(DevSession));
+  if (table_bytes) memcpy(tab, reinterpret_cast<const uint8_t*>(img) + sizeof(DevSession), table_bytes);
+  return 0;
+}
+int launch_scrub_session(DevSession* sess, DevGcmTables* tab, hipStream_t s) {
+  return launch("launch_scrub_session", s, {{"sessions", sess}, {"tables", tab}});
 }
 int launch_wire_frame(const tlsgpu_wire_stream* streams, uint32_t, const uint8_t* wire,
                       const DevSession* sessions, uint32_t, uint32_t, tlsgpu_record* recs,

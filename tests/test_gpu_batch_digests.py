@@ -44,13 +44,16 @@ def _batches():
 
 @pytest.mark.parametrize("name", ["B", "C", "D", "B_S1", "B_Sn", "B_inter", "D_inter", "old_small",
                                   "D_small", "inter_small", "E_shard_small"] +
-                         [f"E_shard{r}" for r in range(8)])
+                         [f"E_shard{r}" for r in range(8)] + ["B:hinted", "D:hinted"])
 def test_batch_digest_matches_reference(ta, engine, name):
     """E_shard<r>: config E is one 524,288-record batch split
     across 8 GPUs; each of its 8 shards is built here, on one GPU, exactly as
     GPU r builds it under bench.py --gpus 8, and must reproduce the reference's
     digest of that slice of the batch."""
     from talos_amd.workload import Workload, zipf_lengths
+    # ":hinted": the batch-shape hints bench.py states (talos_amd.batch_hints),
+    # so B and D run the fused queue kernel (engine.cpp run_batch `fused`)
+    name, _, hinted = name.partition(":")
     d = _batches()[name]
     kind = ta.AEAD_NAMES[d["aead"]]
     n, S, seed, te = d["records"], d["sessions"], d["seed"], d["tamper_every"]
@@ -60,6 +63,9 @@ def test_batch_digest_matches_reference(ta, engine, name):
                   record_len=0 if zipf else d["lengths"], interleave=d.get("interleave", False),
                   shard=(lo, hi))
     try:
+        if hinted:
+            wl.table.hint(ta.batch_hints(wl.lengths + ta.EXPLICIT_NONCE_LEN[kind] + ta.TAG_LEN,
+                                         wl.session, seal=False))
         assert int(wl.lengths.sum()) == d["payload_bytes"]
         assert wl.sealed_digest() == d["sealed_sha256"], "sealed bodies differ from the reference"
         wl.apply_tamper(te)

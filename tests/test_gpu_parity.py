@@ -550,6 +550,74 @@ def test_batch_bounds(ta, engine, oracle, mode):
     table.close()
 
 
+@pytest.mark.parametrize("mode", ["open", "seal"])
+@pytest.mark.parametrize("hints", [2, 3])
+@pytest.mark.parametrize("name", ["aes-128-gcm", "aes-256-gcm"])
+def test_batch_fused_prologue(ta, engine, oracle, gcm_impl, mode, hints, name):
+    """The fused queue kernel (round 5, engine.cpp run_batch `fused`): one AES
+    key size installed and SESSION_RUNS stated, so the queue kernel is the
+    batch's only launch and checks bounds, writes the initial statuses and
+    derives each record's constants in its own prologue (no
+    check_record_bounds, no gcm_prep_kernel, no descriptor copy).  hints = 3
+    (NO_SHORT_RECORDS too) runs the no-pack variant, 2 the pack variant.  Every
+    record equals the oracle's tls1_enc, tampered records are zero-filled,
+    out-of-bounds records (input past d_in, output past d_out, offset
+    overflow; short records, which the pack plan must leave out, among them)
+    get REC_OUT_OF_BOUNDS and leave their output untouched."""
+    import numpy as np
+    from talos_amd.batch import RecordBatch
+    gcm_impl("queue")
+    rnd = random.Random(90 + hints)
+    kind = KINDS[name]
+    params = _mk_sessions(ta, rnd, [kind] * 4)
+    table = ta.SessionTable(engine, 4)
+    table.install(0, params)
+    table.hint(hints)
+    osess = _oracle_sessions(oracle, params)
+    lengths = [0, 1, 15, 16, 17, 100, 1000, 16384, 5000, 64, 992, 993, 2000]
+    recs = []
+    for sid in range(4):                           # session runs of 80 records
+        for i in range(80):
+            n = lengths[(i + sid) % len(lengths)]
+            recs.append((sid, 1000 * sid + i, 23, bytes(rnd.getrandbits(8) for _ in range(n)), kind))
+    if mode == "open":
+        tamper = {i for i in range(len(recs)) if i % 7 == 3 and recs[i][3]}
+        bodies = []
+        for i, (sid, seq, rt, pt, k) in enumerate(recs):
+            b = bytearray(oracle.tls_seal(osess[sid], seq, rt, pt))
+            if i in tamper:
+                b[rnd.randrange(len(b))] ^= 4
+            bodies.append((sid, seq, rt, bytes(b), k))
+        batch = RecordBatch(engine, bodies, "open")
+    else:
+        batch = RecordBatch(engine, recs, "seal")
+    descs = batch.d_recs.download().view(ta.RECORD_DTYPE).copy()
+    oob = {5: ("in_off", batch.d_in.nbytes - 3), 81: ("out_off", batch.d_out.nbytes - 8),
+           162: ("in_off", (1 << 63) + 5), 252: ("out_off", batch.d_out.nbytes - 8)}
+    for i, (f, v) in oob.items():
+        descs[i][f] = v
+    batch.d_recs.upload(descs.view(np.uint8))
+    batch.run(table)
+    res = batch.results()
+    out = batch.d_out.download()
+    for i, ((st, got), (sid, seq, rt, pt, k)) in enumerate(zip(res, recs)):
+        if i in oob:
+            assert st == ta.REC_OUT_OF_BOUNDS, (i, st)
+            continue
+        if mode == "seal":
+            exp = oracle.tls_seal(osess[sid], seq, rt, pt)
+            assert st == len(exp) and got == exp, (i, len(pt), st)
+        else:
+            est, exp = oracle.tls_open(osess[sid], seq, rt, bodies[i][3])
+            if i in tamper:
+                assert est == -1 and st == ta.REC_BAD_MAC and got == bytes(len(got)), i
+            else:
+                assert st == len(pt) and got == pt, (i, len(pt), st)
+    o = int(descs[252]["out_off"])
+    assert (out[o:] == 0xA5).all()                 # nothing written past d_out
+    table.close()
+
+
 def test_batch_per_wave_session_kernel_forced(ta):
     """TLSGPU_PWS=1: every queue-impl GCM batch runs on the per-wave-session
     kernel (gcm_pw.hip: per-wave nibble GHASH tables, Shoup weights from HBM,

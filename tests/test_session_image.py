@@ -1,0 +1,215 @@
+"""The session image EVP_AEAD_CTX_init builds on the host (round 5,
+talos_amd/csrc/session_host.cpp; VERDICT r04 next-round 6 and hygiene).
+
+EVP_AEAD_CTX_init no longer launches the install kernel with the raw key as a
+kernel argument: the calling thread derives what aead_aes_gcm_init /
+CRYPTO_gcm128_init derive on the CPU (crypto/evp/e_aes.c:1372-1413,
+crypto/modes/gcm128.c:681-747: the FIPS-197 key schedule, H = E_K(0^128), and
+for the batch kernels the powers H^1..H^65, their 4-bit Shoup tables and the
+basis H^64 * x^q) into a pinned key area that one kernel copies into the slot.
+
+CPU: every field of the image against an independent model — AES from the
+oracle (oracle/aes.c restates aes_core.c), GF(2^128) products in Python in
+gcm128.c's bit order, pinned to the oracle's gf128_mul; ChaCha and invalid
+parameters.  GPU: the host image equals, byte for byte, what the device install
+kernel (install_sessions) writes for the same parameters.
+"""
+import ctypes as C
+import os
+import random
+import struct
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import pyoracle as po  # noqa: E402
+
+IMG = 1024 + 2048 + 65 * 256 + 15 * 512   # DevSession + DevGcmTables
+TABLES_USED = 2048 + 65 * 256              # basis + Shoup tables (the default kernels)
+
+
+@pytest.fixture(scope="module")
+def ta():
+    import talos_amd
+    lib = talos_amd.load_library()
+    lib.tlsgpu_session_image.restype = C.c_int
+    lib.tlsgpu_session_image.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+    return talos_amd
+
+
+@pytest.fixture(scope="module")
+def engine(ta):
+    e = ta.Engine(0)
+    yield e
+    e.close()
+
+
+def image(ta, params):
+    p = params.to_c()
+    out = (C.c_uint8 * IMG)()
+    assert ta.load_library().tlsgpu_session_image(C.byref(p), out, IMG) == 0
+    return bytes(out)
+
+
+# --- GF(2^128) in gcm128.c's bit order: bit 127 of the int is x^0
+R = 0xE1 << 120
+
+
+def mulx(v):
+    return (v >> 1) ^ (R if v & 1 else 0)
+
+
+def gmul(a, b):
+    z = 0
+    for i in range(128):
+        if (a >> (127 - i)) & 1:
+            z ^= b
+        b = mulx(b)
+    return z
+
+
+def be_int(b):
+    return int.from_bytes(b, "big")
+
+
+def le_words(v):   # 16-byte string of v as 4 little-endian words
+    return struct.unpack("<4I", v.to_bytes(16, "big"))
+
+
+def be_words(v):
+    return struct.unpack(">4I", v.to_bytes(16, "big"))
+
+
+def shoup(y):
+    m = [0] * 16
+    m[8] = y
+    m[4] = mulx(m[8])
+    m[2] = mulx(m[4])
+    m[1] = mulx(m[2])
+    a = 2
+    while a < 16:
+        for b in range(1, a):
+            m[a + b] = m[a] ^ m[b]
+        a <<= 1
+    return m
+
+
+SBOX = None
+
+
+def key_schedule(key):   # FIPS-197, big-endian words
+    global SBOX
+    if SBOX is None:   # from the oracle's AES: S(x) = E applied... derive by the standard formula
+        def xt(x):
+            return ((x << 1) ^ (0x1B if x & 0x80 else 0)) & 0xFF
+        exp, log = [0] * 256, [0] * 256
+        p = 1
+        for i in range(255):
+            exp[i], log[p] = p, i
+            p ^= xt(p)
+        SBOX = []
+        for x in range(256):
+            inv = exp[(255 - log[x]) % 255] if x else 0
+            r = inv
+            for k in range(1, 5):
+                r ^= ((inv << k) | (inv >> (8 - k))) & 0xFF
+            SBOX.append(r ^ 0x63)
+    nk = len(key) // 4
+    rounds = nk + 6
+    w = [int.from_bytes(key[4 * i:4 * i + 4], "big") for i in range(nk)]
+    rcon = 1
+    for i in range(nk, 4 * (rounds + 1)):
+        t = w[-1]
+        if i % nk == 0:
+            t = ((t << 8) | (t >> 24)) & 0xFFFFFFFF
+            t = (SBOX[t >> 24] << 24) | (SBOX[(t >> 16) & 255] << 16) | (SBOX[(t >> 8) & 255] << 8) | SBOX[t & 255]
+            t ^= rcon << 24
+            rcon = ((rcon << 1) ^ (0x1B if rcon & 0x80 else 0)) & 0xFF
+        elif nk > 6 and i % nk == 4:
+            t = (SBOX[t >> 24] << 24) | (SBOX[(t >> 16) & 255] << 16) | (SBOX[(t >> 8) & 255] << 8) | SBOX[t & 255]
+        w.append(w[i - nk] ^ t)
+    return rounds, w
+
+
+def test_gf_model_pinned_to_oracle(oracle):
+    rnd = random.Random(3)
+    for _ in range(20):
+        a, b = rnd.randbytes(16), rnd.randbytes(16)
+        assert gmul(be_int(a), be_int(b)) == be_int(oracle.gf128_mul(a, b))
+
+
+@pytest.mark.parametrize("kind", [po.AES_128_GCM, po.AES_256_GCM])
+def test_host_gcm_image_matches_model(ta, oracle, kind):
+    rnd = random.Random(kind * 17)
+    for case in range(3):
+        key = rnd.randbytes(po.KEY_LEN[kind])
+        fiv = rnd.randbytes(4)
+        tag = [0, 16, 12][case]
+        img = image(ta, ta.SessionParams(kind, key, fiv, tag_len=tag, version=0x0303))
+        hdr = struct.unpack_from("<8I", img, 0)
+        rounds, rk_be = key_schedule(key)
+        assert hdr == (kind, rounds, tag or 16, len(key), 4, 0, 1, 0x0303), hdr
+        assert img[32:36] == fiv and img[36:48] == bytes(12)
+        rk = struct.unpack_from("<60I", img, 48)
+        nw = 4 * (rounds + 1)
+        assert list(rk[:nw]) == [int.from_bytes(w.to_bytes(4, "big"), "little") for w in rk_be]
+        assert rk[nw:] == (0,) * (60 - nw)
+        rk_rot = struct.unpack_from("<60I", img, 336)
+        assert list(rk_rot[:nw]) == [((w >> 16) | (w << 16)) & 0xFFFFFFFF for w in rk[:nw]]
+        H = be_int(oracle.aes_encrypt(key, bytes(16)))
+        assert struct.unpack_from("<4I", img, 320) == le_words(H)
+        assert img[288:320] == bytes(32)          # no ChaCha key
+        t = 1024
+        pw, powers = H, []
+        for e in range(65):
+            powers.append(pw)
+            pw = gmul(pw, H)
+        for e in range(65):
+            m = shoup(powers[e])
+            for v in range(16):
+                off = t + 2048 + (e * 16 + v) * 16
+                assert struct.unpack_from("<4I", img, off) == be_words(m[v]), (e, v)
+        b = powers[63]   # H^64
+        for q in range(128):
+            assert struct.unpack_from("<4I", img, t + 16 * q) == le_words(b), q
+            b = mulx(b)
+        bs = t + 2048 + 65 * 256
+        for w in range(128 * (rounds + 1)):
+            r_, byte, k = w // 128, (w % 128) // 8, w % 8
+            want = 0xFFFFFFFF if (rk[4 * r_ + byte // 4] >> (8 * (byte % 4) + k)) & 1 else 0
+            assert struct.unpack_from("<I", img, bs + 4 * (128 * r_ + 8 * byte + k))[0] == want
+
+
+def test_host_chacha_and_invalid_images(ta):
+    key = bytes(range(32))
+    img = image(ta, ta.SessionParams(po.CHACHA20_POLY1305, key, bytes(range(12))))
+    assert struct.unpack_from("<8I", img, 0) == (po.CHACHA20_POLY1305, 0, 16, 32, 12, 1, 0, 0x0303)
+    assert img[32:44] == bytes(range(12)) and img[288:320] == key
+    assert img[1024:] == bytes(IMG - 1024)     # no GCM tables
+    img = image(ta, ta.SessionParams(po.CHACHA20_POLY1305_OLD, key, b""))
+    assert struct.unpack_from("<8I", img, 0)[:6] == (po.CHACHA20_POLY1305_OLD, 0, 16, 32, 0, 0)
+    bad = ta.SessionParams(po.AES_128_GCM, bytes(32), bytes(4))   # 32-byte key for AES-128
+    assert image(ta, bad) == bytes(IMG)
+
+
+@pytest.mark.gpu
+def test_host_image_equals_device_install(ta, engine):
+    """The device install kernel (install_sessions, the batch API's path) and the
+    host image write the same bytes for the same parameters."""
+    rnd = random.Random(11)
+    kinds = [po.AES_128_GCM, po.AES_256_GCM, po.CHACHA20_POLY1305, po.CHACHA20_POLY1305_OLD] * 2
+    params = [ta.SessionParams(k, rnd.randbytes(po.KEY_LEN[k]), rnd.randbytes(po.FIXED_IV_LEN[k]),
+                               tag_len=rnd.choice([0, 16, 13])) for k in kinds]
+    table = ta.SessionTable(engine, len(params))
+    table.install(0, params)
+    lib = ta.load_library()
+    for i, p in enumerate(params):
+        dev = (C.c_uint8 * IMG)()
+        assert lib.tlsgpu_sessions_debug_read(table.handle, i, dev, IMG) == 0
+        host = image(ta, p)
+        used = 1024 + (TABLES_USED if p.aead in (po.AES_128_GCM, po.AES_256_GCM) else 0)
+        assert bytes(dev)[:used] == host[:used], (i, p.aead)
+    table.close()
