@@ -414,7 +414,10 @@ def main():
                      "read_frac": round(algo_rd / per_launch_s / 1e9 / HBM_PEAK_GBS, 4),
                      "kernel": kernel, "traffic_source": traffic_src,
                      "timing": "HIP events around each whole step on the engine stream "
-                               "(prep pass + status memset + main kernel)", **comp},
+                               "(one tlsgpu_open_batch: with the stated hints the fused queue "
+                               "kernel alone, its prologue doing the bounds check, statuses and "
+                               "per-record constants; else bounds + prep passes + main kernels)",
+                     **comp},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if rec_len:

@@ -439,8 +439,10 @@ int tlsgpu_evp_call_stats(uint64_t *seal_calls, uint64_t *open_calls);
  * a context's first call (its key install still queued), draft-suite ChaCha
  * contexts and pooled (queued) contexts use the other paths.  Same as
  * TLSGPU_EVP_DOORBELL=<groups> (TLSGPU_EVP_DOORBELL_MS=<lifetime>) at load;
- * off (0 groups) by default, 64 is the measured setting; must be called
- * before the first EVP call.  tlsgpu_evp_doorbell_stats: jobs
+ * on by default with 64 groups (round 5; 0 turns it off); must be called
+ * before the first EVP call.  With it on, EVP_AEAD_CTX_init launches nothing
+ * (the session image is built on the host and installed by the context's
+ * first call) and EVP_AEAD_CTX_cleanup scrubs the slot through the server.  tlsgpu_evp_doorbell_stats: jobs
  * served and instances launched so far. */
 int tlsgpu_evp_set_doorbell(unsigned groups, unsigned lifetime_ms);
 int tlsgpu_evp_doorbell_stats(uint64_t *jobs, uint64_t *launches);

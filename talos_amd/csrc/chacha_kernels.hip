@@ -621,10 +621,19 @@ int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, h
   if (rfc) {
     // TLSGPU_CC_LDS_PAD=<bytes> (A/B only): unused dynamic LDS per 4-wave
     // workgroup, which lowers the waves per SIMD (40 KiB static: 1 B more = 3)
-    static const unsigned pad = [] {
+    static const unsigned pad_all = [] {
       const char* e = getenv("TLSGPU_CC_LDS_PAD");
       return e ? (unsigned)strtoul(e, nullptr, 10) : 0u;
     }();
+    // per direction (A/B): TLSGPU_CC_LDS_PAD_OPEN / _SEAL
+    static const unsigned pad_dir[2] = {[] {
+      const char* e = getenv("TLSGPU_CC_LDS_PAD_OPEN");
+      return e ? (unsigned)strtoul(e, nullptr, 10) : 0u;
+    }(), [] {
+      const char* e = getenv("TLSGPU_CC_LDS_PAD_SEAL");
+      return e ? (unsigned)strtoul(e, nullptr, 10) : 0u;
+    }()};
+    const unsigned pad = pad_all ? pad_all : pad_dir[seal ? 1 : 0];
     static const uint32_t diag = [] {
       const char* e = getenv("TLSGPU_CC_DIAG");
       return e ? (uint32_t)strtoul(e, nullptr, 0) & 7u : 0u;

@@ -427,6 +427,14 @@ static const bool g_fused = [] {
   const char* v = getenv("TLSGPU_FUSED");
   return !(v && *v == '0');
 }();
+// Work-balanced ranges for the fused kernel (round 5): 0 off, 1 the pack
+// variant (mixed record lengths; the default), 2 always.  Equal record counts
+// per workgroup leave the Zipf workload's slowest CU with 16% more bytes than
+// the mean.
+static const uint32_t g_balance = [] {
+  const char* v = getenv("TLSGPU_BALANCE");
+  return v && *v ? (uint32_t)strtoul(v, nullptr, 10) : 1u;
+}();
 
 // bounds: {in_bytes, out_bytes} of a caller's TLS batch (checked by a pre-pass
 // that hands the kernels a sanitized copy of the descriptors), or null for
@@ -502,7 +510,11 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   static_assert(kSelSlots * kSelWords * 4 <= 1024, "selection words exceed their slot");
   const size_t cnt_bytes = ((size_t)groups * 4 + 255) & ~(size_t)255;
   const size_t ctl_bytes = 2048 + 2 * cnt_bytes;
-  const size_t pre_bytes = gcm_pre ? sizeof(RecPre) * (size_t)n + (fused ? 0 : ctl_bytes) : 0;
+  const bool balance = fused && groups > 1 && groups <= 1024 &&
+                       (g_balance >= 2 || (g_balance == 1 && a.pack != 0));
+  const size_t cut_bytes = balance ? ((size_t)groups * 8 + 255) & ~(size_t)255 : 0;
+  const size_t pre_bytes =
+      gcm_pre ? sizeof(RecPre) * (size_t)n + (fused ? cut_bytes : ctl_bytes) : 0;
   uint8_t* scratch = nullptr;
   uint8_t* pool_scratch = nullptr;
   if (pre_bytes || bounds) {
@@ -526,6 +538,12 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
     a.fused = 1;
     a.in_bytes = bounds->in_bytes;
     a.out_bytes = bounds->out_bytes;
+    if (balance) {  // each count range's work, then the kernel cuts at equal work
+      auto* cw = reinterpret_cast<unsigned long long*>(pre + n);
+      if (launch_range_work(a, groups, cw, s))
+        return fail(TLSGPU_EHIP, "range work launch: %s", hipGetErrorString(hipGetLastError()));
+      a.cut_work = cw;
+    }
   } else if (bounds) {
     // one setup launch: sanitized descriptors, every record's initial status
     // (records whose session is empty / invalid keep TLSGPU_REC_PUBLIC_INVALID)
@@ -1197,7 +1215,51 @@ struct AeadState {
   hipEvent_t installed;   // the slot's event, recorded after the context's key install
   uint32_t key_id = 0;    // unique per install (doorbell server's LDS table cache)
   mutable std::atomic<bool> install_pending{true};  // no call has waited for it yet
+  // Deferred install (round 5): the session image built on the host at init
+  // (session_host.cpp) in a pinned image buffer, installed by the context's
+  // first call — posted with the doorbell job, or one upload kernel ahead of a
+  // launched job — so EVP_AEAD_CTX_init launches nothing.  0: on the device
+  // (or no image), 1: image waiting, 2: a call is installing it
+  mutable std::atomic<int> image{0};
+  uint8_t* img_h = nullptr;  // pinned image (host / device views)
+  uint8_t* img_d = nullptr;
+  bool img_tables = false;   // the image has GCM tables
+  hipEvent_t slot_ev = nullptr;  // the slot's event: its previous owner's scrub
 };
+
+// Pinned image buffers of deferred installs, per device, reused (zeroed on
+// return: key material).
+struct ImagePool {
+  std::mutex mu;
+  std::vector<std::pair<uint8_t*, uint8_t*>> free;  // (host, device view)
+};
+constexpr size_t kImageBytes = sizeof(DevSession) + sizeof(DevGcmTables);
+static ImagePool g_img_pool[64];
+static bool image_take(int dev, uint8_t** h, uint8_t** d) {
+  if (dev < 0 || dev >= 64) return false;
+  {
+    std::lock_guard<std::mutex> lk(g_img_pool[dev].mu);
+    if (!g_img_pool[dev].free.empty()) {
+      *h = g_img_pool[dev].free.back().first;
+      *d = g_img_pool[dev].free.back().second;
+      g_img_pool[dev].free.pop_back();
+      return true;
+    }
+  }
+  if (hipSetDevice(dev) != hipSuccess ||
+      hipHostMalloc((void**)h, kImageBytes, hipHostMallocDefault) != hipSuccess)
+    return false;
+  if (hipHostGetDevicePointer((void**)d, *h, 0) != hipSuccess) {
+    (void)hipHostFree(*h);
+    return false;
+  }
+  return true;
+}
+static void image_give(int dev, uint8_t* h, uint8_t* d) {
+  explicit_bzero(h, kImageBytes);
+  std::lock_guard<std::mutex> lk(g_img_pool[dev].mu);
+  g_img_pool[dev].free.emplace_back(h, d);
+}
 
 // EVP context storage without a device allocation per context (connection
 // churn): contexts outside the coalescing queue take a slot of
@@ -1556,6 +1618,34 @@ static void scrub_slot(tlsgpu_sessions* t, uint32_t slot) {
   (void)hipMemset(t->d_gcm + slot, 0, sizeof(DevGcmTables));
 }
 
+static bool doorbell_enabled();
+// A context whose calls can take the doorbell defers its install to its first
+// call (TLSGPU_EVP_DEFERRED_INSTALL=0: never).
+static const bool g_deferred_install = [] {
+  const char* v = getenv("TLSGPU_EVP_DEFERRED_INSTALL");
+  return !(v && *v == '0');
+}();
+static bool deferred_install_ok(int kind);
+
+static int defer_install(AeadState* st, const tlsgpu_session_params& p) {
+  tlsgpu_sessions* t = st->sess;
+  if (!valid_params(p) || st->slot >= t->capacity) return fail(TLSGPU_EINVAL, "bad session");
+  if (hipSetDevice(t->eng->device) != hipSuccess) return fail(TLSGPU_EHIP, "set device");
+  st->slot_ev = slot_event(t, st->slot);  // its previous owner's scrub, if launched
+  if (!st->slot_ev) return fail(TLSGPU_EHIP, "slot event");
+  if (!image_take(t->eng->device, &st->img_h, &st->img_d)) return fail(TLSGPU_ENOMEM, "session image");
+  st->img_tables = host_session_image(p, reinterpret_cast<DevSession*>(st->img_h),
+                                      reinterpret_cast<DevGcmTables*>(st->img_h + sizeof(DevSession)));
+  st->installed = st->slot_ev;
+  st->install_pending.store(false, std::memory_order_release);  // nothing queued
+  st->image.store(1, std::memory_order_release);
+  std::lock_guard<std::mutex> lk(t->mu);
+  t->kinds[st->slot] = p.aead;
+  t->tag_lens[st->slot] = (uint8_t)(p.tag_len ? p.tag_len : 16);
+  t->have[p.aead] = true;
+  return TLSGPU_OK;
+}
+
 extern "C" int EVP_AEAD_CTX_init(EVP_AEAD_CTX* ctx, const EVP_AEAD* aead, const unsigned char* key,
                                  size_t key_len, size_t tag_len, ENGINE* impl) {
   (void)impl;
@@ -1607,11 +1697,15 @@ extern "C" int EVP_AEAD_CTX_init(EVP_AEAD_CTX* ctx, const EVP_AEAD* aead, const 
   memcpy(p.key, key, key_len);
   p.tag_len = (uint32_t)tag_len;
   p.version = 0x0303;
-  // on this thread's call stream, not waited for: installs of concurrent
-  // threads overlap, and the context's first call is ordered after it
-  const int rc = install_one(st->sess, st->slot, p, &st->installed);
+  // deferred (round 5) where the first call can take the doorbell: nothing is
+  // launched here, the first call installs the host-built image; otherwise on
+  // this thread's call stream, not waited for: installs of concurrent threads
+  // overlap, and the context's first call is ordered after it
+  const int rc = (!st->batcher && deferred_install_ok(aead->kind)) ? defer_install(st, p)
+                                                                   : install_one(st->sess, st->slot, p, &st->installed);
   memset(&p, 0, sizeof(p));
   if (rc != TLSGPU_OK) {
+    if (st->img_h) image_give(st->sess->eng->device, st->img_h, st->img_d);
     release_slot(st);
     delete st;
     return 0;
@@ -1621,13 +1715,19 @@ extern "C" int EVP_AEAD_CTX_init(EVP_AEAD_CTX* ctx, const EVP_AEAD* aead, const 
   return 1;
 }
 
+static bool doorbell_scrub(const AeadState* st);
 extern "C" void EVP_AEAD_CTX_cleanup(EVP_AEAD_CTX* ctx) {
   if (ctx->aead == nullptr) return;
   auto* st = (AeadState*)ctx->aead_state;
   if (st) {
-    // scrub the device key material before the slot is reused
-    // (explicit_bzero analogue, e_aes.c:1415-1422), on this thread's stream
-    scrub_slot(st->sess, st->slot);
+    if (st->image.load(std::memory_order_acquire) == 1) {
+      // deferred and never called: no key material reached the device
+      image_give(st->sess->eng->device, st->img_h, st->img_d);
+    } else if (!doorbell_scrub(st)) {
+      // scrub the device key material before the slot is reused
+      // (explicit_bzero analogue, e_aes.c:1415-1422), on this thread's stream
+      scrub_slot(st->sess, st->slot);
+    }
     release_slot(st);
     delete st;
   }
@@ -1762,12 +1862,16 @@ static EvpServer* g_servers[kMaxEvpDevices] = {};
 static std::atomic<EvpServer*> g_ready_servers[kMaxEvpDevices] = {};
 constexpr uint32_t kExitedWord = 32;  // exit marks after the stop word (256 workgroups max)
 static std::mutex g_server_mu;
-// Off by default: TLSGPU_EVP_DOORBELL=<G> (64 is the measured setting) or
-// tlsgpu_evp_set_doorbell turns it on.  The round-4 exit SIGSEGV is explained
-// and fixed by the shutdown contract below; the default is a
-// design choice: a server holds up to G CUs for a lifetime after the last
-// call, which a process that mixes per-call and batch work should opt into.
-constexpr unsigned kDoorbellDefaultGroups = 0;
+// On by default (round 5), G = 64: TLSGPU_EVP_DOORBELL=0 or
+// tlsgpu_evp_set_doorbell(0, 0) turns it off.  The round-4 exit SIGSEGV is
+// explained and removed (thread-exit destructors made HIP
+// calls; the shutdown contract below drains every instance).  Design grounds:
+// the EVP surface's users are per-call callers (an unchanged libssl under
+// LD_PRELOAD), for whom the doorbell is 1.5-6x the launched path and makes
+// init / cleanup launch-free; a process that never calls EVP never creates a
+// server; an instance holds only as many CUs as calling threads (<= G), and
+// only while calls arrive plus one lifetime (5 ms).
+constexpr unsigned kDoorbellDefaultGroups = 64;
 static unsigned g_doorbell_groups = [] {
   const char* v = getenv("TLSGPU_EVP_DOORBELL");
   return v && *v ? (unsigned)strtoul(v, nullptr, 10) : kDoorbellDefaultGroups;
@@ -2209,6 +2313,88 @@ static bool event_spin(hipEvent_t ev) {
   }
 }
 
+// Post the job written into `slot` (the caller's doorbell slot on server sv,
+// EVP device k) and wait for its answer.  1: served; 0: not served and never
+// will be (shutdown) — take the launched path; -1: failure (launch failed, or
+// no answer in 10 s: the slot is then retired and the staging abandoned).
+static int doorbell_post_wait(EvpServer* sv, DoorbellSlot* slot, uint32_t* seq, size_t k,
+                              Staging* stg, uint64_t* t0_out) {
+  if (!server_ensure(sv)) {
+    if (g_evp_shutdown.load(std::memory_order_acquire) == 0) return -1;  // launch failed
+    return 0;  // shutting down: nothing was posted
+  }
+  const uint32_t n = ++*seq;
+  const uint64_t t0 = mono_ns();
+  *t0_out = t0;
+  if (g_test_post_delay_us) usleep(g_test_post_delay_us);  // test hook: a descheduled caller
+  __atomic_store_n(&slot->post, n, __ATOMIC_RELEASE);
+  for (uint64_t spins = 1; __atomic_load_n(&slot->done, __ATOMIC_ACQUIRE) != n; spins++) {
+    __builtin_ia32_pause();
+    if ((spins & 127) == 0) {
+      // the instance the post was meant for may have left before the post
+      // landed (this thread descheduled between server_ensure and the store
+      // for more than half a lifetime): past the deadline, relaunch — the new
+      // instance picks the post up
+      const int sd = g_evp_shutdown.load(std::memory_order_acquire);
+      if (sd == 0 && !server_ensure(sv) && g_evp_shutdown.load() == 0) return -1;
+      if (sd == 2) {  // drained: no instance will ever serve it
+        if (__atomic_load_n(&slot->done, __ATOMIC_ACQUIRE) == n) return 1;
+        t_slots.slot[k] = -1;  // this thread posts no more
+        return 0;
+      }
+      const uint64_t waited = mono_ns() - t0;
+      if (waited > 10000000000ull) {  // 10 s: the device is gone
+        // the post stays outstanding: retire the slot (never handed out
+        // again) and leave the staging buffer to the job that may still run
+        // (never freed, never reused)
+        t_slots.slot[k] = -1;
+        stg->abandon();
+        return -1;
+      }
+      if (waited > g_doorbell_yield_ns) sched_yield();  // let other callers post
+    }
+  }
+  return 1;
+}
+
+static bool doorbell_enabled() {
+  return g_doorbell_groups != 0 && g_evp_shutdown.load(std::memory_order_acquire) == 0;
+}
+static bool deferred_install_ok(int kind) {
+  return g_deferred_install && !g_device_install && g_evp_zerocopy && doorbell_enabled() &&
+         (kind == TLSGPU_AES_128_GCM || kind == TLSGPU_AES_256_GCM ||
+          kind == TLSGPU_CHACHA20_POLY1305);
+}
+
+// EVP_AEAD_CTX_cleanup through the doorbell (round 5): a scrub job zeroes the
+// slot on the device and the server's LDS copies of this key, synchronously —
+// no launch.  false: no server / slot for this thread (the caller scrubs on a
+// stream instead).
+static bool doorbell_scrub(const AeadState* st) {
+  if (st->batcher || !g_evp_zerocopy || !doorbell_enabled() ||
+      st->install_pending.load(std::memory_order_acquire))
+    return false;
+  tlsgpu_engine* e = st->sess->eng;
+  EvpServer* sv = evp_server(st->evp_dev, e);
+  uint32_t* seq = nullptr;
+  DoorbellSlot* slot = sv ? thread_slot(sv, st->evp_dev, &seq) : nullptr;
+  Staging* stg = slot ? stage_for(e->device) : nullptr;
+  if (!stg || !stg->ensure(e->device, 64) || !stg->h_dev) return false;
+  int32_t* status = reinterpret_cast<int32_t*>(stg->h_buf);
+  *status = -1;
+  slot->op = kDoorbellOpScrub << 8;
+  slot->n_sessions = st->sess->capacity;
+  memset(&slot->job, 0, sizeof(RawJob));
+  slot->job.session = st->slot;
+  slot->status = (uint64_t)stg->h_dev;
+  slot->sessions = (uint64_t)st->sess->d_sess;
+  slot->gcm_tables = (uint64_t)st->sess->d_gcm;
+  slot->key_id = st->key_id;
+  uint64_t t0 = 0;
+  return doorbell_post_wait(sv, slot, seq, st->evp_dev, stg, &t0) == 1 &&
+         __atomic_load_n(status, __ATOMIC_ACQUIRE) == 0;
+}
+
 static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, size_t* out_len,
                          size_t max_out_len, const unsigned char* nonce, size_t nonce_len,
                          const unsigned char* in, size_t in_len, const unsigned char* ad,
@@ -2223,6 +2409,36 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
     int r = evp_queue_call(st->batcher, st, seal, out, out_len, max_out_len, nonce, nonce_len,
                            in, in_len, ad, ad_len);
     if (r != -2) return r;
+  }
+  // a deferred install (EVP_AEAD_CTX_init, round 5): one caller installs the
+  // image with its call, concurrent first callers wait for it; a failed call
+  // leaves the image waiting for the next one
+  struct InstallClaim {
+    const AeadState* st;
+    bool active = false;
+    ~InstallClaim() {
+      if (active) st->image.store(1, std::memory_order_release);
+    }
+    void done() {  // on the device: the image buffer goes back, zeroed
+      active = false;
+      st->image.store(0, std::memory_order_release);
+      image_give(st->sess->eng->device, st->img_h, st->img_d);
+    }
+  } claim{st};
+  if (st->image.load(std::memory_order_acquire) != 0) {
+    int expect = 1;
+    if (st->image.compare_exchange_strong(expect, 2, std::memory_order_acq_rel)) {
+      claim.active = true;
+      // the slot's previous owner's scrub, if it went through a stream
+      if (hipEventQuery(st->slot_ev) != hipSuccess && hipEventSynchronize(st->slot_ev) != hipSuccess)
+        return -1;
+    } else {
+      for (uint64_t spins = 1; st->image.load(std::memory_order_acquire) != 0; spins++) {
+        __builtin_ia32_pause();
+        if ((spins & 255) == 0) sched_yield();
+        if (spins > (1ull << 34)) return -1;
+      }
+    }
   }
   auto al = [](size_t v) { return (v + 15) & ~(size_t)15; };
   const size_t out_bytes = seal ? in_len + st->tag_len : std::max(max_out_len, in_len);
@@ -2273,57 +2489,32 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
     if (slot && !st->install_pending.load(std::memory_order_acquire)) {
       // the job travels in the slot (one wave load brings it to the server),
       // nonce and AAD inline when they fit
-      const bool inl = nonce_len + ad_len <= kDoorbellInline;
+      // (an installing call carries the image's address in `inl` instead)
+      const bool inl = !claim.active && nonce_len + ad_len <= kDoorbellInline;
       const uint32_t kop = st->kind == TLSGPU_AES_128_GCM   ? 10u
                            : st->kind == TLSGPU_AES_256_GCM ? 14u
                                                             : 20u;  // ChaCha (evp_server.hip)
-      slot->op = (uint32_t)(seal ? 1 : 0) | (kop << 8) | (inl ? 1u << 16 : 0u);
+      slot->op = (uint32_t)(seal ? 1 : 0) | (kop << 8) | (inl ? 1u << 16 : 0u) |
+                 (claim.active ? kDoorbellOpInstall : 0u) |
+                 (claim.active && st->img_tables ? kDoorbellOpInstallTables : 0u);
       slot->n_sessions = st->sess->capacity;
       memcpy(&slot->job, j, sizeof(RawJob));
       if (inl) {
         if (nonce_len) memcpy(slot->inl, nonce, nonce_len);
         if (ad_len) memcpy(slot->inl + nonce_len, ad, ad_len);
+      } else if (claim.active) {
+        const uint64_t img = (uint64_t)st->img_d;
+        memcpy(slot->inl, &img, sizeof(img));
       }
       slot->status = (uint64_t)(d + o_status);
       slot->sessions = (uint64_t)st->sess->d_sess;
       slot->gcm_tables = (uint64_t)st->sess->d_gcm;
       slot->key_id = st->key_id;
-      if (!server_ensure(sv)) {
-        if (g_evp_shutdown.load(std::memory_order_acquire) == 0) return -1;  // launch failed
-        goto launched;  // shutting down: nothing was posted
-      }
-      const uint32_t n = ++*seq;
-      const uint64_t t0 = mono_ns();
-      {
-        if (g_test_post_delay_us) usleep(g_test_post_delay_us);  // test hook: a descheduled caller
-        __atomic_store_n(&slot->post, n, __ATOMIC_RELEASE);
-        for (uint64_t spins = 1; __atomic_load_n(&slot->done, __ATOMIC_ACQUIRE) != n; spins++) {
-          __builtin_ia32_pause();
-          if ((spins & 127) == 0) {
-            // the instance the post was meant for may have left before the
-            // post landed (this thread descheduled between server_ensure and
-            // the store for more than half a lifetime): past the deadline,
-            // relaunch — the new instance picks the post up
-            const int sd = g_evp_shutdown.load(std::memory_order_acquire);
-            if (sd == 0 && !server_ensure(sv) && g_evp_shutdown.load() == 0) return -1;
-            if (sd == 2) {  // drained: no instance will ever serve it
-              if (__atomic_load_n(&slot->done, __ATOMIC_ACQUIRE) == n) break;
-              t_slots.slot[st->evp_dev] = -1;  // this thread posts no more
-              goto launched;
-            }
-            const uint64_t waited = mono_ns() - t0;
-            if (waited > 10000000000ull) {  // 10 s: the device is gone
-              // the post stays outstanding: retire the slot (never handed out
-              // again) and leave the staging buffer to the job that may still
-              // run (never freed, never reused)
-              t_slots.slot[st->evp_dev] = -1;
-              stg->abandon();
-              return -1;
-            }
-            if (waited > g_doorbell_yield_ns) sched_yield();  // let other callers post
-          }
-        }
-      }
+      uint64_t t0 = 0;
+      const int pr = doorbell_post_wait(sv, slot, seq, st->evp_dev, stg, &t0);
+      if (pr < 0) return -1;
+      if (pr == 0) goto launched;
+      if (claim.active) claim.done();
       sv->jobs.fetch_add(1, std::memory_order_relaxed);
       if (sv->trace) {
         const uint64_t* tr = sv->trace + kTraceWords * (size_t)(slot - sv->slots);
@@ -2364,6 +2555,12 @@ launched:
   a.records_per_group = 1;
   a.status = reinterpret_cast<int32_t*>(d + o_status);
   a.n_sessions = st->sess->capacity;
+  // a deferred install on the launched path: one upload kernel ahead of the job
+  if (claim.active && (hipStreamWaitEvent(s, st->slot_ev, 0) != hipSuccess ||
+                       launch_upload_session(st->img_d, st->sess->d_sess + st->slot,
+                                             st->sess->d_gcm + st->slot,
+                                             st->img_tables ? kGcmTableUploadBytes : 0u, s) != 0))
+    return -1;
   int rc = gcm ? launch_gcm(a, seal, true, st->kind == TLSGPU_AES_128_GCM ? 10 : 14, 1, s)
                : launch_chacha(a, seal, true, true, true, s);
   if (rc) return -1;
@@ -2374,6 +2571,7 @@ launched:
       hipEventRecord(stg->done, s) != hipSuccess || !event_spin(stg->done))
     return -1;
   st->install_pending.store(false, std::memory_order_release);  // done before this call's work
+  if (claim.active) claim.done();
   if (stg->any_dirty_key_area()) stg->sweep_key_areas();  // this context's image, copied by now
   const int32_t status = *reinterpret_cast<const int32_t*>(h + o_status);
   if (status < 0) {  // the kernel's zero-fill of max_out_len bytes (evp_aead.c:137-143)

@@ -70,6 +70,11 @@ __device__ __forceinline__ const uint8_t* tg_stage_src() { return s_lds + SRV_ST
 namespace tg {
 
 constexpr uint32_t kSrvExit = 0xFFFFFFFFu;
+// DoorbellSlot::op beyond bit 0 (seal), bits 8-15 (10 / 14 AES rounds, 20
+// ChaCha) and bit 16 (inline nonce / AAD) — engine.cpp writes the same bits
+constexpr uint32_t kOpInstall = kDoorbellOpInstall;            // the image at inl[0..7] first
+constexpr uint32_t kOpInstallTables = kDoorbellOpInstallTables;  // ... with its GCM tables
+constexpr uint32_t kOpScrub = kDoorbellOpScrub;                  // zero the slot (bits 8-15)
 constexpr uint32_t SRV_SEL_OFF = PLAN_OFF + 16 * 16;  // after gcm_raw_job's part_y words
 static_assert(SRV_SEL_OFF + 4 <= PLAN_OFF + 272, "gcm_raw_job's E_K(J0) word follows");
 constexpr uint32_t SRV_SLOT_OFF = PLAN_OFF + 512;     // LDS copy of the picked slot (256 B)
@@ -183,8 +188,16 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
         const uint32_t kop = (opw >> 8) & 0xFFu;
         const uint32_t sid = __builtin_amdgcn_readlane(w, kSlotWordSid);
         const uint32_t key = __builtin_amdgcn_readlane(w, kSlotWordKey);
-        if ((kop == 10 || kop == 14) && sid < (uint32_t)__builtin_amdgcn_readlane(w, kSlotWordNSess) &&
-            key != 0 && key != sess_key) {
+        if (opw & kOpInstall) {
+          // the context's image is installed below by every wave, which also
+          // fills the LDS DevSession copy (a ChaCha image too: the copy then
+          // holds no GCM key's session)
+          sess_key = (kop == 10 || kop == 14) ? key : 0u;
+        } else if (kop == kOpScrub) {
+          sess_key = 0;  // the scrub below zeroes the LDS copy
+        } else if ((kop == 10 || kop == 14) &&
+                   sid < (uint32_t)__builtin_amdgcn_readlane(w, kSlotWordNSess) && key != 0 &&
+                   key != sess_key) {
           const uint64_t sp = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(w, kSlotWordSessions + 1) << 32) |
                               (uint32_t)__builtin_amdgcn_readlane(w, kSlotWordSessions);
           const uint4* src = reinterpret_cast<const uint4*>(sp) + (size_t)sid * (sizeof(DevSession) / 16);
@@ -214,6 +227,58 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
     const uint32_t sid = __builtin_amdgcn_readfirstlane(c->job.session);
     if (((op >> 8) == 10 || (op >> 8) == 14) && sid < a.n_sessions && key != 0)  // GCM: LDS copy
       a.sessions = reinterpret_cast<const DevSession*>(s_lds + SRV_SESS_OFF) - sid;
+    if (c->op & kOpInstall) {
+      // EVP_AEAD_CTX_init's deferred install (round 5, engine.cpp): the image
+      // the host built (session_host.cpp) goes from pinned memory into the
+      // slot in HBM, and the DevSession also into the LDS copy, before the job
+      // reads either; the GCM tables only when bit 18 says the image has them
+      const uint4* img = reinterpret_cast<const uint4*>(
+          *reinterpret_cast<const unsigned long long*>(&c->inl[0]));
+      uint4* dsess = reinterpret_cast<uint4*>(const_cast<DevSession*>(
+          reinterpret_cast<const DevSession*>(c->sessions) + sid));
+      uint4* dtab = reinterpret_cast<uint4*>(const_cast<DevGcmTables*>(
+          reinterpret_cast<const DevGcmTables*>(c->gcm_tables) + sid));
+      constexpr uint32_t kS = sizeof(DevSession) / 16;
+      const uint32_t nw = kS + ((c->op & kOpInstallTables) ? kGcmTableUploadBytes / 16 : 0u);
+      if (sid < a.n_sessions) {
+        for (uint32_t i = threadIdx.x; i < nw; i += kThreads) {
+          const uint4 v = img[i];
+          if (i < kS) {
+            dsess[i] = v;
+            reinterpret_cast<uint4*>(s_lds + SRV_SESS_OFF)[i] = v;
+          } else {
+            dtab[i - kS] = v;
+          }
+        }
+      }
+      __threadfence();  // the slot's HBM copy before this job's table loads
+      __syncthreads();
+    }
+    if (op >> 8 == kOpScrub) {
+      // EVP_AEAD_CTX_cleanup (e_aes.c:1415-1422 explicit_bzero analogue): the
+      // slot's DevSession and GCM tables zeroed in HBM, and this workgroup's
+      // LDS copies of them when they are this key's
+      uint4* dsess = reinterpret_cast<uint4*>(const_cast<DevSession*>(
+          reinterpret_cast<const DevSession*>(c->sessions) + sid));
+      uint4* dtab = reinterpret_cast<uint4*>(const_cast<DevGcmTables*>(
+          reinterpret_cast<const DevGcmTables*>(c->gcm_tables) + sid));
+      constexpr uint32_t kS = sizeof(DevSession) / 16, kT = sizeof(DevGcmTables) / 16;
+      const uint4 z = make_uint4(0, 0, 0, 0);
+      if (sid < a.n_sessions)
+        for (uint32_t i = threadIdx.x; i < kS + kT; i += kThreads) {
+          if (i < kS) dsess[i] = z;
+          else dtab[i - kS] = z;
+        }
+      if (key != 0 && key == cached_key) {  // the byte table (64 KiB at KT_OFF) and Shoup copy
+        for (uint32_t i = threadIdx.x; i < (R4_OFF - KT_OFF) / 16; i += kThreads)
+          if (KT_OFF + 16 * i < AES_OFF || KT_OFF + 16 * i >= SH_OFF)
+            reinterpret_cast<uint4*>(s_lds + KT_OFF)[i] = z;
+        cached_key = 0;
+      }
+      if (threadIdx.x < kS) reinterpret_cast<uint4*>(s_lds + SRV_SESS_OFF)[threadIdx.x] = z;
+      __syncthreads();
+      if (threadIdx.x == 0) a.status[0] = 0;
+    }
     const bool hit = key != 0 && key == cached_key;
     // the table cache is keyed only on a job that really loaded (or kept)
     // its session's tables; a job rejected by the session check before the
@@ -226,6 +291,7 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
       case (14 << 8) | 1: cached_key = gcm_raw_job<true, 14>(a, 0, hit) ? key : 0; break;
       case 20 << 8: srv_chacha_job<false>(a, c->job); break;
       case (20 << 8) | 1: srv_chacha_job<true>(a, c->job); break;
+      case kOpScrub << 8: break;  // done above
       default:  // not a job this server runs (the host never posts one)
         if (threadIdx.x == 0) a.status[0] = TLSGPU_REC_PUBLIC_INVALID;
         cached_key = 0;

@@ -669,6 +669,70 @@ __device__ void fused_prologue(const BatchArgs& a, RecPre* __restrict__ pre, uin
   __threadfence_block();  // the statuses and constants before this workgroup's main loop
 }
 
+// Inclusive prefix sum of one value per thread over the workgroup, and the
+// total; `tmp` holds NT/64 words of LDS.  Every thread calls it.
+template <int NT>
+__device__ uint64_t block_scan_incl(uint64_t v, uint64_t* tmp, uint64_t* total) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint64_t u = __shfl_up(v, d);
+    if (lane >= d) v += u;
+  }
+  if (lane == 63) tmp[wave] = v;
+  __syncthreads();
+  uint64_t off = 0, tot = 0;
+  for (uint32_t w = 0; w < (uint32_t)NT / 64; w++) {
+    const uint64_t t = tmp[w];
+    off += w < wave ? t : 0;
+    tot += t;
+  }
+  __syncthreads();  // tmp is reused by the next scan
+  *total = tot;
+  return v + off;
+}
+
+// Work-balanced ranges (round 5, a.cut_work): cut k of gridDim.x is the first
+// record i whose work prefix W(i) = sum_{j<i} cut_work_of(D[j]) reaches
+// total * k / G.  W is strictly increasing (every weight > 0), so the cuts are
+// non-decreasing with cut(0) = 0 and cut(G) = n, and the two workgroups that
+// share a cut compute it from the same sums: the ranges partition the batch.
+// The count-range sums (range_work_kernel) locate the range the cut falls in;
+// a scan of that range's records finds the record.  LDS: PLAN_OFF (free
+// until the main loop).
+template <int NT>
+__device__ uint32_t work_cut(const BatchArgs& a, uint32_t k) {
+  const uint32_t G = gridDim.x;
+  if (k == 0) return 0;
+  if (k >= G) return a.n;
+  const tlsgpu_record* D = reinterpret_cast<const tlsgpu_record*>(a.descs);
+  uint64_t* tmp = reinterpret_cast<uint64_t*>(s_lds + PLAN_OFF);
+  uint64_t* res = tmp + NT / 64;  // [0] range, [1] work before it, [2] the cut
+  const uint64_t v = threadIdx.x < G ? a.cut_work[threadIdx.x] : 0;
+  uint64_t total;
+  const uint64_t incl = block_scan_incl<NT>(v, tmp, &total);
+  const uint64_t target = total * k / G;  // >= 1: total >= 256 n >= G
+  if (threadIdx.x < G && incl - v < target && target <= incl) {
+    res[0] = threadIdx.x;
+    res[1] = incl - v;
+  }
+  __syncthreads();
+  const uint32_t q = (uint32_t)res[0];
+  uint64_t base = res[1];
+  const uint32_t lo = q * a.records_per_group, hi = min(a.n, lo + a.records_per_group);
+  for (uint32_t c = lo; c < hi; c += NT) {  // workgroup-uniform trip count
+    const uint32_t i = c + threadIdx.x;
+    const uint64_t w = i < hi ? cut_work_of(D[i].len_type) : 0;
+    uint64_t tot;
+    const uint64_t in = block_scan_incl<NT>(w, tmp, &tot);
+    if (i < hi && base + in - w < target && target <= base + in) res[2] = i + 1;
+    base += tot;
+  }
+  __syncthreads();
+  const uint32_t cut = (uint32_t)res[2];
+  __syncthreads();  // res is rewritten by the next call
+  return cut;
+}
+
 // NT threads, the first BSW waves bitsliced (0: a pure T-table queue kernel,
 // 16 waves of <= 128 VGPRs), T-table waves NB blocks wide; B16W > 0: the first
 // B16W waves take the packed bitsliced role (hy_b16_record, one per SIMD for
@@ -702,9 +766,13 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
   fill_aes_lds<NT>();
   if (a.dbg && threadIdx.x < 32) reinterpret_cast<unsigned long long*>(s_lds + DBG_OFF)[threadIdx.x] = 0;
 
-  const uint32_t rlo = blockIdx.x * a.records_per_group;
-  const uint32_t rhi = min(a.n, rlo + a.records_per_group);
+  uint32_t rlo = blockIdx.x * a.records_per_group;
+  uint32_t rhi = min(a.n, rlo + a.records_per_group);
   if (BSW == 0 && B16W == 0 && a.fused) {
+    if (a.cut_work) {  // work-balanced ranges (engine.cpp run_batch)
+      rlo = work_cut<NT>(a, blockIdx.x);
+      rhi = work_cut<NT>(a, blockIdx.x + 1);
+    }
     __syncthreads();  // the T-tables
     fused_prologue<SEAL, ROUNDS, NT>(a, const_cast<RecPre*>(pre), rlo, rhi);
   }
@@ -770,7 +838,9 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
             const uint32_t at = sh ? bb + (uint32_t)__builtin_popcountll(sm & below)
                                    : fb + (uint32_t)__builtin_popcountll(lm & below);
             order[at] = (uint16_t)t;
-            plan_need[at] = (uint8_t)nd;
+            // a record left out of the packs (long, or fused and out of
+            // bounds) never starts or joins one: kPackNone stops plan_k
+            plan_need[at] = (uint8_t)(sh ? nd : kPackNone);
           }
         }
         __syncthreads();

@@ -210,7 +210,20 @@ struct BatchArgs {
                                     // check_record_bounds / gcm_prep_kernel launches); descs
                                     // are the caller's, checked against in_bytes / out_bytes
   uint64_t in_bytes, out_bytes;     // fused: sizes of the caller's in / out buffers
+  const unsigned long long* cut_work;  // fused, non-null: the work of each count range
+                                       // (range_work_kernel); each workgroup takes the
+                                       // records between its two work cuts instead
 };
+
+// Work-balanced ranges (round 5): a record's work for the cut — its payload
+// bytes plus a per-record cost (parse, J0 / tag, the GHASH finish: about a
+// quarter of a 1 KiB record's time in the queue kernel).  Any positive weight
+// gives a correct partition (each cut is computed the same way by the two
+// workgroups that share it); this one balances the Zipf-length workload.
+constexpr uint32_t kCutRecordWork = 256;
+__host__ __device__ __forceinline__ uint64_t cut_work_of(uint32_t len_type) {
+  return (uint64_t)(len_type & 0xFFFFFFu) + kCutRecordWork;
+}
 
 // Average session-run length below which the per-wave-session kernel (gcm_pw.hip)
 // replaces the queue kernel: a run shorter than the workgroup's wave count leaves
@@ -244,6 +257,7 @@ int launch_gcm(const BatchArgs& a, bool seal, bool raw, int rounds, int groups,
                hipStream_t s);
 int launch_gcm_split(const BatchArgs& a, bool seal, int rounds, hipStream_t s);
 int launch_gcm_prep(const BatchArgs& a, RecPre* pre, bool seal, int rounds, hipStream_t s);
+int launch_range_work(const BatchArgs& a, int groups, unsigned long long* out, hipStream_t s);
 int launch_gcm_queue(const BatchArgs& a, const RecPre* pre, bool seal, int rounds, int groups,
                      hipStream_t s);
 int launch_gcm_queue_b16(const BatchArgs& a, const RecPre* pre, bool seal, int rounds, int groups,
@@ -290,6 +304,12 @@ static_assert(sizeof(RawJob) == 56, "RawJob layout");
 static_assert(sizeof(DoorbellSlot) == 256 && offsetof(DoorbellSlot, job) == 48,
               "DoorbellSlot layout");
 constexpr uint32_t kDoorbellInline = 152;
+// DoorbellSlot::op bits beyond the job (evp_server.hip): install the session
+// image whose device address is in inl[0..7] before the job (deferred
+// EVP_AEAD_CTX_init), with its GCM tables; op code (bits 8-15) 30: scrub the slot
+constexpr uint32_t kDoorbellOpInstall = 1u << 17;
+constexpr uint32_t kDoorbellOpInstallTables = 1u << 18;
+constexpr uint32_t kDoorbellOpScrub = 30;
 struct ServerArgs {
   DoorbellSlot* slots;        // device view of the pinned slot array
   uint32_t nslots;

@@ -354,7 +354,8 @@ int launch_batch(const char* what, const BatchArgs& a, hipStream_t s,
   const int d = stream_dev(what, s);
   const std::pair<const char*, const void*> mem[] = {
       {"sessions", a.sessions}, {"gcm_tables", a.gcm_tables}, {"descs", a.descs}, {"in", a.in},
-      {"out", a.out}, {"status", a.status}, {"sel", a.sel}, {"wg_next", a.wg_next}, {"dbg", a.dbg}};
+      {"out", a.out}, {"status", a.status}, {"sel", a.sel}, {"wg_next", a.wg_next}, {"dbg", a.dbg},
+      {"cut_work", a.cut_work}};
   for (const auto& m : mem) mem_on(what, m.first, m.second, d);
   for (const auto& m : more) mem_on(what, m.first, m.second, d);
   return 0;
@@ -369,6 +370,9 @@ int launch_gcm_split(const BatchArgs& a, bool, int, hipStream_t s) {
 }
 int launch_gcm_prep(const BatchArgs& a, RecPre* pre, bool, int, hipStream_t s) {
   return launch_batch("launch_gcm_prep", a, s, {{"pre", pre}});
+}
+int launch_range_work(const BatchArgs& a, int, unsigned long long* out, hipStream_t s) {
+  return launch_batch("launch_range_work", a, s, {{"out", out}});
 }
 int launch_gcm_queue(const BatchArgs& a, const RecPre* pre, bool, int, int, hipStream_t s) {
   return launch_batch("launch_gcm_queue", a, s, {{"pre", pre}});

@@ -137,9 +137,10 @@ def stub_lib():
 
 
 def test_every_member_call_reaches_its_device(stub_lib):
+    # the stub runs no kernel, so no doorbell server could answer: launched path
     env = dict(os.environ, TLSGPU_LIBRARY=stub_lib, TLSGPU_STUB_DEVICES="3",
-               TLSGPU_DEVICES="0,1,2")
-    for k in ("TLSGPU_EVP_DOORBELL", "TLSGPU_EVP_BATCH_US", "TLSGPU_DEVICE"):
+               TLSGPU_DEVICES="0,1,2", TLSGPU_EVP_DOORBELL="0")
+    for k in ("TLSGPU_EVP_BATCH_US", "TLSGPU_DEVICE"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, "-c", _CHILD, ROOT], env=env, capture_output=True,
                        text=True, timeout=240)

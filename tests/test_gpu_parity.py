@@ -554,6 +554,11 @@ def test_batch_bounds(ta, engine, oracle, mode):
 @pytest.mark.parametrize("hints", [2, 3])
 @pytest.mark.parametrize("name", ["aes-128-gcm", "aes-256-gcm"])
 def test_batch_fused_prologue(ta, engine, oracle, gcm_impl, mode, hints, name):
+    gcm_impl("queue")
+    _fused_case(ta, engine, oracle, mode, hints, name)
+
+
+def _fused_case(ta, engine, oracle, mode, hints, name, lengths=None):
     """The fused queue kernel (round 5, engine.cpp run_batch `fused`): one AES
     key size installed and SESSION_RUNS stated, so the queue kernel is the
     batch's only launch and checks bounds, writes the initial statuses and
@@ -566,7 +571,6 @@ def test_batch_fused_prologue(ta, engine, oracle, gcm_impl, mode, hints, name):
     get REC_OUT_OF_BOUNDS and leave their output untouched."""
     import numpy as np
     from talos_amd.batch import RecordBatch
-    gcm_impl("queue")
     rnd = random.Random(90 + hints)
     kind = KINDS[name]
     params = _mk_sessions(ta, rnd, [kind] * 4)
@@ -574,7 +578,7 @@ def test_batch_fused_prologue(ta, engine, oracle, gcm_impl, mode, hints, name):
     table.install(0, params)
     table.hint(hints)
     osess = _oracle_sessions(oracle, params)
-    lengths = [0, 1, 15, 16, 17, 100, 1000, 16384, 5000, 64, 992, 993, 2000]
+    lengths = lengths or [0, 1, 15, 16, 17, 100, 1000, 16384, 5000, 64, 992, 993, 2000]
     recs = []
     for sid in range(4):                           # session runs of 80 records
         for i in range(80):
@@ -616,6 +620,38 @@ def test_batch_fused_prologue(ta, engine, oracle, gcm_impl, mode, hints, name):
     o = int(descs[252]["out_off"])
     assert (out[o:] == 0xA5).all()                 # nothing written past d_out
     table.close()
+
+
+# 16 KiB records every 40th, the rest 0..17 bytes: a 16 KiB record outweighs
+# a workgroup's share of the work, so some work-balanced ranges are empty
+# (the out-of-bounds records of _fused_case get >= 9 bytes)
+SKEWED_LENGTHS = [16384] + [17, 16, 15, 12, 9] * 7 + [3, 5, 1, 0]
+
+
+@pytest.mark.parametrize("balance", ["0", "2"])
+def test_batch_fused_balanced_ranges(ta, balance):
+    """Work-balanced ranges (round 5, engine.cpp run_batch `balance`,
+    gcm_hybrid.h work_cut): the fused kernel's workgroups take the records
+    between cuts at equal work (payload bytes + 256 per record) instead of
+    equal counts.  TLSGPU_BALANCE=2 cuts the no-pack variant too, 0 neither
+    (the pack variant cuts by default, test_batch_fused_prologue hints = 2).
+    The fused prologue cases — bounds, statuses, tamper, both variants — and a
+    skewed batch whose cuts leave ranges empty, all against the oracle, in a
+    child process with the variable set."""
+    import subprocess
+    code = ("import sys; sys.path[:0] = [%r, %r]\n"
+            "import test_gpu_parity as t, pyoracle as po, talos_amd as ta\n"
+            "ta.load_library(); e = ta.Engine(0); o = po.Oracle()\n"
+            "for name in ('aes-128-gcm', 'aes-256-gcm'):\n"
+            "    for mode in ('seal', 'open'):\n"
+            "        for hints in (2, 3):\n"
+            "            t._fused_case(ta, e, o, mode, hints, name)\n"
+            "            t._fused_case(ta, e, o, mode, hints, name, lengths=t.SKEWED_LENGTHS)\n"
+            "e.close(); print('ok')\n") % (os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle"))
+    env = dict(os.environ, TLSGPU_BALANCE=balance, TLSGPU_GCM_IMPL="queue")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=110,
+                       env=env, cwd=ROOT)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
 
 
 def test_batch_per_wave_session_kernel_forced(ta):
