@@ -498,6 +498,14 @@ int tlsgpu_evp_cipher_stats(uint64_t *programs);
  * optionally resets them.  Fails when the variable is not set. */
 int tlsgpu_debug_phase_stats(tlsgpu_engine *e, unsigned long long *out32, int reset);
 
+/* Diagnostic: per-workgroup timing of the queue kernel.  With
+ * TLSGPU_WG_TIMES=1 in the environment every queue launch writes, per
+ * workgroup g, out[4g..4g+3] = {start, end (100 MHz s_memrealtime ticks),
+ * first record, end record}; this call synchronizes the device and copies the
+ * first `groups` (<= 1024) entries of the last launch.  Fails when the
+ * variable is not set or before the first launch. */
+int tlsgpu_debug_wg_times(tlsgpu_engine *e, unsigned long long *out, unsigned groups);
+
 /* Diagnostic: ECB-encrypt nblocks 16-byte blocks (device memory) under the
  * AES key of GCM session `session` with the bitsliced AES core. */
 int tlsgpu_aes_ecb_bitsliced(tlsgpu_sessions *t, uint32_t session, const uint8_t *d_in,

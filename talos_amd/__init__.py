@@ -136,6 +136,7 @@ def load_library(path: str = LIBPATH) -> C.CDLL:
         "tlsgpu_get_gcm_impl": (i32, []),
         "tlsgpu_aes_ecb_bitsliced": (i32, [vp, u32, vp, vp, u32, vp]),
         "tlsgpu_debug_phase_stats": (i32, [vp, C.POINTER(C.c_ulonglong), i32]),
+        "tlsgpu_debug_wg_times": (i32, [vp, C.POINTER(C.c_ulonglong), C.c_uint]),
         "tlsgpu_open_wire": (i32, [vp, vp, u32, vp, u32, vp, vp, vp, vp, vp]),
         "tlsgpu_open_host": (i32, [vp, vp, u32, vp, C.c_size_t, vp, C.c_size_t, vp]),
         "tlsgpu_seal_wire": (i32, [vp, vp, u32, vp, C.c_size_t, vp, C.c_size_t, u32, vp, vp, vp,
@@ -436,6 +437,14 @@ def debug_phase_stats(engine: "Engine", reset: bool = True) -> list[int]:
     _check(engine.lib.tlsgpu_debug_phase_stats(engine.handle, out, int(reset)),
            "tlsgpu_debug_phase_stats")
     return list(out)
+
+
+def debug_wg_times(engine: "Engine", groups: int) -> list[tuple[int, int, int, int]]:
+    """Diagnostic (TLSGPU_WG_TIMES=1): {start, end, rlo, rhi} per workgroup of the
+    last queue-kernel launch (100 MHz ticks)."""
+    out = (C.c_ulonglong * (4 * groups))()
+    _check(engine.lib.tlsgpu_debug_wg_times(engine.handle, out, groups), "tlsgpu_debug_wg_times")
+    return [tuple(out[4 * g:4 * g + 4]) for g in range(groups)]
 
 
 def aes_ecb_bitsliced(table: "SessionTable", session: int, d_in: int, d_out: int, nblocks: int,

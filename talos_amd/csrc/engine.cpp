@@ -376,6 +376,30 @@ extern "C" int tlsgpu_debug_phase_stats(tlsgpu_engine* e, unsigned long long* ou
   return TLSGPU_OK;
 }
 
+// Diagnostic per-workgroup timing of the queue kernel (TLSGPU_WG_TIMES=1):
+// {start, end, rlo, rhi} of each workgroup of the last queue launch, read with
+// tlsgpu_debug_wg_times (s_memrealtime ticks, 100 MHz).
+static unsigned long long* g_wg_times = nullptr;
+static unsigned long long* wg_times_for(const tlsgpu_engine* e) {
+  static const bool on = [] {
+    const char* v = getenv("TLSGPU_WG_TIMES");
+    return v && *v && *v != '0';
+  }();
+  if (!on) return nullptr;
+  if (!g_wg_times && hipMalloc((void**)&g_wg_times, 4 * 1024 * sizeof(unsigned long long)) == hipSuccess)
+    (void)hipMemset(g_wg_times, 0, 4 * 1024 * sizeof(unsigned long long));
+  (void)e;
+  return g_wg_times;
+}
+extern "C" int tlsgpu_debug_wg_times(tlsgpu_engine* e, unsigned long long* out, unsigned groups) {
+  if (!e || !out || groups > 1024) return fail(TLSGPU_EINVAL, "bad arguments");
+  if (!g_wg_times) return fail(TLSGPU_EINVAL, "TLSGPU_WG_TIMES not set");
+  HIPCHK(hipSetDevice(e->device));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(out, g_wg_times, 4 * (size_t)groups * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return TLSGPU_OK;
+}
+
 // Hybrid-kernel experiment flags (TLSGPU_HY_FLAGS, tlsgpu_internal.h).  Bit 2
 // parks the waves of gcm_hy_kernel that are not bitsliced-pair waves, bit 4 the
 // bitsliced-pair waves.  A setting that parks every wave of the kernel that
@@ -427,13 +451,21 @@ static const bool g_fused = [] {
   const char* v = getenv("TLSGPU_FUSED");
   return !(v && *v == '0');
 }();
-// Work-balanced ranges for the fused kernel (round 5): 0 off, 1 the pack
-// variant (mixed record lengths; the default), 2 always.  Equal record counts
-// per workgroup leave the Zipf workload's slowest CU with 16% more bytes than
-// the mean.
+// Work-balanced ranges for the fused kernel (round 5, TLSGPU_BALANCE): 0 off
+// (the default), 1 the pack variant (mixed record lengths), 2 always.  Equal
+// record counts per workgroup leave the Zipf workload's slowest CU with 16 %
+// more bytes than the mean, but a cut inside a session run costs both of its
+// workgroups a table build, a plan and a run-end wait, and config D measured
+// no faster with equal-work cuts.
 static const uint32_t g_balance = [] {
   const char* v = getenv("TLSGPU_BALANCE");
-  return v && *v ? (uint32_t)strtoul(v, nullptr, 10) : 1u;
+  return v && *v ? (uint32_t)strtoul(v, nullptr, 10) : 0u;
+}();
+// ... and how near a session-run boundary a cut snaps to it, in 1/1024 of a
+// workgroup's share of the work (TLSGPU_BALANCE_SNAP; 0: exact cuts)
+static const uint32_t g_balance_snap = [] {
+  const char* v = getenv("TLSGPU_BALANCE_SNAP");
+  return v && *v ? (uint32_t)strtoul(v, nullptr, 10) : 0u;
 }();
 
 // bounds: {in_bytes, out_bytes} of a caller's TLS batch (checked by a pre-pass
@@ -465,6 +497,7 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   a.bs_reserve = g_bs_reserve;
 
   a.dbg = g_phase_stats;
+  a.wg_times = wg_times_for(t->eng);
   a.bs16_min = g_bs16_min;
   // batch-shape hints rule out the kernels the device would not select
   // (tlsgpu_sessions_hint); the TLSGPU_PACK / TLSGPU_PWS overrides win
@@ -543,6 +576,7 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
       if (launch_range_work(a, groups, cw, s))
         return fail(TLSGPU_EHIP, "range work launch: %s", hipGetErrorString(hipGetLastError()));
       a.cut_work = cw;
+      a.cut_snap = g_balance_snap;
     }
   } else if (bounds) {
     // one setup launch: sanitized descriptors, every record's initial status

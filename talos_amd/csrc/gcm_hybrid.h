@@ -728,7 +728,44 @@ __device__ uint32_t work_cut(const BatchArgs& a, uint32_t k) {
     base += tot;
   }
   __syncthreads();
-  const uint32_t cut = (uint32_t)res[2];
+  uint32_t cut = (uint32_t)res[2];
+  if (a.cut_snap != 0 && cut > 0 && cut < a.n) {
+    // Snap to the nearest session-run boundary when one lies within
+    // a.cut_snap / 1024 of a workgroup's share of the work (a split run costs
+    // both workgroups a table build, a plan and a run-end wait): rs = the last
+    // boundary <= cut, re = the first >= cut, each looked for within NT
+    // records.  Monotone in the target — two targets in one run find the same
+    // boundaries and the nearer-boundary rule never crosses them over — so
+    // the cuts still partition the batch.
+    const uint32_t i = cut;
+    uint32_t* bnd = reinterpret_cast<uint32_t*>(res + 3);  // [0] i - rs, [1] re - i
+    if (threadIdx.x < 2) bnd[threadIdx.x] = 0xFFFFFFFFu;
+    __syncthreads();
+    const uint32_t t = threadIdx.x;
+    if (t < i) {  // p = i - t; a boundary at p: D[p - 1] and D[p] in different sessions
+      const uint32_t p = i - t;
+      if (D[p].session != D[p - 1].session) atomicMin(bnd, t);
+    } else if (t == i) {
+      atomicMin(bnd, t);  // p = 0
+    }
+    if (i + t <= a.n) {
+      const uint32_t p = i + t;
+      if (p == a.n || D[p].session != D[p - 1].session) atomicMin(bnd + 1, t);
+    }
+    __syncthreads();
+    const uint32_t dlr = bnd[0], drr = bnd[1];
+    const uint64_t wl = t < dlr && dlr != 0xFFFFFFFFu ? cut_work_of(D[i - 1 - t].len_type) : 0;
+    const uint64_t wr = t < drr && drr != 0xFFFFFFFFu ? cut_work_of(D[i + t].len_type) : 0;
+    uint64_t dl, dr;
+    (void)block_scan_incl<NT>(wl, tmp, &dl);
+    (void)block_scan_incl<NT>(wr, tmp, &dr);
+    const uint64_t thr = total / G * a.cut_snap / 1024;
+    const bool has_l = dlr != 0xFFFFFFFFu, has_r = drr != 0xFFFFFFFFu;
+    if (dlr != 0 && drr != 0) {  // not on a boundary already
+      if (has_l && dl < thr && (!has_r || dl <= dr)) cut = i - dlr;
+      else if (has_r && dr < thr && (!has_l || dr < dl)) cut = i + drr;
+    }
+  }
   __syncthreads();  // res is rewritten by the next call
   return cut;
 }
@@ -763,6 +800,7 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
   if (B16W > 0 && !b16_role && !(a.hy_flags & 8u)) __builtin_amdgcn_s_setprio(1);
   uint32_t* q = reinterpret_cast<uint32_t*>(s_lds + Q_OFF);
 
+  if (a.wg_times && threadIdx.x == 0) a.wg_times[4 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
   fill_aes_lds<NT>();
   if (a.dbg && threadIdx.x < 32) reinterpret_cast<unsigned long long*>(s_lds + DBG_OFF)[threadIdx.x] = 0;
 
@@ -794,15 +832,31 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
     const uint32_t run_cap = packing ? min(rhi, pos + kPlanCap) : rhi;
     bool has_short = packing && pack_need<SEAL>(as_const(&D[pos].len_type)[0], tag_len) <= kPackMaxNeed;
     uint32_t run_end = pos + 1;
+    // the run's end: 4 x 64 descriptors per memory round trip (the scan is
+    // on the run-to-run critical path of the wave that finished last; round 5,
+    // same-box A/B against one 64-record step per trip: B +0.3 %, D +0.2 %,
+    // profiles/r05j_ab_run_scan.txt)
     while (run_end < run_cap) {
-      uint32_t p = run_end + lane;
-      uint32_t s = p < run_cap ? D[p].session : sid;
-      if (packing)  // a hint only: records past the run's end may count
-        has_short |= __ballot(p < run_cap && s == sid &&
-                              pack_need<SEAL>(D[p].len_type, tag_len) <= kPackMaxNeed) != 0;
-      uint64_t diff = __ballot(p < run_cap && s != sid);
-      if (diff) { run_end += __builtin_amdgcn_readfirstlane((uint32_t)__builtin_ctzll(diff)); break; }
-      run_end = min(run_cap, run_end + 64);
+      uint32_t s[4], lt[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; u++) {
+        const uint32_t p = run_end + 64u * u + lane;
+        s[u] = p < run_cap ? D[p].session : sid;
+        lt[u] = packing && p < run_cap ? D[p].len_type : 0u;
+      }
+      uint32_t found = 0xFFFFFFFFu;
+#pragma unroll
+      for (uint32_t u = 0; u < 4; u++) {
+        const uint32_t p = run_end + 64u * u + lane;
+        if (packing)  // a hint only: records past the run's end may count
+          has_short |= __ballot(p < run_cap && s[u] == sid &&
+                                pack_need<SEAL>(lt[u], tag_len) <= kPackMaxNeed) != 0;
+        const uint64_t diff = __ballot(p < run_cap && s[u] != sid);
+        if (diff && found == 0xFFFFFFFFu)
+          found = 64u * u + __builtin_amdgcn_readfirstlane((uint32_t)__builtin_ctzll(diff));
+      }
+      if (found != 0xFFFFFFFFu) { run_end += found; break; }
+      run_end = min(run_cap, run_end + 256);
     }
     const uint32_t kind = as_const(&S->kind)[0];
     const bool usable = in_range && is_gcm(kind) && (int)as_const(&S->rounds)[0] == ROUNDS;
@@ -947,6 +1001,14 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
     __syncthreads();
     if (threadIdx.x < 32)
       atomicAdd(a.dbg + threadIdx.x, reinterpret_cast<unsigned long long*>(s_lds + DBG_OFF)[threadIdx.x]);
+  }
+  if (a.wg_times) {  // diagnostic: when the workgroup's last wave is done, and its range
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      a.wg_times[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+      a.wg_times[4 * blockIdx.x + 2] = rlo;
+      a.wg_times[4 * blockIdx.x + 3] = rhi;
+    }
   }
 }
 

@@ -213,6 +213,10 @@ struct BatchArgs {
   const unsigned long long* cut_work;  // fused, non-null: the work of each count range
                                        // (range_work_kernel); each workgroup takes the
                                        // records between its two work cuts instead
+  uint32_t cut_snap;                // cut_work: snap a cut to a session-run boundary within
+                                    // cut_snap / 1024 of a share of the work (0: exact cuts)
+  unsigned long long* wg_times;     // diagnostic (TLSGPU_WG_TIMES=1), normally null: per
+                                    // workgroup {start, end (s_memrealtime), rlo, rhi}
 };
 
 // Work-balanced ranges (round 5): a record's work for the cut — its payload
