@@ -19,6 +19,9 @@
 // h_le and basis little-endian words of the 16-byte string; shoup entries the
 // big-endian 32-bit words (gcm128.c's u128 hi/lo as four words).
 #include <cstring>
+#if !defined(__HIP_DEVICE_COMPILE__)
+#include <immintrin.h>
+#endif
 
 #include "aes_common.h"
 #include "tlsgpu_internal.h"
@@ -83,6 +86,47 @@ U128 gmult_4bit(U128 x, const U128 (&m)[16]) {
   }
   return z;
 }
+
+#if !defined(__HIP_DEVICE_COMPILE__)
+// x * y with the carry-less multiply (the host's PCLMULQDQ), GCM's bit order:
+// the 16-byte strings as 128-bit big-endian integers (lo qword = U128::lo),
+// the product shifted left by one for the reflected convention, reduced
+// modulo x^128 + x^7 + x^2 + x + 1 (Intel's GCM white paper, Algorithm 5).
+// tests/test_session_image.py pins the products against gmult_4bit's model.
+__attribute__((target("pclmul,sse4.1"))) U128 gmult_clmul(U128 x, U128 y) {
+  const __m128i a = _mm_set_epi64x((long long)x.hi, (long long)x.lo);
+  const __m128i b = _mm_set_epi64x((long long)y.hi, (long long)y.lo);
+  __m128i t3 = _mm_clmulepi64_si128(a, b, 0x00);
+  __m128i t4 = _mm_clmulepi64_si128(a, b, 0x10);
+  __m128i t5 = _mm_clmulepi64_si128(a, b, 0x01);
+  __m128i t6 = _mm_clmulepi64_si128(a, b, 0x11);
+  t4 = _mm_xor_si128(t4, t5);
+  t5 = _mm_slli_si128(t4, 8);
+  t4 = _mm_srli_si128(t4, 8);
+  t3 = _mm_xor_si128(t3, t5);
+  t6 = _mm_xor_si128(t6, t4);  // 256-bit product t6:t3
+  __m128i t7 = _mm_srli_epi32(t3, 31), t8 = _mm_srli_epi32(t6, 31);
+  t3 = _mm_slli_epi32(t3, 1);
+  t6 = _mm_slli_epi32(t6, 1);
+  __m128i t9 = _mm_srli_si128(t7, 12);
+  t8 = _mm_slli_si128(t8, 4);
+  t7 = _mm_slli_si128(t7, 4);
+  t3 = _mm_or_si128(t3, t7);
+  t6 = _mm_or_si128(_mm_or_si128(t6, t8), t9);  // shifted left by one
+  t7 = _mm_xor_si128(_mm_xor_si128(_mm_slli_epi32(t3, 31), _mm_slli_epi32(t3, 30)),
+                     _mm_slli_epi32(t3, 25));
+  t8 = _mm_srli_si128(t7, 4);
+  t7 = _mm_slli_si128(t7, 12);
+  t3 = _mm_xor_si128(t3, t7);
+  __m128i t2 = _mm_xor_si128(_mm_xor_si128(_mm_srli_epi32(t3, 1), _mm_srli_epi32(t3, 2)),
+                             _mm_srli_epi32(t3, 7));
+  t2 = _mm_xor_si128(t2, t8);
+  t3 = _mm_xor_si128(t3, t2);
+  t6 = _mm_xor_si128(t6, t3);
+  return U128{(uint64_t)_mm_extract_epi64(t6, 1), (uint64_t)_mm_cvtsi128_si64(t6)};
+}
+const bool g_have_clmul = __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1");
+#endif
 
 inline uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 
@@ -152,7 +196,8 @@ void aes_encrypt(const uint32_t* rk_be, int rounds, uint8_t s[16]) {
 // zero for invalid parameters, kind 0), *t only for AES-GCM (returns true).
 // The caller's buffers may hold anything; every byte install_body writes is
 // written here.
-bool host_session_image(const tlsgpu_session_params& p, DevSession* s, DevGcmTables* t) {
+bool host_session_image(const tlsgpu_session_params& p, DevSession* s, DevGcmTables* t,
+                        bool bitsliced_masks) {
   memset(s, 0, sizeof(*s));
   const bool gcm = p.aead == TLSGPU_AES_128_GCM || p.aead == TLSGPU_AES_256_GCM;
   const bool cc = p.aead == TLSGPU_CHACHA20_POLY1305 || p.aead == TLSGPU_CHACHA20_POLY1305_OLD;
@@ -186,11 +231,14 @@ bool host_session_image(const tlsgpu_session_params& p, DevSession* s, DevGcmTab
     H.lo = (H.lo << 8) | hb[8 + k];
   }
   store_le(s->h_le, H);
-  // bitsliced AddRoundKey masks (the experimental kernels): rows 0..rounds
-  for (uint32_t w = 0; w < 128u * (uint32_t)(rounds + 1); w++) {
-    const uint32_t r = w / 128, b = (w % 128) / 8, k = w % 8;
-    t->bsrk[r][8 * b + k] = 0u - ((s->rk[4 * r + b / 4] >> (8 * (b % 4) + k)) & 1u);
-  }
+  // bitsliced AddRoundKey masks (the experimental kernels, the only readers:
+  // kGcmTableUploadBytes leaves them out of the default build's uploads)
+  if (bitsliced_masks)
+    for (int r = 0; r <= rounds; r++)
+      for (uint32_t b = 0; b < 16; b++) {
+        const uint32_t byte = s->rk[4 * r + b / 4] >> (8 * (b % 4));
+        for (uint32_t k = 0; k < 8; k++) t->bsrk[r][8 * b + k] = 0u - ((byte >> k) & 1u);
+      }
   // H^1 .. H^65 and their Shoup tables; basis[q] = H^64 * x^q
   U128 mh[16];
   shoup_table(H, mh);
@@ -205,6 +253,12 @@ bool host_session_image(const tlsgpu_session_params& p, DevSession* s, DevGcmTab
         b = mulx(b);
       }
     }
+#if !defined(__HIP_DEVICE_COMPILE__)
+    if (g_have_clmul) {
+      pw = gmult_clmul(pw, H);
+      continue;
+    }
+#endif
     pw = gmult_4bit(pw, mh);
   }
   memset(rk_be, 0, sizeof(rk_be));
@@ -221,6 +275,6 @@ extern "C" int tlsgpu_session_image(const tlsgpu_session_params* p, uint8_t* out
   auto* s = reinterpret_cast<tg::DevSession*>(out);
   auto* t = reinterpret_cast<tg::DevGcmTables*>(out + sizeof(tg::DevSession));
   memset(t, 0, sizeof(*t));
-  tg::host_session_image(*p, s, t);
+  tg::host_session_image(*p, s, t, true);
   return TLSGPU_OK;
 }

@@ -348,8 +348,6 @@ int launch_fill_synthetic(uint8_t* d_out, uint64_t stride, uint32_t span_len,
 int launch_upload_session(const void* img, DevSession* sess, DevGcmTables* tab,
                           uint32_t table_bytes, hipStream_t s);
 int launch_scrub_session(DevSession* sess, DevGcmTables* tab, hipStream_t s);
-// session_host.cpp: the image install_body writes, built on the host
-bool host_session_image(const tlsgpu_session_params& p, DevSession* s, DevGcmTables* t);
 // GCM table bytes the default kernels read (basis + Shoup tables; the
 // bitsliced masks only in the experimental build)
 #ifdef TG_EXPERIMENTAL
@@ -357,6 +355,10 @@ constexpr uint32_t kGcmTableUploadBytes = sizeof(DevGcmTables);
 #else
 constexpr uint32_t kGcmTableUploadBytes = offsetof(DevGcmTables, bsrk);
 #endif
+// session_host.cpp: the image install_body writes, built on the host (the
+// bitsliced masks only when a kernel of this build reads them)
+bool host_session_image(const tlsgpu_session_params& p, DevSession* s, DevGcmTables* t,
+                        bool bitsliced_masks = kGcmTableUploadBytes > offsetof(DevGcmTables, bsrk));
 int launch_check_bounds(const tlsgpu_record* recs, tlsgpu_record* safe, uint32_t n,
                         const DevSession* sessions, uint32_t n_sessions, uint64_t in_bytes,
                         uint64_t out_bytes, bool seal, int32_t* status, uint32_t* ctl,
