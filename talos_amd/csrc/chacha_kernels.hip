@@ -253,10 +253,23 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
   uint32_t sq_hi = 0, sq_lo = 0;
   if (r < a.n) {
     const tlsgpu_record d = reinterpret_cast<const tlsgpu_record*>(a.descs)[r];
+    // fused (round 5, engine.cpp run_batch: a batch of RFC ChaCha sessions
+    // only): the caller's descriptors, checked here by check_record_bounds's
+    // rule, and the initial status of a record this kernel does not run
+    int32_t st0 = TLSGPU_REC_PUBLIC_INVALID;
     if (d.session < a.n_sessions) {  // else the status stays PUBLIC_INVALID
       const DevSession* S = a.sessions + d.session;
       const uint32_t kind = S->kind;
-      if (kind == TLSGPU_CHACHA20_POLY1305) {  // the draft ("old") suite: chacha_batch_kernel
+      bool in_bounds = true;
+      if (a.fused) {
+        const uint64_t len = d.len_type & 0xFFFFFFu, tag = S->tag_len;
+        const uint64_t eiv = S->nonce_in_record ? 8u : 0u;
+        const uint64_t out_len = SEAL ? len + eiv + tag : (len >= eiv + tag ? len - eiv - tag : 0);
+        in_bounds = !(d.in_off > a.in_bytes || len > a.in_bytes - d.in_off ||
+                      d.out_off > a.out_bytes || out_len > a.out_bytes - d.out_off);
+        if (!in_bounds) st0 = TLSGPU_REC_OUT_OF_BOUNDS;
+      }
+      if (kind == TLSGPU_CHACHA20_POLY1305 && in_bounds) {  // the draft ("old") suite: chacha_batch_kernel
         tag_len = S->tag_len;
         const uint32_t len = d.len_type & 0xFFFFFFu, type = d.len_type >> 24;
         if (!SEAL && len < tag_len) {  // t1_enc.c:958-959 (no explicit nonce for ChaCha)
@@ -281,6 +294,7 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
         }
       }
     }
+    if (a.fused && !active) a.status[r] = st0;
   }
   uint8_t* key = keys + 16u * lane;
   lds_wave_sync();

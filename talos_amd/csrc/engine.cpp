@@ -532,9 +532,16 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   // own records in its prologue: no check_record_bounds, no gcm_prep_kernel, no
   // checked-descriptor copy, no variant that exits at once (TLSGPU_FUSED=0
   // keeps the launch sequence with the device-side selection).
-  const bool fused = g_fused && bounds && impl == TLSGPU_GCM_QUEUE && a.pws == 1 &&
-                     (have[TLSGPU_AES_128_GCM] != have[TLSGPU_AES_256_GCM]) &&
-                     !have[TLSGPU_CHACHA20_POLY1305] && !have[TLSGPU_CHACHA20_POLY1305_OLD];
+  const bool fused_gcm = g_fused && bounds && impl == TLSGPU_GCM_QUEUE && a.pws == 1 &&
+                         (have[TLSGPU_AES_128_GCM] != have[TLSGPU_AES_256_GCM]) &&
+                         !have[TLSGPU_CHACHA20_POLY1305] && !have[TLSGPU_CHACHA20_POLY1305_OLD];
+  // ... and the same for a batch of RFC 7539 ChaCha sessions only: the staged
+  // ChaCha kernel checks bounds and writes the statuses of the records it does
+  // not run itself (chacha_kernels.hip cc_tls_wave)
+  const bool fused_cc = g_fused && bounds && !raw && have[TLSGPU_CHACHA20_POLY1305] &&
+                        !have[TLSGPU_CHACHA20_POLY1305_OLD] && !have[TLSGPU_AES_128_GCM] &&
+                        !have[TLSGPU_AES_256_GCM];
+  const bool fused = fused_gcm || fused_cc;
   // per-stream scratch: [RecPre x n (queue kernels) | ctl_bytes control words |
   // checked descriptors x n].  Control words per key size k (0: AES-128, 1:
   // AES-256): selection words (kSelSlots x 64 B) at 1024 k, then one uint32
@@ -543,14 +550,14 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   static_assert(kSelSlots * kSelWords * 4 <= 1024, "selection words exceed their slot");
   const size_t cnt_bytes = ((size_t)groups * 4 + 255) & ~(size_t)255;
   const size_t ctl_bytes = 2048 + 2 * cnt_bytes;
-  const bool balance = fused && groups > 1 && groups <= 1024 &&
+  const bool balance = fused_gcm && groups > 1 && groups <= 1024 &&
                        (g_balance >= 2 || (g_balance == 1 && a.pack != 0));
   const size_t cut_bytes = balance ? ((size_t)groups * 8 + 255) & ~(size_t)255 : 0;
   const size_t pre_bytes =
       gcm_pre ? sizeof(RecPre) * (size_t)n + (fused ? cut_bytes : ctl_bytes) : 0;
   uint8_t* scratch = nullptr;
   uint8_t* pool_scratch = nullptr;
-  if (pre_bytes || bounds) {
+  if (pre_bytes || (bounds && !fused)) {
     const size_t sbytes = pre_bytes + (bounds && !fused ? sizeof(tlsgpu_record) * (size_t)n : 0);
     if (g_pre_pool) {  // diagnostic only (DESIGN.md §4.1 pool scratch): stream-ordered pool
       if (hipMallocAsync((void**)&scratch, sbytes, s) != hipSuccess) scratch = nullptr;

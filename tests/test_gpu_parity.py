@@ -558,6 +558,16 @@ def test_batch_fused_prologue(ta, engine, oracle, gcm_impl, mode, hints, name):
     _fused_case(ta, engine, oracle, mode, hints, name)
 
 
+@pytest.mark.parametrize("mode", ["open", "seal"])
+def test_batch_fused_chacha(ta, engine, oracle, mode):
+    """The fused ChaCha batch (round 5, engine.cpp run_batch `fused_cc`): a
+    table of RFC 7539 ChaCha20-Poly1305 sessions only, so the staged ChaCha
+    kernel is the batch's only launch and checks bounds and writes the statuses
+    of the records it does not run itself (no check_record_bounds, no
+    descriptor copy) — the same cases as the fused GCM prologue."""
+    _fused_case(ta, engine, oracle, mode, 0, "chacha20-poly1305")
+
+
 def _fused_case(ta, engine, oracle, mode, hints, name, lengths=None):
     """The fused queue kernel (round 5, engine.cpp run_batch `fused`): one AES
     key size installed and SESSION_RUNS stated, so the queue kernel is the
