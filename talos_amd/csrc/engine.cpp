@@ -1853,9 +1853,11 @@ static const bool g_evp_zerocopy = [] {
 // after half of that has passed, on the same stream: a job is only posted
 // while an instance that still polls for at least half a lifetime is queued or
 // running, so every posted job is served, and a process that stops calling
-// leaves nothing spinning.  Draft ("old") ChaCha20-Poly1305 contexts, pooled
-// (queued) contexts and a context's first call keep the launched path; a short
-// GCM job's input is staged into LDS by the server's idle waves.
+// leaves nothing spinning.  Draft ("old") ChaCha20-Poly1305 contexts and pooled
+// (queued) contexts keep the launched path; a context's first call carries its
+// deferred install (the host-built image, defer_install) and its cleanup posts
+// a scrub job; a short GCM job's input is staged into LDS by the server's idle
+// waves.  On by default (round 5, kDoorbellDefaultGroups).
 // The lifetime is short on purpose: this box runs at most GPU_MAX_HW_QUEUES = 4
 // hardware queues per process, so with more streams than that (engine + 4 call
 // streams + server) the server's queue is shared, and a kernel launched on a
