@@ -12,7 +12,7 @@
  *
  * usage: cpubench LIB AEAD OP REC_LEN|@lengths.u32 NREC THREADS SECONDS
  *   @file: NREC little-endian uint32 record lengths (the config-D Zipf mix)
- *   AEAD: aes-128-gcm | aes-256-gcm | chacha20-poly1305
+ *   AEAD: aes-128-gcm | aes-256-gcm | chacha20-poly1305 | chacha20-poly1305-old (8-byte nonce)
  *   OP:   open | seal | both  (both = seal then open per record, config C)
  *         init  connection churn: every thread loops EVP_AEAD_CTX_init with a
  *               fresh key + one seal of a REC_LEN record + EVP_AEAD_CTX_cleanup
@@ -37,6 +37,7 @@ typedef int (*crypt_fn)(const EVP_AEAD_CTX *, unsigned char *, size_t *, size_t,
     const unsigned char *, size_t, const unsigned char *, size_t,
     const unsigned char *, size_t);
 
+static size_t g_nonce_len = 12;	/* 8 for the draft ChaCha AEAD */
 static init_fn p_init;
 static crypt_fn p_seal, p_open;
 static void (*p_cleanup)(EVP_AEAD_CTX *);
@@ -111,7 +112,7 @@ churn_worker(void *arg)
 			t->failures++;
 			break;
 		}
-		if (!p_seal(&c, out, &out_len, rec_len + 16, nonce, 12, pt, rec_len, ad, 13))
+		if (!p_seal(&c, out, &out_len, rec_len + 16, nonce, g_nonce_len, pt, rec_len, ad, 13))
 			t->failures++;
 		p_cleanup(&c);
 		t->records++;
@@ -139,12 +140,12 @@ worker(void *arg)
 		int ok = 1;
 		if (op == 0 || op == 2) {
 			if (op == 2)
-				ok &= p_seal(c, out, &out_len, r->len + 16, r->nonce, 12,
+				ok &= p_seal(c, out, &out_len, r->len + 16, r->nonce, g_nonce_len,
 				    r->pt, r->len, r->ad, 13);
-			ok &= p_open(c, out, &out_len, r->len, r->nonce, 12, r->ct,
+			ok &= p_open(c, out, &out_len, r->len, r->nonce, g_nonce_len, r->ct,
 			    r->len + 16, r->ad, 13);
 		} else {
-			ok &= p_seal(c, out, &out_len, r->len + 16, r->nonce, 12, r->pt,
+			ok &= p_seal(c, out, &out_len, r->len + 16, r->nonce, g_nonce_len, r->pt,
 			    r->len, r->ad, 13);
 		}
 		t->failures += !ok;
@@ -193,6 +194,10 @@ main(int argc, char **argv)
 	} else if (!strcmp(argv[2], "aes-256-gcm")) {
 		which = (aead_fn)dlsym(h, "EVP_aead_aes_256_gcm");
 		key_len = 32;
+	} else if (!strcmp(argv[2], "chacha20-poly1305-old")) {
+		which = (aead_fn)dlsym(h, "EVP_aead_chacha20_poly1305_old");
+		key_len = 32;
+		g_nonce_len = 8;
 	} else {
 		which = (aead_fn)dlsym(h, "EVP_aead_chacha20_poly1305");
 		key_len = 32;
@@ -275,7 +280,7 @@ main(int argc, char **argv)
 		fill(0x1234ULL + k, r->ad, 13);
 		r->ad[11] = (unsigned char)(r->len >> 8);
 		r->ad[12] = (unsigned char)r->len;
-		if (!p_seal(&ctxs[r->sess], r->ct, &ol, r->len + 16, r->nonce, 12,
+		if (!p_seal(&ctxs[r->sess], r->ct, &ol, r->len + 16, r->nonce, g_nonce_len,
 		    r->pt, r->len, r->ad, 13)) {
 			fprintf(stderr, "seal failed\n");
 			return 1;

@@ -574,7 +574,7 @@ __global__ __launch_bounds__(256) void chacha_batch_kernel(BatchArgs a) {
 }
 
 // Raw EVP jobs, one wave per job: the RFC 7539 AEAD on the whole wave
-// (chacha_wave.h: per-call latency), the draft AEAD on lane 0 (cc_record).
+// (chacha_wave.h: per-call latency), the draft AEAD too (cc_wave_job_old, round 5).
 template <bool SEAL>
 __global__ __launch_bounds__(kWave) void chacha_raw_wave_kernel(BatchArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t stage[4096];
@@ -594,11 +594,8 @@ __global__ __launch_bounds__(kWave) void chacha_raw_wave_kernel(BatchArgs a) {
   }
   if (kind == TLSGPU_CHACHA20_POLY1305) {
     cc_wave_job<SEAL>(j, S, slot, stage);
-  } else if (kind == TLSGPU_CHACHA20_POLY1305_OLD && threadIdx.x == 0) {
-    CcRec rc;
-    uint32_t tag_len;
-    cc_parse_raw<SEAL>(j, S, rc, tag_len);
-    cc_record<SEAL>(rc, tag_len, slot);
+  } else if (kind == TLSGPU_CHACHA20_POLY1305_OLD) {
+    cc_wave_job_old<SEAL>(j, S, slot, true);
   }
 }
 

@@ -302,4 +302,174 @@ __device__ void cc_wave_job(const RawJob& j, const DevSession* S, int32_t* statu
   if (lane == 0) *status = TLSGPU_REC_BAD_MAC;
 }
 
+// Bytes [off, off + 16) of the segment p[0, len) as little-endian words,
+// zero outside it; off may be negative.  A window inside the segment takes
+// dword loads (load16_any, global memory); an edge window goes byte by byte
+// through the generic pointer (the server's inline AAD lives in LDS).
+__device__ __forceinline__ void cw_seg16(const uint8_t* p, int64_t len, int64_t off, bool global,
+                                         uint32_t w[4]) {
+  w[0] = w[1] = w[2] = w[3] = 0;
+  if (off >= len || off + 16 <= 0) return;
+  if (global && off >= 0 && off + 16 <= len) {
+    load16_any(p + off, w);
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int64_t q = off + k;
+    if (q >= 0 && q < len) w[k >> 2] |= (uint32_t)p[q] << (8 * (k & 3));
+  }
+}
+
+// The same window of the 8-byte little-endian encoding of v.
+__device__ __forceinline__ void cw_le64_16(uint64_t v, int64_t off, uint32_t w[4]) {
+  w[0] = w[1] = w[2] = w[3] = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int64_t q = off + k;
+    if (q >= 0 && q < 8) w[k >> 2] |= (uint32_t)((v >> (8 * q)) & 0xFF) << (8 * (k & 3));
+  }
+}
+
+// Poly1305 tag of the draft AEAD's byte stream AD || le64(|AD|) || CT ||
+// le64(|CT|) (e_chacha20poly1305.c:160-170, poly1305_update over
+// unpadded pieces), with the lane split of cc_wave_job: lane l takes stream
+// blocks b = l (mod 64), Horner with r^64, weight r^(N - b_last), wave sum.
+// The last block, if partial, carries the 0x01 byte after its data and no
+// 2^128 bit (poly1305-donna's final block).  pw: r^(l+1) on lane l.
+__device__ __forceinline__ void cw_old_mac(const uint8_t* aad, uint32_t ad_len, bool aad_global,
+                                           const uint8_t* ct, uint32_t n, const P5& pw,
+                                           const uint32_t pad[4], uint32_t mac[4]) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t M = (uint64_t)ad_len + 8 + n + 8;
+  const uint32_t N = (uint32_t)((M + 15) >> 4);
+  const P5 r64 = p5_readlane(pw, 63);
+  P5 acc = {0, 0, 0, 0, 0};
+  for (uint32_t b = lane; b < N; b += 64) {
+    const int64_t o = 16 * (int64_t)b;
+    uint32_t w[4], t[4];
+    cw_seg16(aad, ad_len, o, aad_global, w);
+    cw_le64_16(ad_len, o - ad_len, t);
+    w[0] |= t[0]; w[1] |= t[1]; w[2] |= t[2]; w[3] |= t[3];
+    cw_seg16(ct, n, o - ad_len - 8, true, t);
+    w[0] |= t[0]; w[1] |= t[1]; w[2] |= t[2]; w[3] |= t[3];
+    cw_le64_16(n, o - ad_len - 8 - n, t);
+    w[0] |= t[0]; w[1] |= t[1]; w[2] |= t[2]; w[3] |= t[3];
+    uint32_t hibit = 1u << 24;
+    const uint64_t left = M - (uint64_t)o;
+    if (left < 16) {  // poly1305 final block: 0x01 after the data, no 2^128
+      w[left >> 2] |= 1u << (8 * (left & 3));
+      hibit = 0;
+    }
+    acc = p5_add(p5_mul(acc, r64), p5_block(w[0], w[1], w[2], w[3], hibit));
+  }
+  const uint32_t wgt = lane < N ? N - (lane + 64 * ((N - 1 - lane) >> 6)) : 1u;
+  acc = p5_mul(acc, p5_shfl(pw, (int)wgt - 1));
+  acc = p5_wave_sum(acc);
+  Poly p = {};
+  p.h0 = acc.v0; p.h1 = acc.v1; p.h2 = acc.v2; p.h3 = acc.v3; p.h4 = acc.v4;
+  p.pad0 = pad[0]; p.pad1 = pad[1]; p.pad2 = pad[2]; p.pad3 = pad[3];
+  poly_finish(p, mac);
+}
+
+// Run raw job j of the draft ("old") ChaCha20-Poly1305 AEAD on the calling
+// wave (round 5: the doorbell server's op 21 and chacha_raw_wave_kernel).
+// e_chacha20poly1305.c:124-286 with the 8-byte nonce: ChaCha20 with a 64-bit
+// block counter in words 12-13 and the nonce in words 14-15 (counter 0: the
+// one-time Poly1305 key, data from counter 1); the MAC over the byte stream
+// of cw_old_mac.  Open checks the tag before it writes any plaintext (the
+// reference's order), seal MACs the ciphertext it wrote.  Same contract as
+// cc_wave_job (host-side checks are the caller's).
+template <bool SEAL>
+__device__ void cc_wave_job_old(const RawJob& j, const DevSession* S, int32_t* status,
+                                bool aad_global) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t* sw = reinterpret_cast<const uint32_t*>(S);
+  static_assert(offsetof(DevSession, chacha_key) == 72 * 4, "DevSession layout");
+  const uint32_t sv = sw[lane < 8 ? lane : 64 + (lane & 15)];
+  const uint32_t tag_len = __builtin_amdgcn_readlane(sv, 2);
+  uint32_t in[16];
+  in[0] = 0x61707865u; in[1] = 0x3320646eu; in[2] = 0x79622d32u; in[3] = 0x6b206574u;
+#pragma unroll
+  for (int i = 0; i < 8; i++) in[4 + i] = __builtin_amdgcn_readlane(sv, 8 + i);
+  const uint8_t* nonce = reinterpret_cast<const uint8_t*>(j.nonce);
+  in[13] = 0;
+  in[14] = ld_le32(nonce);
+  in[15] = ld_le32(nonce + 4);
+  const uint32_t n = SEAL ? j.in_len : j.in_len - tag_len;
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(j.in);
+  uint8_t* dst = reinterpret_cast<uint8_t*>(j.out);
+  const uint8_t* aad = reinterpret_cast<const uint8_t*>(j.aad);
+  const bool aligned = ((((uintptr_t)src) | ((uintptr_t)dst)) & 15) == 0;
+
+  // the one-time key (counter 0, lane 0's block) and r^1..r^64 by doubling
+  uint32_t ks[16];
+  in[12] = 0;
+  chacha_block(in, ks);
+  uint32_t k[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) k[i] = __builtin_amdgcn_readfirstlane(ks[i]);
+  Poly p0;
+  poly_init(p0, k);
+  const uint32_t pad[4] = {k[4], k[5], k[6], k[7]};
+  P5 pw = {p0.r0, p0.r1, p0.r2, p0.r3, p0.r4};
+#pragma unroll
+  for (int lev = 0; lev < 6; lev++) {
+    const int step = 1 << lev;
+    const P5 base = p5_readlane(pw, step - 1);
+    const P5 lo = p5_shfl(pw, (int)lane - step);
+    const P5 m = p5_mul(lo, base);
+    if ((int)lane >= step && (int)lane < 2 * step) pw = m;
+  }
+  uint32_t mac[4];
+  if (!SEAL) cw_old_mac(aad, j.aad_len, aad_global, src, n, pw, pad, mac);
+  bool bad = false;
+  if (!SEAL) {
+    const uint8_t* tag_in = src + n;
+    bad = __ballot(lane < tag_len && (tag_in[lane] ^ cw_mac_byte(mac, lane)) != 0) != 0;
+  }
+  if (!bad) {
+    // data: lane l of pass t runs counter 64 t + l + 1 over bytes [64 kb, 64 kb + 64)
+    const uint32_t nkb = (n + 63) >> 6;
+    for (uint32_t kb = lane; kb - lane < nkb; kb += 64) {  // wave-uniform trip count
+      if (kb >= nkb) continue;
+      in[12] = kb + 1;  // < 2^26 blocks per job: word 13 stays 0
+      chacha_block(in, ks);
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t o = 64 * kb + 16 * q;
+        if (o < n) {
+          const uint32_t nb = min(16u, n - o);
+          uint32_t x[4], y[4];
+          cw_load16(src + o, nb, aligned, x);
+#pragma unroll
+          for (int w = 0; w < 4; w++) y[w] = x[w] ^ ks[4 * q + w];
+          cw_store16(dst + o, nb, aligned, y);
+        }
+      }
+    }
+  }
+  if (SEAL) {
+    // the ciphertext other lanes stored, before the MAC reads it
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    cw_old_mac(aad, j.aad_len, aad_global, dst, n, pw, pad, mac);
+    if (lane < tag_len) dst[n + lane] = (uint8_t)cw_mac_byte(mac, lane);
+    if (lane == 0) *status = (int32_t)(n + tag_len);
+    return;
+  }
+  if (!bad) {
+    if (lane == 0) *status = (int32_t)n;
+    return;
+  }
+  const uint64_t z = j.max_out;  // evp_aead.c:137-143
+  const bool zal = (((uintptr_t)dst) & 15) == 0;
+  for (uint64_t o = 16 * (uint64_t)lane; o < z; o += 1024) {
+    const uint32_t zero[4] = {0, 0, 0, 0};
+    cw_store16(dst + o, z - o < 16 ? (uint32_t)(z - o) : 16u, zal, zero);
+  }
+  if (lane == 0) *status = TLSGPU_REC_BAD_MAC;
+}
+
 }  // namespace tg

@@ -1853,8 +1853,8 @@ static const bool g_evp_zerocopy = [] {
 // after half of that has passed, on the same stream: a job is only posted
 // while an instance that still polls for at least half a lifetime is queued or
 // running, so every posted job is served, and a process that stops calling
-// leaves nothing spinning.  Draft ("old") ChaCha20-Poly1305 contexts and pooled
-// (queued) contexts keep the launched path; a context's first call carries its
+// leaves nothing spinning.  AES-GCM, RFC 7539 and (round 5) draft ChaCha20-
+// Poly1305 jobs; pooled (queued) contexts keep the launched path; a context's first call carries its
 // deferred install (the host-built image, defer_install) and its cleanup posts
 // a scrub job; a short GCM job's input is staged into LDS by the server's idle
 // waves.  On by default (round 5, kDoorbellDefaultGroups).
@@ -2406,7 +2406,7 @@ static bool doorbell_enabled() {
 static bool deferred_install_ok(int kind) {
   return g_deferred_install && !g_device_install && g_evp_zerocopy && doorbell_enabled() &&
          (kind == TLSGPU_AES_128_GCM || kind == TLSGPU_AES_256_GCM ||
-          kind == TLSGPU_CHACHA20_POLY1305);
+          kind == TLSGPU_CHACHA20_POLY1305 || kind == TLSGPU_CHACHA20_POLY1305_OLD);
 }
 
 // EVP_AEAD_CTX_cleanup through the doorbell (round 5): a scrub job zeroes the
@@ -2521,7 +2521,8 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
   // doorbell (zero-copy AES-GCM and RFC 7539 ChaCha20-Poly1305 calls): post
   // the job to a resident server workgroup instead of launching; the staging
   // buffer is the job's memory
-  if (zc && (gcm || st->kind == TLSGPU_CHACHA20_POLY1305)) {
+  if (zc && (gcm || st->kind == TLSGPU_CHACHA20_POLY1305 ||
+             st->kind == TLSGPU_CHACHA20_POLY1305_OLD)) {
     EvpServer* sv = evp_server(st->evp_dev, e);
     uint32_t* seq = nullptr;
     DoorbellSlot* slot = sv ? thread_slot(sv, st->evp_dev, &seq) : nullptr;
@@ -2536,7 +2537,8 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
       const bool inl = !claim.active && nonce_len + ad_len <= kDoorbellInline;
       const uint32_t kop = st->kind == TLSGPU_AES_128_GCM   ? 10u
                            : st->kind == TLSGPU_AES_256_GCM ? 14u
-                                                            : 20u;  // ChaCha (evp_server.hip)
+                           : st->kind == TLSGPU_CHACHA20_POLY1305 ? 20u
+                                                                  : 21u;  // draft ChaCha
       slot->op = (uint32_t)(seal ? 1 : 0) | (kop << 8) | (inl ? 1u << 16 : 0u) |
                  (claim.active ? kDoorbellOpInstall : 0u) |
                  (claim.active && st->img_tables ? kDoorbellOpInstallTables : 0u);

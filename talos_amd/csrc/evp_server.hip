@@ -114,6 +114,25 @@ __device__ __forceinline__ void srv_chacha_job(const BatchArgs& a, const RawJob&
   cc_wave_job<SEAL>(j, S, a.status, s_lds + SRV_STAGE_OFF);
 }
 
+// A draft ("old") ChaCha20-Poly1305 job on wave 0 (round 5, chacha_wave.h
+// cc_wave_job_old); inl: the AAD sits in the LDS copy of the slot.
+template <bool SEAL>
+__device__ __forceinline__ void srv_chacha_old_job(const BatchArgs& a, const RawJob& j, bool inl) {
+  if (threadIdx.x >= kWave) return;
+  const uint32_t sid = j.session;
+  if (sid >= a.n_sessions) {
+    if (threadIdx.x == 0) a.status[0] = TLSGPU_REC_PUBLIC_INVALID;
+    return;
+  }
+  const DevSession* S = a.sessions + sid;
+  const uint32_t kw = reinterpret_cast<const uint32_t*>(S)[threadIdx.x & 7];
+  if (__builtin_amdgcn_readlane(kw, 0) != TLSGPU_CHACHA20_POLY1305_OLD) {
+    if (threadIdx.x == 0) a.status[0] = TLSGPU_REC_PUBLIC_INVALID;
+    return;
+  }
+  cc_wave_job_old<SEAL>(j, S, a.status, !inl);
+}
+
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -291,6 +310,8 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
       case (14 << 8) | 1: cached_key = gcm_raw_job<true, 14>(a, 0, hit) ? key : 0; break;
       case 20 << 8: srv_chacha_job<false>(a, c->job); break;
       case (20 << 8) | 1: srv_chacha_job<true>(a, c->job); break;
+      case 21 << 8: srv_chacha_old_job<false>(a, c->job, (c->op & (1u << 16)) != 0); break;
+      case (21 << 8) | 1: srv_chacha_old_job<true>(a, c->job, (c->op & (1u << 16)) != 0); break;
       case kOpScrub << 8: break;  // done above
       default:  // not a job this server runs (the host never posts one)
         if (threadIdx.x == 0) a.status[0] = TLSGPU_REC_PUBLIC_INVALID;

@@ -7,10 +7,9 @@ be the oracle's (e_aes.c:1424-1510 through evp_aead.c:89-144: tag, zero-fill
 and return 0 on a bad tag, odd nonce lengths, truncated tags), with threads
 cycling init / seal / open / cleanup so session slots are re-keyed while the
 server runs, across server relaunches (short lifetime), and the server must
-stop by itself when the calls stop.  ChaCha jobs run on the server's wave 0
-(chacha_wave.h) between GCM jobs, whose LDS table cache they must leave
-intact; draft-suite ChaCha contexts take the launched path in the same
-threads.  A GCM job's input up to 4 KiB is staged into LDS by the server's
+stop by itself when the calls stop.  ChaCha jobs (RFC 7539, and since round
+5 the draft suite) run on the server's wave 0 (chacha_wave.h) between GCM
+jobs, whose LDS table cache they must leave intact.  A GCM job's input up to 4 KiB is staged into LDS by the server's
 idle waves 12-15 while waves 0-1 parse: the lengths cover both sides of that
 limit for seal (4,096 B of plaintext) and open (4,080 + 16 B of ciphertext
 and tag)."""
