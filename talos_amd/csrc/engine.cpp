@@ -380,16 +380,20 @@ extern "C" int tlsgpu_debug_phase_stats(tlsgpu_engine* e, unsigned long long* ou
 // {start, end, rlo, rhi} of each workgroup of the last queue launch, read with
 // tlsgpu_debug_wg_times (s_memrealtime ticks, 100 MHz).
 static unsigned long long* g_wg_times = nullptr;
+static int g_wg_times_dev = -1;  // the first engine's device only
 static unsigned long long* wg_times_for(const tlsgpu_engine* e) {
   static const bool on = [] {
     const char* v = getenv("TLSGPU_WG_TIMES");
     return v && *v && *v != '0';
   }();
   if (!on) return nullptr;
-  if (!g_wg_times && hipMalloc((void**)&g_wg_times, 4 * 1024 * sizeof(unsigned long long)) == hipSuccess)
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!g_wg_times && hipMalloc((void**)&g_wg_times, 4 * 1024 * sizeof(unsigned long long)) == hipSuccess) {
     (void)hipMemset(g_wg_times, 0, 4 * 1024 * sizeof(unsigned long long));
-  (void)e;
-  return g_wg_times;
+    g_wg_times_dev = e->device;
+  }
+  return e->device == g_wg_times_dev ? g_wg_times : nullptr;
 }
 extern "C" int tlsgpu_debug_wg_times(tlsgpu_engine* e, unsigned long long* out, unsigned groups) {
   if (!e || !out || groups > 1024) return fail(TLSGPU_EINVAL, "bad arguments");
