@@ -432,18 +432,18 @@ int tlsgpu_evp_call_stats(uint64_t *seal_calls, uint64_t *open_calls);
  * resident on every EVP device while calls arrive: a calling thread posts its
  * job (the same zero-copy RawJob the launched path builds) in a slot of pinned
  * host memory and spins on the answer, so a synchronous EVP_AEAD_CTX_seal /
- * _open on an AES-GCM or RFC 7539 ChaCha20-Poly1305 context costs one PCIe
- * round trip instead of a kernel launch + stream sync.  Each server instance
- * exits after lifetime_ms (0 = 5 ms) and is relaunched by the next call, so an
- * idle process leaves nothing running.  Threads beyond 8 * groups per device,
- * a context's first call (its key install still queued), draft-suite ChaCha
- * contexts and pooled (queued) contexts use the other paths.  Same as
+ * _open on an AES-GCM, RFC 7539 or draft ChaCha20-Poly1305 context costs one
+ * PCIe round trip instead of a kernel launch + stream sync.  Each server
+ * instance exits after lifetime_ms (0 = 5 ms) and is relaunched by the next
+ * call, so an idle process leaves nothing running.  Threads beyond
+ * 8 * groups per device and pooled (queued) contexts use the other paths.
+ * Same as
  * TLSGPU_EVP_DOORBELL=<groups> (TLSGPU_EVP_DOORBELL_MS=<lifetime>) at load;
  * on by default with 64 groups (round 5; 0 turns it off); must be called
  * before the first EVP call.  With it on, EVP_AEAD_CTX_init launches nothing
  * (the session image is built on the host and installed by the context's
- * first call) and EVP_AEAD_CTX_cleanup scrubs the slot through the server.  tlsgpu_evp_doorbell_stats: jobs
- * served and instances launched so far. */
+ * first call) and EVP_AEAD_CTX_cleanup scrubs the slot through the server.
+ * tlsgpu_evp_doorbell_stats: jobs served and instances launched so far. */
 int tlsgpu_evp_set_doorbell(unsigned groups, unsigned lifetime_ms);
 int tlsgpu_evp_doorbell_stats(uint64_t *jobs, uint64_t *launches);
 /* tlsgpu_evp_doorbell_warm: launch a server instance now on every EVP device
