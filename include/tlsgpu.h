@@ -501,8 +501,9 @@ int tlsgpu_debug_phase_stats(tlsgpu_engine *e, unsigned long long *out32, int re
 /* Diagnostic: per-workgroup timing of the queue kernel.  With
  * TLSGPU_WG_TIMES=1 in the environment every queue launch writes, per
  * workgroup g, out[4g..4g+3] = {start, end (100 MHz s_memrealtime ticks),
- * first record, end record}; this call synchronizes the device and copies the
- * first `groups` (<= 1024) entries of the last launch.  Fails when the
+ * records, work (payload bytes + 256 per record)} of the records it ran; this
+ * call synchronizes the device and copies the first `groups` (<= 1024)
+ * entries of the last launch.  Fails when the
  * variable is not set or before the first launch. */
 int tlsgpu_debug_wg_times(tlsgpu_engine *e, unsigned long long *out, unsigned groups);
 

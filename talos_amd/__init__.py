@@ -440,8 +440,8 @@ def debug_phase_stats(engine: "Engine", reset: bool = True) -> list[int]:
 
 
 def debug_wg_times(engine: "Engine", groups: int) -> list[tuple[int, int, int, int]]:
-    """Diagnostic (TLSGPU_WG_TIMES=1): {start, end, rlo, rhi} per workgroup of the
-    last queue-kernel launch (100 MHz ticks)."""
+    """Diagnostic (TLSGPU_WG_TIMES=1): {start, end (100 MHz ticks), records, work}
+    per workgroup of the last queue-kernel launch."""
     out = (C.c_ulonglong * (4 * groups))()
     _check(engine.lib.tlsgpu_debug_wg_times(engine.handle, out, groups), "tlsgpu_debug_wg_times")
     return [tuple(out[4 * g:4 * g + 4]) for g in range(groups)]

@@ -465,6 +465,16 @@ static const uint32_t g_balance = [] {
   const char* v = getenv("TLSGPU_BALANCE");
   return v && *v ? (uint32_t)strtoul(v, nullptr, 10) : 0u;
 }();
+// Whole-piece balance (round 5, TLSGPU_PIECES): 0 off, 1 the pack variant
+// (mixed record lengths; the default), 2 always — each workgroup takes whole
+// pieces (a session run inside one count range) from a list sorted by work,
+// in snake order (gcm_queue.hip piece_sort_kernel), instead of its count
+// range: config D +1.4 % same-box, B (uniform records) −1 % (the two plan
+// launches), DESIGN.md §4.1c.
+static const uint32_t g_pieces = [] {
+  const char* v = getenv("TLSGPU_PIECES");
+  return v && *v ? (uint32_t)strtoul(v, nullptr, 10) : 1u;
+}();
 // ... and how near a session-run boundary a cut snaps to it, in 1/1024 of a
 // workgroup's share of the work (TLSGPU_BALANCE_SNAP; 0: exact cuts)
 static const uint32_t g_balance_snap = [] {
@@ -556,7 +566,11 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
   const size_t ctl_bytes = 2048 + 2 * cnt_bytes;
   const bool balance = fused_gcm && groups > 1 && groups <= 1024 &&
                        (g_balance >= 2 || (g_balance == 1 && a.pack != 0));
-  const size_t cut_bytes = balance ? ((size_t)groups * 8 + 255) & ~(size_t)255 : 0;
+  const bool pieces = fused_gcm && !balance && groups > 1 && groups <= 1024 &&
+                      (g_pieces >= 2 || (g_pieces == 1 && a.pack != 0));
+  const size_t cut_bytes = balance  ? ((size_t)groups * 8 + 255) & ~(size_t)255
+                           : pieces ? ((kPieceScratchBytes((uint32_t)groups) + 255) & ~(size_t)255) + 256
+                                    : 0;
   const size_t pre_bytes =
       gcm_pre ? sizeof(RecPre) * (size_t)n + (fused ? cut_bytes : ctl_bytes) : 0;
   uint8_t* scratch = nullptr;
@@ -588,6 +602,11 @@ static int run_batch(tlsgpu_sessions* t, const void* d_descs, uint32_t n, const 
         return fail(TLSGPU_EHIP, "range work launch: %s", hipGetErrorString(hipGetLastError()));
       a.cut_work = cw;
       a.cut_snap = g_balance_snap;
+    } else if (pieces) {  // whole pieces sorted by work
+      uint8_t* ps = reinterpret_cast<uint8_t*>(pre + n);
+      ps += (256 - ((uintptr_t)ps & 255)) & 255;
+      if (launch_piece_plan(a, groups, ps, &a.pieces, &a.n_pieces, s))
+        return fail(TLSGPU_EHIP, "piece plan launch: %s", hipGetErrorString(hipGetLastError()));
     }
   } else if (bounds) {
     // one setup launch: sanitized descriptors, every record's initial status

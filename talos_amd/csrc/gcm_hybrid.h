@@ -624,21 +624,24 @@ __device__ __forceinline__ RecPre rec_pre(const uint32_t j0[4], RK rk, T0F T0, T
 // kernel is the batch's only one (one AES key size installed, no ChaCha, no
 // pack / per-wave-session variants: engine.cpp run_batch), so every status
 // write here precedes this workgroup's own final one (barrier below).
-template <bool SEAL, int ROUNDS, int NT>
-__device__ void fused_prologue(const BatchArgs& a, RecPre* __restrict__ pre, uint32_t rlo,
-                               uint32_t rhi) {
+// `nrec` records, the L-th of them record map(L) (one range, or the
+// workgroup's whole pieces: one pass over all of them).
+template <bool SEAL, int ROUNDS, int NT, typename MAP>
+__device__ void fused_prologue_map(const BatchArgs& a, RecPre* __restrict__ pre, uint32_t nrec,
+                                   MAP map) {
   const tlsgpu_record* D = reinterpret_cast<const tlsgpu_record*>(a.descs);
   const uint32_t* te = reinterpret_cast<const uint32_t*>(s_lds + AES_OFF);
   const uint32_t l32 = threadIdx.x & 31;
   auto T0 = [&](uint32_t w, int b) { return te[(((w >> (8 * b)) & 0xFF) << 6) | l32]; };
   auto T1 = [&](uint32_t w, int b) { return te[(((w >> (8 * b)) & 0xFF) << 6) | 32 | l32]; };
   auto SB = [&](uint32_t w, int b) { return (T0(w, b) >> 8) & 0xFF; };
-  for (uint32_t base = rlo; base < rhi; base += NT) {  // wave-uniform trip count
-    const uint32_t r = base + threadIdx.x;
+  for (uint32_t base = 0; base < nrec; base += NT) {  // wave-uniform trip count
+    const uint32_t L = base + threadIdx.x;
+    const uint32_t r = L < nrec ? map(L) : 0u;
     bool mine = false;
     tlsgpu_record d = {};
     const DevSession* S = nullptr;
-    if (r < rhi) {
+    if (L < nrec) {
       d = D[r];
       int32_t st = TLSGPU_REC_PUBLIC_INVALID;
       if (d.session < a.n_sessions) {
@@ -667,6 +670,13 @@ __device__ void fused_prologue(const BatchArgs& a, RecPre* __restrict__ pre, uin
                      : rec_pre<SEAL, ROUNDS>(j0, S->rk, T0, T1, SB);
   }
   __threadfence_block();  // the statuses and constants before this workgroup's main loop
+}
+
+template <bool SEAL, int ROUNDS, int NT>
+__device__ __forceinline__ void fused_prologue(const BatchArgs& a, RecPre* __restrict__ pre,
+                                               uint32_t rlo, uint32_t rhi) {
+  fused_prologue_map<SEAL, ROUNDS, NT>(a, pre, rhi > rlo ? rhi - rlo : 0u,
+                                       [&](uint32_t L) { return rlo + L; });
 }
 
 // Inclusive prefix sum of one value per thread over the workgroup, and the
@@ -804,17 +814,89 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
   fill_aes_lds<NT>();
   if (a.dbg && threadIdx.x < 32) reinterpret_cast<unsigned long long*>(s_lds + DBG_OFF)[threadIdx.x] = 0;
 
-  uint32_t rlo = blockIdx.x * a.records_per_group;
-  uint32_t rhi = min(a.n, rlo + a.records_per_group);
+  // whole pieces sorted by work (a.pieces, written by piece_sort_kernel: a
+  // vector load), else this workgroup's count range (or work cuts)
+  const uint32_t n_pieces =
+      a.pieces ? __builtin_amdgcn_readfirstlane(*reinterpret_cast<const volatile uint32_t*>(a.n_pieces))
+               : 0u;
+  // piece m of this workgroup: false when it has no more
+  auto piece = [&](uint32_t m, uint32_t& rlo, uint32_t& rhi) -> bool {
+    if (n_pieces != 0) {
+      const uint32_t G = gridDim.x;
+      const uint32_t idx = m * G + ((m & 1u) ? G - 1u - blockIdx.x : blockIdx.x);
+      if (idx >= n_pieces) return false;
+      // vector loads (the plan was written by the previous kernel)
+      const volatile uint32_t* pw = reinterpret_cast<const volatile uint32_t*>(a.pieces + idx);
+      rlo = __builtin_amdgcn_readfirstlane(pw[0]);
+      rhi = __builtin_amdgcn_readfirstlane(pw[1]);
+      return true;
+    }
+    if (m != 0) return false;
+    rlo = blockIdx.x * a.records_per_group;
+    rhi = min(a.n, rlo + a.records_per_group);
+    return true;
+  };
+  uint32_t rlo = 0, rhi = 0;
   if (BSW == 0 && B16W == 0 && a.fused) {
+    __syncthreads();  // the T-tables
     if (a.cut_work) {  // work-balanced ranges (engine.cpp run_batch)
       rlo = work_cut<NT>(a, blockIdx.x);
       rhi = work_cut<NT>(a, blockIdx.x + 1);
+      fused_prologue<SEAL, ROUNDS, NT>(a, const_cast<RecPre*>(pre), rlo, rhi);
+    } else if (n_pieces == 0) {
+      piece(0, rlo, rhi);
+      fused_prologue<SEAL, ROUNDS, NT>(a, const_cast<RecPre*>(pre), rlo, rhi);
+    } else {
+      // the workgroup's pieces (at most kPiecesPerRange: n_pieces <= that
+      // many per workgroup) into LDS, then one prologue pass over all of them
+      uint32_t* pl = reinterpret_cast<uint32_t*>(s_lds + PLAN_OFF + 512);
+      if (threadIdx.x < kPiecesPerRange) {
+        const uint32_t t = threadIdx.x, G = gridDim.x;
+        const uint32_t idx = t * G + ((t & 1u) ? G - 1u - blockIdx.x : blockIdx.x);
+        uint32_t lo = 0, hi = 0;
+        if (idx < n_pieces) {
+          const volatile uint32_t* pw = reinterpret_cast<const volatile uint32_t*>(a.pieces + idx);
+          lo = pw[0];
+          hi = pw[1];
+        }
+        pl[2 * t] = lo;
+        pl[2 * t + 1] = hi;
+      }
+      __syncthreads();
+      uint32_t nrec = 0;
+      for (uint32_t k = 0; k < kPiecesPerRange; k++) nrec += pl[2 * k + 1] - pl[2 * k];
+      fused_prologue_map<SEAL, ROUNDS, NT>(a, const_cast<RecPre*>(pre), nrec, [&](uint32_t L) {
+        uint32_t k = 0;
+        for (; k + 1 < kPiecesPerRange; k++) {
+          const uint32_t len = pl[2 * k + 1] - pl[2 * k];
+          if (L < len) break;
+          L -= len;
+        }
+        return pl[2 * k] + L;
+      });
     }
-    __syncthreads();  // the T-tables
-    fused_prologue<SEAL, ROUNDS, NT>(a, const_cast<RecPre*>(pre), rlo, rhi);
+  }
+  if (a.wg_times) {  // diagnostic: the workgroup's records and work
+    uint64_t recs = 0, work = 0;
+    for (uint32_t m = 0; a.cut_work ? m == 0 : piece(m, rlo, rhi); m++) {
+      for (uint32_t c = rlo; c < rhi; c += NT) {
+        const uint32_t i = c + threadIdx.x;
+        uint64_t t;
+        (void)block_scan_incl<NT>(i < rhi ? cut_work_of(D[i].len_type) : 0u,
+                                  reinterpret_cast<uint64_t*>(s_lds + PLAN_OFF), &t);
+        work += t;
+      }
+      recs += rhi - rlo;
+    }
+    if (threadIdx.x == 0) {
+      a.wg_times[4 * blockIdx.x + 2] = recs;
+      a.wg_times[4 * blockIdx.x + 3] = work;
+    }
   }
   uint32_t cur = 0xFFFFFFFFu;
+  // one loop over the workgroup's pieces and their session runs
+  uint32_t m = 0;
+  if (!a.cut_work && !piece(0, rlo, rhi)) rlo = rhi = 0;
   uint32_t pos = rlo;
   // short-record packs (gcm_pack): T-table waves only, planned per run in LDS
   const bool packing = PACK && BSW == 0 && a.pack != 0;
@@ -824,7 +906,12 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
   uint8_t* plan_need = s_lds + PLAN_OFF + 2 * kPlanCap;  // pack_need of order[t]
   uint8_t* plan_k = plan_need + kPlanCap;
   uint32_t* ends = q + 1;  // [0]: next long slot (from the front), [1]: short slots (from the back)
-  while (pos < rhi) {
+  for (;;) {
+    if (pos >= rhi) {  // the next piece
+      if (a.cut_work || !piece(++m, rlo, rhi)) break;
+      pos = rlo;
+      continue;
+    }
     const uint32_t sid = __builtin_amdgcn_readfirstlane(D[pos].session);
     const bool in_range = sid < a.n_sessions;
     const DevSession* __restrict__ S = a.sessions + (in_range ? sid : 0);
@@ -1002,13 +1089,9 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
     if (threadIdx.x < 32)
       atomicAdd(a.dbg + threadIdx.x, reinterpret_cast<unsigned long long*>(s_lds + DBG_OFF)[threadIdx.x]);
   }
-  if (a.wg_times) {  // diagnostic: when the workgroup's last wave is done, and its range
+  if (a.wg_times) {  // diagnostic: when the workgroup's last wave is done, its records and work
     __syncthreads();
-    if (threadIdx.x == 0) {
-      a.wg_times[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-      a.wg_times[4 * blockIdx.x + 2] = rlo;
-      a.wg_times[4 * blockIdx.x + 3] = rhi;
-    }
+    if (threadIdx.x == 0) a.wg_times[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
   }
 }
 

@@ -215,6 +215,10 @@ struct BatchArgs {
                                        // records between its two work cuts instead
   uint32_t cut_snap;                // cut_work: snap a cut to a session-run boundary within
                                     // cut_snap / 1024 of a share of the work (0: exact cuts)
+  const uint2* pieces;              // fused, non-null: whole pieces (a session run inside
+  const uint32_t* n_pieces;         // one count range) sorted by work, largest first; workgroup
+                                    // w takes pieces m*G + (m even ? w : G-1-w) (piece_sort_kernel;
+                                    // *n_pieces == 0: the count ranges)
   unsigned long long* wg_times;     // diagnostic (TLSGPU_WG_TIMES=1), normally null: per
                                     // workgroup {start, end (s_memrealtime), rlo, rhi}
 };
@@ -262,6 +266,16 @@ int launch_gcm(const BatchArgs& a, bool seal, bool raw, int rounds, int groups,
 int launch_gcm_split(const BatchArgs& a, bool seal, int rounds, hipStream_t s);
 int launch_gcm_prep(const BatchArgs& a, RecPre* pre, bool seal, int rounds, hipStream_t s);
 int launch_range_work(const BatchArgs& a, int groups, unsigned long long* out, hipStream_t s);
+// Whole-piece balance (round 5): the pieces of every count range, then all of
+// them sorted by work (gcm_queue.hip).  scratch: kPieceScratchBytes(groups).
+constexpr uint32_t kPiecesPerRange = 16;  // more in one count range: no plan (count ranges)
+constexpr uint32_t kMaxPieces = 4096;     // the sort's LDS capacity
+__host__ __device__ constexpr size_t kPieceScratchBytes(uint32_t groups) {
+  return (size_t)groups * kPiecesPerRange * 16 + (size_t)((groups + 3) & ~3u) * 4 +
+         (size_t)groups * kPiecesPerRange * 8 + 256;
+}
+int launch_piece_plan(const BatchArgs& a, int groups, uint8_t* scratch, const uint2** pieces,
+                      const uint32_t** n_pieces, hipStream_t s);
 int launch_gcm_queue(const BatchArgs& a, const RecPre* pre, bool seal, int rounds, int groups,
                      hipStream_t s);
 int launch_gcm_queue_b16(const BatchArgs& a, const RecPre* pre, bool seal, int rounds, int groups,

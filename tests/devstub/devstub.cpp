@@ -355,7 +355,7 @@ int launch_batch(const char* what, const BatchArgs& a, hipStream_t s,
   const std::pair<const char*, const void*> mem[] = {
       {"sessions", a.sessions}, {"gcm_tables", a.gcm_tables}, {"descs", a.descs}, {"in", a.in},
       {"out", a.out}, {"status", a.status}, {"sel", a.sel}, {"wg_next", a.wg_next}, {"dbg", a.dbg},
-      {"cut_work", a.cut_work}};
+      {"cut_work", a.cut_work}, {"pieces", a.pieces}};
   for (const auto& m : mem) mem_on(what, m.first, m.second, d);
   for (const auto& m : more) mem_on(what, m.first, m.second, d);
   return 0;
@@ -370,6 +370,12 @@ int launch_gcm_split(const BatchArgs& a, bool, int, hipStream_t s) {
 }
 int launch_gcm_prep(const BatchArgs& a, RecPre* pre, bool, int, hipStream_t s) {
   return launch_batch("launch_gcm_prep", a, s, {{"pre", pre}});
+}
+int launch_piece_plan(const BatchArgs& a, int, uint8_t* scratch, const uint2** pieces,
+                      const uint32_t** n_pieces, hipStream_t s) {
+  *pieces = reinterpret_cast<const uint2*>(scratch);
+  *n_pieces = reinterpret_cast<const uint32_t*>(scratch);
+  return launch_batch("launch_piece_plan", a, s, {{"scratch", scratch}});
 }
 int launch_range_work(const BatchArgs& a, int, unsigned long long* out, hipStream_t s) {
   return launch_batch("launch_range_work", a, s, {{"out", out}});

@@ -638,14 +638,17 @@ def _fused_case(ta, engine, oracle, mode, hints, name, lengths=None):
 SKEWED_LENGTHS = [16384] + [17, 16, 15, 12, 9] * 7 + [3, 5, 1, 0]
 
 
-@pytest.mark.parametrize("balance,snap", [("1", "0"), ("2", "0"), ("2", "300")])
-def test_batch_fused_balanced_ranges(ta, balance, snap):
+@pytest.mark.parametrize("balance,snap,pieces", [("1", "0", "0"), ("2", "0", "0"), ("2", "300", "0"),
+                                                 ("0", "0", "2")])
+def test_batch_fused_balanced_ranges(ta, balance, snap, pieces):
     """Work-balanced ranges (round 5, engine.cpp run_batch `balance`,
     gcm_hybrid.h work_cut): the fused kernel's workgroups take the records
     between cuts at equal work (payload bytes + 256 per record) instead of
     equal counts (opt-in, measured no faster on config D).  TLSGPU_BALANCE=1
     cuts the pack variant's batches, 2 the no-pack variant's too;
     TLSGPU_BALANCE_SNAP moves cuts near a session-run boundary onto it.
+    TLSGPU_PIECES=2: whole pieces (a session run inside a count range)
+    sorted by work and dealt to the workgroups in snake order.
     The fused prologue cases — bounds, statuses, tamper, both variants — and a
     skewed batch whose cuts leave ranges empty, all against the oracle, in a
     child process with the variable set."""
@@ -659,7 +662,8 @@ def test_batch_fused_balanced_ranges(ta, balance, snap):
             "            t._fused_case(ta, e, o, mode, hints, name)\n"
             "            t._fused_case(ta, e, o, mode, hints, name, lengths=t.SKEWED_LENGTHS)\n"
             "e.close(); print('ok')\n") % (os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle"))
-    env = dict(os.environ, TLSGPU_BALANCE=balance, TLSGPU_BALANCE_SNAP=snap, TLSGPU_GCM_IMPL="queue")
+    env = dict(os.environ, TLSGPU_BALANCE=balance, TLSGPU_BALANCE_SNAP=snap, TLSGPU_PIECES=pieces,
+               TLSGPU_GCM_IMPL="queue")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=110,
                        env=env, cwd=ROOT)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]

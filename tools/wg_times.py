@@ -43,19 +43,17 @@ def main():
     groups = (per_gpu + rpg - 1) // rpg
     wl.open(None)
     eng.sync()
-    csum = np.concatenate([[0], np.cumsum(wl.lengths.astype(np.int64))])
     for it in range(args.launches):
         wl.open(None)
         eng.sync()
         t = np.array(ta.debug_wg_times(eng, groups), dtype=np.int64)
-        st, en, lo, hi = t[:, 0], t[:, 1], t[:, 2], t[:, 3]
+        st, en, recs, work = t[:, 0], t[:, 1], t[:, 2].astype(np.float64), t[:, 3]
         dur = (en - st) / 100.0          # us
-        nbytes = (csum[hi] - csum[lo]).astype(np.float64)
-        recs = (hi - lo).astype(np.float64)
-        runs = np.array([len(np.unique(wl.session[a:b])) for a, b in zip(lo, hi)])
+        nbytes = (work - 256 * recs).astype(np.float64)   # work = bytes + 256 per record
+        runs = np.zeros(len(st))
         span = (en.max() - st.min()) / 100.0
         out = {
-            "launch": it, "balance": os.environ.get("TLSGPU_BALANCE", "default"),
+            "launch": it, "balance": os.environ.get("TLSGPU_BALANCE", "default"), "pieces": os.environ.get("TLSGPU_PIECES", "0"),
             "span_us": round(span, 1),
             "start_spread_us": round((st.max() - st.min()) / 100.0, 1),
             "end_spread_us": round((en.max() - en.min()) / 100.0, 1),
@@ -64,14 +62,13 @@ def main():
             "dur_max_over_mean": round(dur.max() / dur.mean(), 3),
             "corr_dur_bytes": round(float(np.corrcoef(dur, nbytes)[0, 1]), 3),
             "corr_dur_records": round(float(np.corrcoef(dur, recs)[0, 1]), 3),
-            "corr_dur_runs": round(float(np.corrcoef(dur, runs)[0, 1]), 3) if runs.std() else None,
-            "runs_per_group": {"mean": round(runs.mean(), 2), "max": int(runs.max())},
+            "records_per_group": {"mean": round(recs.mean(), 1), "max": int(recs.max())},
             # ns per byte from a least-squares fit dur = a + b * bytes + c * runs
         }
-        A = np.stack([np.ones_like(dur), nbytes, runs.astype(np.float64)], 1)
+        A = np.stack([np.ones_like(dur), nbytes, recs], 1)
         coef, *_ = np.linalg.lstsq(A, dur, rcond=None)
         out["fit_us"] = {"const": round(coef[0], 1), "per_MiB": round(coef[1] * (1 << 20), 1),
-                         "per_run": round(coef[2], 1)}
+                         "per_record": round(coef[2], 3)}
         print(json.dumps(out), flush=True)
     eng.close()
 
