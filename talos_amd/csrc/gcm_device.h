@@ -1068,6 +1068,10 @@ __device__ void gcm_record_x4(const RecCtx& rc, const DevSession* __restrict__ S
   }
   uint32_t start = 0;
   gcm_blocks_xN<SEAL, ROUNDS, NB>(rc, S, rcc, x, start, lane, laneoff, gl);
+#ifdef TG_XN_ODD_STEP
+  // an odd full step left by the NB-wide loop: the pipelined one-step loop
+  if (NB > 1) gcm_blocks_xN<SEAL, ROUNDS, 1>(rc, S, rcc, x, start, lane, laneoff, gl);
+#endif
   pc.lap(9, lane);
   const CtrConst none = {};
   gcm_blocks<SEAL, ROUNDS, true>(rc, S, rcc, none, x, start, lane, laneoff, gl);
