@@ -76,4 +76,29 @@ __device__ __forceinline__ uint32_t wave_xor_total(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readlane((int)a, 63);
 }
 
+// Inclusive scans over the 64 lanes (all active) with DPP instead of 6
+// dependent __shfl_up (ds_bpermute) levels: row_shr 1 / 2 / 4 / 8 inside each
+// 16-lane row, then row_bcast 15 (rows 1, 3 take lane 15 of the row before)
+// and row_bcast 31 (rows 2, 3 take lane 31): 6 VALU ops (the scan LLVM's
+// atomic optimizer builds for wave64 on gfx9).  Lanes without a source read 0
+// (the identity of ^ and +).
+__device__ __forceinline__ uint32_t wave_scan_xor(uint32_t v) {
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_scan_add(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+  return v;
+}
+
 }  // namespace tg

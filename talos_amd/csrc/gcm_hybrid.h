@@ -424,12 +424,16 @@ __device__ void gcm_pack(const BatchArgs& a, const RecPre* __restrict__ pre, uin
   const uint32_t version = as_const(&S->version)[0];
   // lane layout: exclusive prefix sum of the needs
   const uint32_t own = lane < k ? need : 0u;
+#ifndef TG_PACK_SHFL_SCAN
+  const uint32_t incl = wave_scan_add(own);  // DPP (aes_common.h)
+#else
   uint32_t incl = own;
 #pragma unroll
   for (int d = 1; d < kWave; d <<= 1) {
     const uint32_t t = __shfl_up(incl, d);
     if (lane >= (uint32_t)d) incl += t;
   }
+#endif
   const uint32_t base_of = incl - own;  // lane i < k: first lane of record r0 + i
   uint32_t ri = 0;
   for (uint32_t i = 1; i < k; i++) ri += __builtin_amdgcn_readlane(base_of, i) <= lane ? 1u : 0u;
@@ -505,6 +509,10 @@ __device__ void gcm_pack(const BatchArgs& a, const RecPre* __restrict__ pre, uin
   mul_shoup(e, used ? (uint32_t)((int32_t)nb + 1 - j) : 1u, y);
 #pragma unroll
   for (int w = 0; w < 4; w++) y[w] = used ? y[w] : 0u;
+#ifndef TG_PACK_SHFL_SCAN
+#pragma unroll
+  for (int w = 0; w < 4; w++) y[w] = wave_scan_xor(y[w]);
+#else
 #pragma unroll
   for (int dd = 1; dd < kWave; dd <<= 1) {
 #pragma unroll
@@ -513,6 +521,7 @@ __device__ void gcm_pack(const BatchArgs& a, const RecPre* __restrict__ pre, uin
       if (lane >= (uint32_t)dd) y[w] ^= t;
     }
   }
+#endif
   uint32_t tag[4];
 #pragma unroll
   for (int w = 0; w < 4; w++) {
