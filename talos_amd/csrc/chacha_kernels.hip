@@ -595,7 +595,7 @@ __global__ __launch_bounds__(kWave) void chacha_raw_wave_kernel(BatchArgs a) {
   if (kind == TLSGPU_CHACHA20_POLY1305) {
     cc_wave_job<SEAL>(j, S, slot, stage);
   } else if (kind == TLSGPU_CHACHA20_POLY1305_OLD) {
-    cc_wave_job_old<SEAL>(j, S, slot, true);
+    cc_wave_job_old<SEAL>(j, S, slot, true, stage);
   }
 }
 

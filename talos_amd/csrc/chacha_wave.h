@@ -338,8 +338,8 @@ __device__ __forceinline__ void cw_le64_16(uint64_t v, int64_t off, uint32_t w[4
 // The last block, if partial, carries the 0x01 byte after its data and no
 // 2^128 bit (poly1305-donna's final block).  pw: r^(l+1) on lane l.
 __device__ __forceinline__ void cw_old_mac(const uint8_t* aad, uint32_t ad_len, bool aad_global,
-                                           const uint8_t* ct, uint32_t n, const P5& pw,
-                                           const uint32_t pad[4], uint32_t mac[4]) {
+                                           const uint8_t* ct, uint32_t n, bool ct_global,
+                                           const P5& pw, const uint32_t pad[4], uint32_t mac[4]) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t M = (uint64_t)ad_len + 8 + n + 8;
   const uint32_t N = (uint32_t)((M + 15) >> 4);
@@ -351,7 +351,7 @@ __device__ __forceinline__ void cw_old_mac(const uint8_t* aad, uint32_t ad_len, 
     cw_seg16(aad, ad_len, o, aad_global, w);
     cw_le64_16(ad_len, o - ad_len, t);
     w[0] |= t[0]; w[1] |= t[1]; w[2] |= t[2]; w[3] |= t[3];
-    cw_seg16(ct, n, o - ad_len - 8, true, t);
+    cw_seg16(ct, n, o - ad_len - 8, ct_global, t);
     w[0] |= t[0]; w[1] |= t[1]; w[2] |= t[2]; w[3] |= t[3];
     cw_le64_16(n, o - ad_len - 8 - n, t);
     w[0] |= t[0]; w[1] |= t[1]; w[2] |= t[2]; w[3] |= t[3];
@@ -382,7 +382,7 @@ __device__ __forceinline__ void cw_old_mac(const uint8_t* aad, uint32_t ad_len, 
 // cc_wave_job (host-side checks are the caller's).
 template <bool SEAL>
 __device__ void cc_wave_job_old(const RawJob& j, const DevSession* S, int32_t* status,
-                                bool aad_global) {
+                                bool aad_global, uint8_t* stage) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t* sw = reinterpret_cast<const uint32_t*>(S);
   static_assert(offsetof(DevSession, chacha_key) == 72 * 4, "DevSession layout");
@@ -421,8 +421,26 @@ __device__ void cc_wave_job_old(const RawJob& j, const DevSession* S, int32_t* s
     const P5 m = p5_mul(lo, base);
     if ((int)lane >= step && (int)lane < 2 * step) pw = m;
   }
+  // a job whose data fits the 4 KiB LDS stage (one pass: every TLS record of
+  // up to 4,032 B) MACs from there: open copies its ciphertext in once (the
+  // MAC and the decryption read it from LDS), seal stages what it writes —
+  // the input and output live in pinned host memory, where every re-read is
+  // a PCIe round trip
+  const bool staged = n <= 4096u - 64u;
   uint32_t mac[4];
-  if (!SEAL) cw_old_mac(aad, j.aad_len, aad_global, src, n, pw, pad, mac);
+  if (!SEAL) {
+    if (staged) {
+      for (uint32_t o = 16 * lane; o < n; o += 1024) {
+        uint32_t x[4];
+        cw_load16(src + o, min(16u, n - o), aligned, x);
+        *reinterpret_cast<uint4*>(stage + o) = make_uint4(x[0], x[1], x[2], x[3]);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    cw_old_mac(aad, j.aad_len, aad_global, staged ? stage : src, n, !staged, pw, pad, mac);
+  }
   bool bad = false;
   if (!SEAL) {
     const uint8_t* tag_in = src + n;
@@ -441,20 +459,34 @@ __device__ void cc_wave_job_old(const RawJob& j, const DevSession* S, int32_t* s
         if (o < n) {
           const uint32_t nb = min(16u, n - o);
           uint32_t x[4], y[4];
-          cw_load16(src + o, nb, aligned, x);
+          if (!SEAL && staged) {
+            const uint4 t = *reinterpret_cast<const uint4*>(stage + o);
+            x[0] = t.x; x[1] = t.y; x[2] = t.z; x[3] = t.w;
+          } else {
+            cw_load16(src + o, nb, aligned, x);
+          }
 #pragma unroll
           for (int w = 0; w < 4; w++) y[w] = x[w] ^ ks[4 * q + w];
           cw_store16(dst + o, nb, aligned, y);
+          if (SEAL && staged) {  // the MAC's copy (bytes past n are never read)
+            *reinterpret_cast<uint4*>(stage + o) = make_uint4(y[0], y[1], y[2], y[3]);
+          }
         }
       }
     }
   }
   if (SEAL) {
     // the ciphertext other lanes stored, before the MAC reads it
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    cw_old_mac(aad, j.aad_len, aad_global, dst, n, pw, pad, mac);
+    if (staged) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    cw_old_mac(aad, j.aad_len, aad_global, staged ? stage : dst, n, !staged, pw, pad, mac);
     if (lane < tag_len) dst[n + lane] = (uint8_t)cw_mac_byte(mac, lane);
     if (lane == 0) *status = (int32_t)(n + tag_len);
     return;

@@ -130,7 +130,7 @@ __device__ __forceinline__ void srv_chacha_old_job(const BatchArgs& a, const Raw
     if (threadIdx.x == 0) a.status[0] = TLSGPU_REC_PUBLIC_INVALID;
     return;
   }
-  cc_wave_job_old<SEAL>(j, S, a.status, !inl);
+  cc_wave_job_old<SEAL>(j, S, a.status, !inl, s_lds + SRV_STAGE_OFF);
 }
 
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
