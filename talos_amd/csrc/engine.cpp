@@ -1298,6 +1298,8 @@ struct ImagePool {
   std::vector<std::pair<uint8_t*, uint8_t*>> free;  // (host, device view)
 };
 constexpr size_t kImageBytes = sizeof(DevSession) + sizeof(DevGcmTables);
+constexpr size_t kImageSlab = 32;
+static_assert(kImageBytes % 256 == 0, "session images stay 256-B aligned in a slab");
 static ImagePool g_img_pool[64];
 static bool image_take(int dev, uint8_t** h, uint8_t** d) {
   if (dev < 0 || dev >= 64) return false;
@@ -1310,13 +1312,24 @@ static bool image_take(int dev, uint8_t** h, uint8_t** d) {
       return true;
     }
   }
+  // none free: one pinned slab of kImageSlab images (one hipHostMalloc per 32
+  // contexts instead of one per context; held for the process, like the pool)
+  uint8_t *hs = nullptr, *ds = nullptr;
   if (hipSetDevice(dev) != hipSuccess ||
-      hipHostMalloc((void**)h, kImageBytes, hipHostMallocDefault) != hipSuccess)
+      hipHostMalloc((void**)&hs, kImageBytes * kImageSlab, hipHostMallocDefault) != hipSuccess)
     return false;
-  if (hipHostGetDevicePointer((void**)d, *h, 0) != hipSuccess) {
-    (void)hipHostFree(*h);
+  if (hipHostGetDevicePointer((void**)&ds, hs, 0) != hipSuccess) {
+    (void)hipHostFree(hs);
     return false;
   }
+  memset(hs, 0, kImageBytes * kImageSlab);
+  {
+    std::lock_guard<std::mutex> lk(g_img_pool[dev].mu);
+    for (size_t i = 1; i < kImageSlab; i++)
+      g_img_pool[dev].free.emplace_back(hs + i * kImageBytes, ds + i * kImageBytes);
+  }
+  *h = hs;
+  *d = ds;
   return true;
 }
 static void image_give(int dev, uint8_t* h, uint8_t* d) {
