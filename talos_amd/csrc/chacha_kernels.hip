@@ -241,7 +241,7 @@ __device__ __forceinline__ void cc_block_lds(uint32_t x[16], const uint8_t* key,
 
 // One wave: records r = (first record of the wave) + lane, one per lane
 // (t1_enc.c:832-975 for the ChaCha suites, e_chacha20poly1305.c:124-286).
-template <bool SEAL>
+template <bool SEAL, bool LATE_STORES>
 __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8_t* tile,
                             uint8_t* keys) {
   // --- parse (the fields the end of the record needs are re-derived there)
@@ -335,14 +335,29 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
       }
     }
   };
+  // Step order.  LATE_STORES (round 5): the scatter of step s reads its pieces
+  // from the tile into registers, the tile takes step s + 1's gathered pieces
+  // in the same pass (the lane's own slots, so no wave sync between), and only
+  // then are step s's stores and step s + 2's loads issued.  vmcnt counts loads
+  // and stores together and the compiler waits for zero when both are pending,
+  // so a tile fill right after the stores (the other order) makes every step
+  // wait for its previous step's write acknowledgements, which are slow for the
+  // partial lines a straddling window writes; with LATE_STORES everything the
+  // fill waits for was issued before the step's compute.
   uint4 pf[kCcP];
   gather(0, pf);
+  if (LATE_STORES) {
+#pragma unroll
+    for (int k = 0; k < kCcP; k++) *reinterpret_cast<uint4*>(tile + 1024u * k + 16u * lane) = pf[k];
+    if (steps > 1) gather(kCcStep, pf);
+  }
   for (uint32_t s = 0; s < steps; s++) {
     const uint32_t base = s * kCcStep;
+    if (!LATE_STORES) {
 #pragma unroll
-    for (int k = 0; k < kCcP; k++)
-      *reinterpret_cast<uint4*>(tile + 1024u * k + 16u * lane) = pf[k];
-    if (s + 1 < steps) gather(base + kCcStep, pf);
+      for (int k = 0; k < kCcP; k++) *reinterpret_cast<uint4*>(tile + 1024u * k + 16u * lane) = pf[k];
+      if (s + 1 < steps) gather(base + kCcStep, pf);
+    }
     lds_wave_sync();
     // en/decrypt + MAC this lane's row: 2 ChaCha blocks
     if (base < n && !(a.hy_flags & kCcDiagNoCompute)) {
@@ -379,16 +394,26 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
       }
     }
     lds_wave_sync();
-    // scatter
+    // scatter.  LATE_STORES: one wait for everything issued before the compute
+    // (step s + 1's loads, step s - 1's stores), then per piece: read the slot,
+    // refill it with step s + 1's piece, store the read piece
+    const bool refill = LATE_STORES && s + 1 < steps;
+    if (LATE_STORES) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) only
 #pragma unroll
     for (int k = 0; k < kCcP; k++) {
       const uint32_t rr = kCcR * k + lane / kCcP;
       const uint32_t off = base + 16u * (((lane % kCcP) - (rr >> 1)) & 7u);
       const uint32_t snk = __shfl(n, (int)rr);
       const uint64_t dstk = shfl64((uint64_t)(uintptr_t)dst, rr);
+      uint4* tslot = reinterpret_cast<uint4*>(tile + 1024u * k + 16u * lane);
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (LATE_STORES) {
+        v = *tslot;
+        if (refill) *tslot = pf[k];
+      }
       if (off < snk && !(a.hy_flags & kCcDiagNoStores)) {
         uint8_t* dp = (uint8_t*)(uintptr_t)dstk + off;
-        const uint4 v = *reinterpret_cast<const uint4*>(tile + 1024u * k + 16u * lane);
+        if (!LATE_STORES) v = *tslot;
         if (off + 16 <= snk && ((uintptr_t)dp & 15) == 0) {
           gstore16(dp, v);
         } else if (off + 16 <= snk) {
@@ -401,7 +426,11 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
         }
       }
     }
-    lds_wave_sync();
+    if (LATE_STORES) {
+      if (s + 2 < steps) gather(base + 2 * kCcStep, pf);
+    } else {
+      lds_wave_sync();
+    }
   }
   if (!active) return;
   poly_block(p, 13u, 0, n, 0, 1u << 24);  // le64(ad_len) || le64(ct_len)
@@ -535,7 +564,22 @@ __global__ __launch_bounds__(kCcThreads) void chacha_tls_kernel(BatchArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t tiles[kCcThreads / kWave][kCcTile];
   __shared__ __attribute__((aligned(16))) uint8_t keys[kCcThreads / kWave][kCcKeys];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  cc_tls_wave<SEAL>(a, blockIdx.x * blockDim.x + threadIdx.x, lane, tiles[wave], keys[wave]);
+  cc_tls_wave<SEAL, false>(a, blockIdx.x * blockDim.x + threadIdx.x, lane, tiles[wave], keys[wave]);
+}
+// the LATE_STORES order; W4: held to 128 VGPRs (4 waves per SIMD)
+template <bool SEAL>
+__global__ __launch_bounds__(kCcThreads) void chacha_tls_late_kernel(BatchArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t tiles[kCcThreads / kWave][kCcTile];
+  __shared__ __attribute__((aligned(16))) uint8_t keys[kCcThreads / kWave][kCcKeys];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  cc_tls_wave<SEAL, true>(a, blockIdx.x * blockDim.x + threadIdx.x, lane, tiles[wave], keys[wave]);
+}
+template <bool SEAL>
+__global__ __launch_bounds__(kCcThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void chacha_tls_late_w4_kernel(BatchArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t tiles[kCcThreads / kWave][kCcTile];
+  __shared__ __attribute__((aligned(16))) uint8_t keys[kCcThreads / kWave][kCcKeys];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  cc_tls_wave<SEAL, true>(a, blockIdx.x * blockDim.x + threadIdx.x, lane, tiles[wave], keys[wave]);
 }
 
 // Per-lane data path: raw EVP jobs, TLS records of the draft suite (OLD_ONLY:
@@ -651,8 +695,24 @@ int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, h
     }();
     BatchArgs b = a;
     b.hy_flags = diag;
-    if (seal) hipLaunchKernelGGL((chacha_tls_kernel<true>), grid, block, pad, s, b);
-    else hipLaunchKernelGGL((chacha_tls_kernel<false>), grid, block, pad, s, b);
+    // TLSGPU_CC_ORDER (A/B): 0 tile fill after the stores (round 3-4), 1
+    // LATE_STORES (131 VGPRs, 3 waves per SIMD), 2 (default) LATE_STORES held
+    // to 4 waves per SIMD (5 spilled VGPRs): C +0.6 %, wire C +1.8 % over 0
+    // (profiles/r05w_ab_cc_order.txt)
+    static const int order = [] {
+      const char* e = getenv("TLSGPU_CC_ORDER");
+      return e ? atoi(e) : 2;
+    }();
+    if (order == 1) {
+      if (seal) hipLaunchKernelGGL((chacha_tls_late_kernel<true>), grid, block, pad, s, b);
+      else hipLaunchKernelGGL((chacha_tls_late_kernel<false>), grid, block, pad, s, b);
+    } else if (order == 2) {
+      if (seal) hipLaunchKernelGGL((chacha_tls_late_w4_kernel<true>), grid, block, pad, s, b);
+      else hipLaunchKernelGGL((chacha_tls_late_w4_kernel<false>), grid, block, pad, s, b);
+    } else {
+      if (seal) hipLaunchKernelGGL((chacha_tls_kernel<true>), grid, block, pad, s, b);
+      else hipLaunchKernelGGL((chacha_tls_kernel<false>), grid, block, pad, s, b);
+    }
   }
   if (old) {
     if (seal) hipLaunchKernelGGL((chacha_batch_kernel<true, false, true>), grid, block, 0, s, a);
