@@ -691,3 +691,25 @@ def test_batch_per_wave_session_kernel_forced(ta):
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=110,
                        env=env, cwd=ROOT)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+
+
+# Randomized differential sweep (round 5): each seed draws a batch shape the
+# fixed cases above do not combine — a random mix of the four AEADs over up to
+# 9 sessions, lengths weighted toward the block / pack / step edges (0..20000),
+# per-record input shifts, grouped or interleaved order, any hint word — and
+# the whole seal + open round trip (every 5th record tampered) must equal the
+# oracle's tls1_enc byte for byte.
+EDGE_LENGTHS = [0, 1, 15, 16, 17, 63, 64, 65, 991, 992, 993, 1023, 1024, 1025, 1400, 4095,
+                4096, 4097, 16383, 16384, 16385]
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_batch_random_differential(ta, engine, oracle, seed):
+    rnd = random.Random(9000 + seed)
+    kinds = [rnd.choice(list(KINDS.values())) for _ in range(rnd.randint(1, 9))]
+    lengths = [rnd.choice(EDGE_LENGTHS) if rnd.random() < 0.5 else rnd.randrange(0, 20001)
+               for _ in range(rnd.randint(4, 24))]
+    shifts = [rnd.choice([0, 0, 0, 1, 3, 8, 13]) for _ in range(len(kinds) * len(lengths))]
+    _run_seal_open(ta, engine, oracle, kinds, lengths, grouped=rnd.random() < 0.5,
+                   in_shift=shifts, out_shift=rnd.choice([0, 0, 5]), seed=seed,
+                   in_place=False, hints=rnd.choice([0, 0, 1, 2, 3]))

@@ -682,7 +682,10 @@ __device__ __forceinline__ void st16_pol(void* p, v4u_t v) {
   else if constexpr (POL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
   else asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(p), "v"(v) : "memory");
 }
-template <int STEP, int POL = 0>
+// SHIFT (round 5): a record whose output starts 64 B into a line has its
+// windows shifted back by 64 B in record space (still whole 64-B ChaCha
+// blocks), so its writes are line-aligned; offsets 32 / 96 keep straddling.
+template <int STEP, int POL = 0, bool SHIFT = false>
 __global__ void __launch_bounds__(256) copy_records(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                     uint32_t nrec, uint32_t len, uint32_t in_stride,
                                                     uint32_t in_off, uint32_t out_stride, uint32_t out_off) {
@@ -694,18 +697,21 @@ __global__ void __launch_bounds__(256) copy_records(const uint8_t* __restrict__ 
   const uint32_t r0 = wave * 64;
   if (r0 >= nrec) return;
   const uint32_t piece = 16 * (lane % LPR);
-  for (uint32_t s = 0; s * STEP < len; s++) {
+  const uint32_t span = SHIFT ? len + 64 : len;
+  for (uint32_t s = 0; s * STEP < span; s++) {
     v4u_t x[NI];
 #pragma unroll
     for (int i = 0; i < NI; i++) {
       const uint32_t r = r0 + i * RPI + lane / LPR;
-      const uint32_t o = s * STEP + piece;
+      const uint32_t sh = SHIFT ? (uint32_t)(((size_t)r * out_stride + out_off) & 64) : 0u;
+      const uint32_t o = s * STEP + piece - sh;  // wraps (large) before the record
       x[i] = o < len ? *(const v4u_t*)(in + (size_t)r * in_stride + in_off + o) : v4u_t{0, 0, 0, 0};
     }
 #pragma unroll
     for (int i = 0; i < NI; i++) {
       const uint32_t r = r0 + i * RPI + lane / LPR;
-      const uint32_t o = s * STEP + piece;
+      const uint32_t sh = SHIFT ? (uint32_t)(((size_t)r * out_stride + out_off) & 64) : 0u;
+      const uint32_t o = s * STEP + piece - sh;
       if (o < len) st16_pol<POL>(out + (size_t)r * out_stride + out_off + o, x[i]);
     }
   }
@@ -925,7 +931,7 @@ static void set6() {
   CK(hipMalloc(&a, cap));
   CK(hipMalloc(&b, cap));
   CK(hipMemset(a, 1, cap));
-  struct V { const char* name; int step; uint32_t is, io, os, oo; int pol = 0; };
+  struct V { const char* name; int step; uint32_t is, io, os, oo; int pol = 0; bool shift = false; };
   const V vs[] = {
       {"seal_like_1408_to_1440+8", 128, 1408, 0, 1440, 8},
       {"open_like_1440+8_to_1408", 128, 1440, 8, 1408, 0},
@@ -938,11 +944,14 @@ static void set6() {
       {"seal_like_store_sc1", 128, 1408, 0, 1440, 8, 2},
       {"seal_like_store_sc0sc1", 128, 1408, 0, 1440, 8, 3},
       {"seal_like_1408_to_1440+0", 128, 1408, 0, 1440, 0},
+      {"seal_like_1408_to_1440+0_shift64", 128, 1408, 0, 1440, 0, 0, true},
   };
   for (const V& v : vs) {
     auto launch = [&]() {
       const uint32_t blocks = nrec / 64 / 4;
-      if (v.step == 128 && v.pol == 1)
+      if (v.shift)
+        copy_records<128, 0, true><<<blocks, 256>>>(a, b, nrec, len, v.is, v.io, v.os, v.oo);
+      else if (v.step == 128 && v.pol == 1)
         copy_records<128, 1><<<blocks, 256>>>(a, b, nrec, len, v.is, v.io, v.os, v.oo);
       else if (v.step == 128 && v.pol == 2)
         copy_records<128, 2><<<blocks, 256>>>(a, b, nrec, len, v.is, v.io, v.os, v.oo);
