@@ -560,22 +560,23 @@ __device__ __forceinline__ void cc_parse_raw(const RawJob& j, const DevSession* 
 
 // TLS batches: LDS-staged coalesced data path (cc_tls_wave), 4 waves per SIMD.
 template <bool SEAL>
-__global__ __launch_bounds__(kCcThreads) void chacha_tls_kernel(BatchArgs a) {
+__global__ __launch_bounds__(kCcThreads) void chacha_tls_r4_kernel(BatchArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t tiles[kCcThreads / kWave][kCcTile];
   __shared__ __attribute__((aligned(16))) uint8_t keys[kCcThreads / kWave][kCcKeys];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   cc_tls_wave<SEAL, false>(a, blockIdx.x * blockDim.x + threadIdx.x, lane, tiles[wave], keys[wave]);
 }
-// the LATE_STORES order; W4: held to 128 VGPRs (4 waves per SIMD)
+// the LATE_STORES order at 3 waves per SIMD (131 VGPRs; A/B only), and held
+// to 128 VGPRs (4 waves per SIMD): the default chacha_tls_kernel
 template <bool SEAL>
-__global__ __launch_bounds__(kCcThreads) void chacha_tls_late_kernel(BatchArgs a) {
+__global__ __launch_bounds__(kCcThreads) void chacha_tls_late3_kernel(BatchArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t tiles[kCcThreads / kWave][kCcTile];
   __shared__ __attribute__((aligned(16))) uint8_t keys[kCcThreads / kWave][kCcKeys];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   cc_tls_wave<SEAL, true>(a, blockIdx.x * blockDim.x + threadIdx.x, lane, tiles[wave], keys[wave]);
 }
 template <bool SEAL>
-__global__ __launch_bounds__(kCcThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void chacha_tls_late_w4_kernel(BatchArgs a) {
+__global__ __launch_bounds__(kCcThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void chacha_tls_kernel(BatchArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t tiles[kCcThreads / kWave][kCcTile];
   __shared__ __attribute__((aligned(16))) uint8_t keys[kCcThreads / kWave][kCcKeys];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -704,11 +705,11 @@ int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, h
       return e ? atoi(e) : 2;
     }();
     if (order == 1) {
-      if (seal) hipLaunchKernelGGL((chacha_tls_late_kernel<true>), grid, block, pad, s, b);
-      else hipLaunchKernelGGL((chacha_tls_late_kernel<false>), grid, block, pad, s, b);
-    } else if (order == 2) {
-      if (seal) hipLaunchKernelGGL((chacha_tls_late_w4_kernel<true>), grid, block, pad, s, b);
-      else hipLaunchKernelGGL((chacha_tls_late_w4_kernel<false>), grid, block, pad, s, b);
+      if (seal) hipLaunchKernelGGL((chacha_tls_late3_kernel<true>), grid, block, pad, s, b);
+      else hipLaunchKernelGGL((chacha_tls_late3_kernel<false>), grid, block, pad, s, b);
+    } else if (order == 0) {
+      if (seal) hipLaunchKernelGGL((chacha_tls_r4_kernel<true>), grid, block, pad, s, b);
+      else hipLaunchKernelGGL((chacha_tls_r4_kernel<false>), grid, block, pad, s, b);
     } else {
       if (seal) hipLaunchKernelGGL((chacha_tls_kernel<true>), grid, block, pad, s, b);
       else hipLaunchKernelGGL((chacha_tls_kernel<false>), grid, block, pad, s, b);
