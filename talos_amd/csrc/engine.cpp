@@ -339,9 +339,20 @@ extern "C" int tlsgpu_aes_ecb_bitsliced(tlsgpu_sessions* t, uint32_t session, co
 #endif
 }
 
+// TLSGPU_WG_PER_CU (A/B): workgroups per CU.  Only one 16-wave workgroup fits
+// a CU at a time (LDS), so k > 1 gives each CU k ranges in turn, handed out by
+// the dispatcher as CUs free up: a CU that runs fast takes more of them.
+static uint32_t wg_per_cu() {
+  static const uint32_t v = [] {
+    const char* e = getenv("TLSGPU_WG_PER_CU");
+    const long k = e ? strtol(e, nullptr, 10) : 1;
+    return (uint32_t)(k < 1 ? 1 : (k > 4 ? 4 : k));
+  }();
+  return v;
+}
 static int groups_for(const tlsgpu_engine* e, uint32_t n, uint32_t* per_group) {
   // one persistent 16-wave workgroup per CU, contiguous record ranges
-  uint32_t groups = (uint32_t)e->num_cus;
+  uint32_t groups = (uint32_t)e->num_cus * wg_per_cu();
   uint32_t min_per = 16;
   if ((uint64_t)groups * min_per > n) groups = (n + min_per - 1) / min_per;
   if (groups == 0) groups = 1;

@@ -22,12 +22,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="D")
     ap.add_argument("--launches", type=int, default=3)
+    ap.add_argument("--records", type=int, default=0, help="override the config's records")
+    ap.add_argument("--sustained", type=int, default=0,
+                    help="launch this many batches back to back before each timed one")
     args = ap.parse_args()
     os.environ.setdefault("TLSGPU_WG_TIMES", "1")
     import bench
     import talos_amd as ta
     from talos_amd.workload import Workload, zipf_lengths
     kind_name, per_gpu, sessions, rec_len, seed, op = bench.CONFIGS[args.config]
+    if args.records:
+        sessions = max(1, sessions * args.records // per_gpu)
+        per_gpu = args.records
     ta.load_library()
     eng = ta.Engine(0)
     kind = ta.AEAD_NAMES[kind_name]
@@ -44,6 +50,8 @@ def main():
     wl.open(None)
     eng.sync()
     for it in range(args.launches):
+        for _ in range(args.sustained):   # the timed launch then follows without a gap
+            wl.open(None)
         wl.open(None)
         eng.sync()
         t = np.array(ta.debug_wg_times(eng, groups), dtype=np.int64)
@@ -53,7 +61,7 @@ def main():
         runs = np.zeros(len(st))
         span = (en.max() - st.min()) / 100.0
         out = {
-            "launch": it, "balance": os.environ.get("TLSGPU_BALANCE", "default"), "pieces": os.environ.get("TLSGPU_PIECES", "0"),
+            "launch": it, "records": per_gpu, "sustained": args.sustained, "balance": os.environ.get("TLSGPU_BALANCE", "default"), "pieces": os.environ.get("TLSGPU_PIECES", "0"),
             "span_us": round(span, 1),
             "start_spread_us": round((st.max() - st.min()) / 100.0, 1),
             "end_spread_us": round((en.max() - en.min()) / 100.0, 1),
