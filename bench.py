@@ -7,7 +7,8 @@ One step = one tlsgpu_open_batch over the whole resident batch (64 Ki records,
 1 GiB of ciphertext in HBM -> 1 GiB of plaintext in HBM + per-record status).
 Inputs are synthetic (counter-SplitMix64 plaintexts, 1024 sessions x 64 records,
 1/1024 records tampered), sealed on the device beforehand by the validated
-sealer; every step's outputs are verified after the warmup.
+sealer; the first step's outputs are verified before the warm-up steps (so the
+GPU is busy up to the timed region) and the last timed step's after it.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config B|C|D]
                   [--sessions S] [--interleave] [--mode device|host|wire|copy]
@@ -223,7 +224,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # 30: the GPU reaches its working clock after ~30 ms of back-to-back steps
+    # (B: warm-up 3 / 10 / 30 / 60 / 100 -> 953 / 1,028 / 1,065 / 1,053 / 1,069
+    # GiB/s; profiles/r05ag_bench_warm_start.txt); a warm-up is untimed
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
     ap.add_argument("--records", type=int, default=0, help="override records per GPU")
     ap.add_argument("--sessions", type=int, default=0,
@@ -319,10 +323,15 @@ def main():
             wl.seal(stream)
             wl.open(stream)
 
-    for _ in range(max(1, args.warmup)):
-        step()
+    # the first step's outputs are verified before the warm-up, not after it:
+    # the verification's host round trips leave the GPU idle for tens of ms,
+    # and the timed region must start at the working clock the warm-up reached
+    # (profiles/r05ag_bench_warm_start.txt)
+    step()
     eng.sync()
     wl.verify_open()
+    for _ in range(max(1, args.warmup)):
+        step()
 
     def barrier():
         eng.sync()
@@ -511,12 +520,13 @@ def group_mode(args, world, rank):
             wl.lengths + ta.EXPLICIT_NONCE_LEN[kind] + ta.TAG_LEN, wl.session, seal=False)
         ta._check(g.lib.tlsgpu_sessions_hint(g.lib.tlsgpu_group_sessions_member(gs.handle, k),
                                              hints), "tlsgpu_sessions_hint")
-    for _ in range(max(1, args.warmup)):
-        gs.batch(shard_arr, seal=False)
+    gs.batch(shard_arr, seal=False)     # verified first, then warmed (as the device mode)
     g.sync()
     for wl in wls:
         wl.verify_open()
     evs = [(ta.Event(m), ta.Event(m)) for m in members]
+    for _ in range(max(1, args.warmup)):
+        gs.batch(shard_arr, seal=False)
     g.sync()
     t0 = time.perf_counter()
     for e0, _ in evs:
