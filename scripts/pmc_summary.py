@@ -15,16 +15,23 @@ import sys
 
 run, prefix, out = sys.argv[1], sys.argv[2], sys.argv[3]
 label = sys.argv[4] if len(sys.argv) > 4 else ""
+# LAST=N (round 5): only each pass's last N launches of the kernel — the timed
+# steps of a warm-start bench run (the warm-up's launches ramp the clock)
+last = int(os.environ.get("LAST", "0"))
 vals = collections.defaultdict(list)
 durs = []
 for f in sorted(glob.glob(os.path.join(run, "pmc*", "pmc_counter_collection.csv"))):
-    for r in csv.DictReader(open(f)):
-        if r["Kernel_Name"].startswith(prefix):
+    rows = [r for r in csv.DictReader(open(f)) if r["Kernel_Name"].startswith(prefix)]
+    ids = sorted({int(r["Dispatch_Id"]) for r in rows})
+    keep = set(ids[-last:]) if last else set(ids)
+    for r in rows:
+        if int(r["Dispatch_Id"]) in keep:
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
 for f in sorted(glob.glob(os.path.join(run, "pmc*", "pmc_kernel_trace.csv"))):
-    for r in csv.DictReader(open(f)):
-        if r["Kernel_Name"].startswith(prefix):
-            durs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    rows = sorted((r for r in csv.DictReader(open(f)) if r["Kernel_Name"].startswith(prefix)),
+                  key=lambda r: int(r["Start_Timestamp"]))
+    for r in (rows[-last:] if last else rows):
+        durs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 mean = {k: sum(v) / len(v) for k, v in vals.items()}
 # the bench line each profiled pass printed (same process as its PMC and kernel trace)
 bench = []
@@ -35,6 +42,7 @@ for f in sorted(glob.glob(os.path.join(run, "pmc*.log"))):
             bench.append({"pass": os.path.basename(f), "value": d["value"],
                           "ms_per_step": d["ms_per_step"]})
 res = {"kernel": prefix, "label": label, "launches_sampled": len(durs),
+       "last_launches_per_pass": last or None,
        "mean_duration_ns_profiled": sum(durs) / len(durs) if durs else None,
        "counters_per_launch_mean": mean, "bench_lines_of_these_passes": bench}
 if durs and bench:  # the main kernel must fit in the step it was timed in
