@@ -437,14 +437,27 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
   uint32_t mac[4];
   poly_finish(p, mac);
   int32_t* slot = a.status + r;
+  // full 16-B tags through dword accesses (one instruction per dword instead
+  // of one per byte: each lane's tag is in another record); truncated tags
+  // byte by byte
   if (SEAL) {
     uint8_t* tag_out = dst + n;
-    for (uint32_t k = 0; k < tag_len; k++) tag_out[k] = (uint8_t)(mac[k >> 2] >> (8 * (k & 3)));
+    if (tag_len == 16) {
+      store16_any(tag_out, mac);
+    } else {
+      for (uint32_t k = 0; k < tag_len; k++) tag_out[k] = (uint8_t)(mac[k >> 2] >> (8 * (k & 3)));
+    }
     *slot = (int32_t)(n + tag_len);
   } else {
     const uint8_t* tag_in = src + n;
     uint32_t diff = 0;
-    for (uint32_t k = 0; k < tag_len; k++) diff |= tag_in[k] ^ ((mac[k >> 2] >> (8 * (k & 3))) & 0xFF);
+    if (tag_len == 16) {  // every byte compared (timingsafe_memcmp)
+      uint32_t t[4];
+      load16_any(tag_in, t);
+      diff = (t[0] ^ mac[0]) | (t[1] ^ mac[1]) | (t[2] ^ mac[2]) | (t[3] ^ mac[3]);
+    } else {
+      for (uint32_t k = 0; k < tag_len; k++) diff |= tag_in[k] ^ ((mac[k >> 2] >> (8 * (k & 3))) & 0xFF);
+    }
     if (diff) {
       zero_fill_lane(dst, n);
       *slot = TLSGPU_REC_BAD_MAC;
