@@ -154,13 +154,23 @@ __device__ void cc_record(const CcRec& rc, uint32_t tag_len, int32_t* status_slo
   }
   uint32_t mac[4];
   poly_finish(p, mac);
-  if (SEAL) {
-    for (uint32_t k = 0; k < tag_len; k++) rc.tag_out[k] = (uint8_t)(mac[k >> 2] >> (8 * (k & 3)));
+  if (SEAL) {  // 16-B tags through dword accesses (as cc_tls_wave)
+    if (tag_len == 16) {
+      store16_any(rc.tag_out, mac);
+    } else {
+      for (uint32_t k = 0; k < tag_len; k++) rc.tag_out[k] = (uint8_t)(mac[k >> 2] >> (8 * (k & 3)));
+    }
     *status_slot = rc.ok_status;
   } else {
     uint32_t diff = 0;
-    for (uint32_t k = 0; k < tag_len; k++)
-      diff |= rc.tag_in[k] ^ ((mac[k >> 2] >> (8 * (k & 3))) & 0xFF);
+    if (tag_len == 16) {  // every byte compared (timingsafe_memcmp)
+      uint32_t t[4];
+      load16_any(rc.tag_in, t);
+      diff = (t[0] ^ mac[0]) | (t[1] ^ mac[1]) | (t[2] ^ mac[2]) | (t[3] ^ mac[3]);
+    } else {
+      for (uint32_t k = 0; k < tag_len; k++)
+        diff |= rc.tag_in[k] ^ ((mac[k >> 2] >> (8 * (k & 3))) & 0xFF);
+    }
     if (diff) {
       zero_fill_lane(rc.dst, rc.zero_len);
       *status_slot = TLSGPU_REC_BAD_MAC;
@@ -573,14 +583,14 @@ __device__ __forceinline__ void cc_parse_raw(const RawJob& j, const DevSession* 
 
 // TLS batches: LDS-staged coalesced data path (cc_tls_wave), 4 waves per SIMD.
 template <bool SEAL>
-__global__ __launch_bounds__(kCcThreads) void chacha_tls_r4_kernel(BatchArgs a) {
+__global__ __launch_bounds__(kCcThreads) void chacha_tls_kernel(BatchArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t tiles[kCcThreads / kWave][kCcTile];
   __shared__ __attribute__((aligned(16))) uint8_t keys[kCcThreads / kWave][kCcKeys];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   cc_tls_wave<SEAL, false>(a, blockIdx.x * blockDim.x + threadIdx.x, lane, tiles[wave], keys[wave]);
 }
-// the LATE_STORES order at 3 waves per SIMD (131 VGPRs; A/B only), and held
-// to 128 VGPRs (4 waves per SIMD): the default chacha_tls_kernel
+// the LATE_STORES order (A/B only, TLSGPU_CC_ORDER): at 3 waves per SIMD (131
+// VGPRs), and held to 128 VGPRs (4 waves per SIMD, 5 spilled)
 template <bool SEAL>
 __global__ __launch_bounds__(kCcThreads) void chacha_tls_late3_kernel(BatchArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t tiles[kCcThreads / kWave][kCcTile];
@@ -589,7 +599,7 @@ __global__ __launch_bounds__(kCcThreads) void chacha_tls_late3_kernel(BatchArgs 
   cc_tls_wave<SEAL, true>(a, blockIdx.x * blockDim.x + threadIdx.x, lane, tiles[wave], keys[wave]);
 }
 template <bool SEAL>
-__global__ __launch_bounds__(kCcThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void chacha_tls_kernel(BatchArgs a) {
+__global__ __launch_bounds__(kCcThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void chacha_tls_late4_kernel(BatchArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t tiles[kCcThreads / kWave][kCcTile];
   __shared__ __attribute__((aligned(16))) uint8_t keys[kCcThreads / kWave][kCcKeys];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -709,20 +719,21 @@ int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, h
     }();
     BatchArgs b = a;
     b.hy_flags = diag;
-    // TLSGPU_CC_ORDER (A/B): 0 tile fill after the stores (round 3-4), 1
-    // LATE_STORES (131 VGPRs, 3 waves per SIMD), 2 (default) LATE_STORES held
-    // to 4 waves per SIMD (5 spilled VGPRs): C +0.6 %, wire C +1.8 % over 0
-    // (profiles/r05w_ab_cc_order.txt)
+    // TLSGPU_CC_ORDER (A/B): 0 (default) tile fill after the stores, 1
+    // LATE_STORES (131 VGPRs, 3 waves per SIMD), 2 LATE_STORES held to 4 waves
+    // per SIMD (5 spilled VGPRs).  2 measured +0.6 % on C in the clock dip of
+    // the old bench order, then -0.9 % with the warm-start bench
+    // (profiles/r05w_ab_cc_order.txt, r05am_ab_warm.txt)
     static const int order = [] {
       const char* e = getenv("TLSGPU_CC_ORDER");
-      return e ? atoi(e) : 2;
+      return e ? atoi(e) : 0;
     }();
     if (order == 1) {
       if (seal) hipLaunchKernelGGL((chacha_tls_late3_kernel<true>), grid, block, pad, s, b);
       else hipLaunchKernelGGL((chacha_tls_late3_kernel<false>), grid, block, pad, s, b);
-    } else if (order == 0) {
-      if (seal) hipLaunchKernelGGL((chacha_tls_r4_kernel<true>), grid, block, pad, s, b);
-      else hipLaunchKernelGGL((chacha_tls_r4_kernel<false>), grid, block, pad, s, b);
+    } else if (order == 2) {
+      if (seal) hipLaunchKernelGGL((chacha_tls_late4_kernel<true>), grid, block, pad, s, b);
+      else hipLaunchKernelGGL((chacha_tls_late4_kernel<false>), grid, block, pad, s, b);
     } else {
       if (seal) hipLaunchKernelGGL((chacha_tls_kernel<true>), grid, block, pad, s, b);
       else hipLaunchKernelGGL((chacha_tls_kernel<false>), grid, block, pad, s, b);
