@@ -204,6 +204,8 @@ constexpr uint32_t kCcKeys = kWave * 32;       // the lanes' ChaCha keys, 2 KiB 
 // stores, or the ChaCha / Poly1305 work, to split the kernel's time.  The
 // results are then wrong; never set outside that harness.
 constexpr uint32_t kCcDiagNoLoads = 1, kCcDiagNoStores = 2, kCcDiagNoCompute = 4;
+// TLSGPU_CC_NARROW=0 (A/B): 64-bit pointer shuffles even when NARROW applies
+constexpr uint32_t kCcNoNarrow = 8;  // (host-side only)
 
 // tile offset of piece q (0..7) of row r
 __device__ __forceinline__ uint32_t cc_slot(uint32_t r, uint32_t q) {
@@ -251,70 +253,21 @@ __device__ __forceinline__ void cc_block_lds(uint32_t x[16], const uint8_t* key,
 
 // One wave: records r = (first record of the wave) + lane, one per lane
 // (t1_enc.c:832-975 for the ChaCha suites, e_chacha20poly1305.c:124-286).
-template <bool SEAL, bool LATE_STORES>
-__device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8_t* tile,
-                            uint8_t* keys) {
-  // --- parse (the fields the end of the record needs are re-derived there)
-  bool active = false;
-  uint32_t n = 0, tag_len = 16, c13 = 0, c14 = 0, c15 = 0;
-  uint32_t ad2 = 0;  // AD word 2 (type, version, length high byte); words 0-1 = c14/c15 (RFC)
-  const uint8_t* src = nullptr;
-  uint8_t* dst = nullptr;
-  uint32_t sq_hi = 0, sq_lo = 0;
-  if (r < a.n) {
-    const tlsgpu_record d = reinterpret_cast<const tlsgpu_record*>(a.descs)[r];
-    // fused (round 5, engine.cpp run_batch: a batch of RFC ChaCha sessions
-    // only): the caller's descriptors, checked here by check_record_bounds's
-    // rule, and the initial status of a record this kernel does not run
-    int32_t st0 = TLSGPU_REC_PUBLIC_INVALID;
-    if (d.session < a.n_sessions) {  // else the status stays PUBLIC_INVALID
-      const DevSession* S = a.sessions + d.session;
-      const uint32_t kind = S->kind;
-      bool in_bounds = true;
-      if (a.fused) {
-        const uint64_t len = d.len_type & 0xFFFFFFu, tag = S->tag_len;
-        const uint64_t eiv = S->nonce_in_record ? 8u : 0u;
-        const uint64_t out_len = SEAL ? len + eiv + tag : (len >= eiv + tag ? len - eiv - tag : 0);
-        in_bounds = !(d.in_off > a.in_bytes || len > a.in_bytes - d.in_off ||
-                      d.out_off > a.out_bytes || out_len > a.out_bytes - d.out_off);
-        if (!in_bounds) st0 = TLSGPU_REC_OUT_OF_BOUNDS;
-      }
-      if (kind == TLSGPU_CHACHA20_POLY1305 && in_bounds) {  // the draft ("old") suite: chacha_batch_kernel
-        tag_len = S->tag_len;
-        const uint32_t len = d.len_type & 0xFFFFFFu, type = d.len_type >> 24;
-        if (!SEAL && len < tag_len) {  // t1_enc.c:958-959 (no explicit nonce for ChaCha)
-          a.status[r] = TLSGPU_REC_PUBLIC_INVALID;
-        } else {
-          active = true;
-          n = SEAL ? len : len - tag_len;
-          src = a.in + d.in_off;
-          dst = a.out + d.out_off;
-          // nonce: RFC 7905 fixed(12) XOR (0^4 || seq)
-          sq_hi = bswap32((uint32_t)(d.seq >> 32));
-          sq_lo = bswap32((uint32_t)d.seq);
-          const uint32_t* fx = reinterpret_cast<const uint32_t*>(S->fixed_nonce);
-          c13 = fx[0];
-          c14 = fx[1] ^ sq_hi;
-          c15 = fx[2] ^ sq_lo;
-          const uint32_t v = S->version;
-          ad2 = type | (((v >> 8) & 0xFF) << 8) | ((v & 0xFF) << 16) | (((n >> 8) & 0xFF) << 24);
-          const uint4* kw = reinterpret_cast<const uint4*>(S->chacha_key);
-          reinterpret_cast<uint4*>(keys)[lane] = kw[0];
-          reinterpret_cast<uint4*>(keys)[kWave + lane] = kw[1];
-        }
-      }
-    }
-    if (a.fused && !active) a.status[r] = st0;
-  }
-  uint8_t* key = keys + 16u * lane;
-  lds_wave_sync();
-  Poly p;
-  if (active) {
-    uint32_t ks[16];
-    cc_block_lds(ks, key, 0u, c13, c14, c15);  // counter 0 block -> one-time Poly1305 key
-    poly_init(p, ks);
-    poly_block(p, sq_hi, sq_lo, ad2, n & 0xFF, 1u << 24);  // 13-B AD, pad16
-  }
+// The staged loop and the record's end.  NARROW (round 5): every source and
+// destination pointer shares its high 32 bits with its buffer's base (one
+// uniform word per side), so a piece's pointer is one ds_bpermute of the low
+// word instead of two.
+template <bool SEAL, bool LATE_STORES, bool NARROW>
+__device__ __forceinline__ void cc_tls_body(const BatchArgs& a, uint32_t r, uint32_t lane, uint8_t* tile,
+                                            uint8_t* key, bool active, uint32_t n, uint32_t tag_len,
+                                            uint32_t c13, uint32_t c14, uint32_t c15,
+                                            const uint8_t* src, uint8_t* dst, uint32_t src_hi,
+                                            uint32_t dst_hi, Poly& p) {
+  auto ptr_of = [&](const void* q, uint32_t hi, uint32_t rr) -> uint64_t {
+    if (NARROW)
+      return ((uint64_t)hi << 32) | (uint32_t)__shfl((int)(uint32_t)(uintptr_t)q, (int)rr);
+    return shfl64((uint64_t)(uintptr_t)q, rr);
+  };
   // pieces this lane moves: records 8k + lane/8, piece (lane % 8 - record/2) % 8
   // of each step; the records' pointers and lengths are fetched with ds_bpermute
   // per step (keeping 8 x 5 of them in VGPRs would cost a wave per SIMD)
@@ -331,7 +284,7 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
       const uint32_t off = base + 16u * (((lane % kCcP) - (rr >> 1)) & 7u);
       const uint32_t snk = __shfl(n, (int)rr);
       // ds_bpermute outside the branch: an inactive source lane reads as 0
-      const uint64_t srck = shfl64((uint64_t)(uintptr_t)src, rr);
+      const uint64_t srck = ptr_of(src, src_hi, rr);
       v[k] = make_uint4(0, 0, 0, 0);
       if (off < snk && !(a.hy_flags & kCcDiagNoLoads)) {
         const uint8_t* sp = (const uint8_t*)(uintptr_t)srck + off;
@@ -414,7 +367,7 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
       const uint32_t rr = kCcR * k + lane / kCcP;
       const uint32_t off = base + 16u * (((lane % kCcP) - (rr >> 1)) & 7u);
       const uint32_t snk = __shfl(n, (int)rr);
-      const uint64_t dstk = shfl64((uint64_t)(uintptr_t)dst, rr);
+      const uint64_t dstk = ptr_of(dst, dst_hi, rr);
       uint4* tslot = reinterpret_cast<uint4*>(tile + 1024u * k + 16u * lane);
       uint4 v = make_uint4(0, 0, 0, 0);
       if (LATE_STORES) {
@@ -475,6 +428,78 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
       *slot = (int32_t)n;
     }
   }
+}
+
+template <bool SEAL, bool LATE_STORES, bool NARROW = false>
+__device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8_t* tile,
+                            uint8_t* keys) {
+  // --- parse (the fields the end of the record needs are re-derived there)
+  bool active = false;
+  uint32_t n = 0, tag_len = 16, c13 = 0, c14 = 0, c15 = 0;
+  uint32_t ad2 = 0;  // AD word 2 (type, version, length high byte); words 0-1 = c14/c15 (RFC)
+  const uint8_t* src = nullptr;
+  uint8_t* dst = nullptr;
+  uint32_t sq_hi = 0, sq_lo = 0;
+  if (r < a.n) {
+    const tlsgpu_record d = reinterpret_cast<const tlsgpu_record*>(a.descs)[r];
+    // fused (round 5, engine.cpp run_batch: a batch of RFC ChaCha sessions
+    // only): the caller's descriptors, checked here by check_record_bounds's
+    // rule, and the initial status of a record this kernel does not run
+    int32_t st0 = TLSGPU_REC_PUBLIC_INVALID;
+    if (d.session < a.n_sessions) {  // else the status stays PUBLIC_INVALID
+      const DevSession* S = a.sessions + d.session;
+      const uint32_t kind = S->kind;
+      bool in_bounds = true;
+      if (a.fused) {
+        const uint64_t len = d.len_type & 0xFFFFFFu, tag = S->tag_len;
+        const uint64_t eiv = S->nonce_in_record ? 8u : 0u;
+        const uint64_t out_len = SEAL ? len + eiv + tag : (len >= eiv + tag ? len - eiv - tag : 0);
+        in_bounds = !(d.in_off > a.in_bytes || len > a.in_bytes - d.in_off ||
+                      d.out_off > a.out_bytes || out_len > a.out_bytes - d.out_off);
+        if (!in_bounds) st0 = TLSGPU_REC_OUT_OF_BOUNDS;
+      }
+      if (kind == TLSGPU_CHACHA20_POLY1305 && in_bounds) {  // the draft ("old") suite: chacha_batch_kernel
+        tag_len = S->tag_len;
+        const uint32_t len = d.len_type & 0xFFFFFFu, type = d.len_type >> 24;
+        if (!SEAL && len < tag_len) {  // t1_enc.c:958-959 (no explicit nonce for ChaCha)
+          a.status[r] = TLSGPU_REC_PUBLIC_INVALID;
+        } else {
+          active = true;
+          n = SEAL ? len : len - tag_len;
+          src = a.in + d.in_off;
+          dst = a.out + d.out_off;
+          // nonce: RFC 7905 fixed(12) XOR (0^4 || seq)
+          sq_hi = bswap32((uint32_t)(d.seq >> 32));
+          sq_lo = bswap32((uint32_t)d.seq);
+          const uint32_t* fx = reinterpret_cast<const uint32_t*>(S->fixed_nonce);
+          c13 = fx[0];
+          c14 = fx[1] ^ sq_hi;
+          c15 = fx[2] ^ sq_lo;
+          const uint32_t v = S->version;
+          ad2 = type | (((v >> 8) & 0xFF) << 8) | ((v & 0xFF) << 16) | (((n >> 8) & 0xFF) << 24);
+          const uint4* kw = reinterpret_cast<const uint4*>(S->chacha_key);
+          reinterpret_cast<uint4*>(keys)[lane] = kw[0];
+          reinterpret_cast<uint4*>(keys)[kWave + lane] = kw[1];
+        }
+      }
+    }
+    if (a.fused && !active) a.status[r] = st0;
+  }
+  uint8_t* key = keys + 16u * lane;
+  lds_wave_sync();
+  Poly p;
+  if (active) {
+    uint32_t ks[16];
+    cc_block_lds(ks, key, 0u, c13, c14, c15);  // counter 0 block -> one-time Poly1305 key
+    poly_init(p, ks);
+    poly_block(p, sq_hi, sq_lo, ad2, n & 0xFF, 1u << 24);  // 13-B AD, pad16
+  }
+  // NARROW (the launch's choice, launch_chacha): the batch's input and output
+  // buffers each lie in one 4 GiB window, so every pointer's high word is the
+  // buffer base's
+  cc_tls_body<SEAL, LATE_STORES, NARROW>(a, r, lane, tile, key, active, n, tag_len, c13, c14, c15,
+                                         src, dst, (uint32_t)((uintptr_t)a.in >> 32),
+                                         (uint32_t)((uintptr_t)a.out >> 32), p);
 }
 
 __device__ __forceinline__ void cc_state(uint32_t st[16], const DevSession* S) {
@@ -583,11 +608,22 @@ __device__ __forceinline__ void cc_parse_raw(const RawJob& j, const DevSession* 
 
 // TLS batches: LDS-staged coalesced data path (cc_tls_wave), 4 waves per SIMD.
 template <bool SEAL>
-__global__ __launch_bounds__(kCcThreads) void chacha_tls_kernel(BatchArgs a) {
+__global__ __launch_bounds__(kCcThreads) void chacha_tls_wide_kernel(BatchArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t tiles[kCcThreads / kWave][kCcTile];
   __shared__ __attribute__((aligned(16))) uint8_t keys[kCcThreads / kWave][kCcKeys];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   cc_tls_wave<SEAL, false>(a, blockIdx.x * blockDim.x + threadIdx.x, lane, tiles[wave], keys[wave]);
+}
+// the same with 32-bit pointer shuffles (NARROW: cc_tls_body) — what a fused
+// batch (bounds known, buffers in one 4 GiB window each) runs: C +0.6 %
+// (profiles/r05ap_ab_cc_narrow.txt); 64-bit shuffles otherwise
+template <bool SEAL>
+__global__ __launch_bounds__(kCcThreads) void chacha_tls_kernel(BatchArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t tiles[kCcThreads / kWave][kCcTile];
+  __shared__ __attribute__((aligned(16))) uint8_t keys[kCcThreads / kWave][kCcKeys];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  cc_tls_wave<SEAL, false, true>(a, blockIdx.x * blockDim.x + threadIdx.x, lane, tiles[wave],
+                                 keys[wave]);
 }
 // the LATE_STORES order (A/B only, TLSGPU_CC_ORDER): at 3 waves per SIMD (131
 // VGPRs), and held to 128 VGPRs (4 waves per SIMD, 5 spilled)
@@ -717,8 +753,20 @@ int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, h
       const char* e = getenv("TLSGPU_CC_DIAG");
       return e ? (uint32_t)strtoul(e, nullptr, 0) & 7u : 0u;
     }();
+    static const uint32_t no_narrow = [] {
+      const char* e = getenv("TLSGPU_CC_NARROW");
+      return e && *e == '0' ? kCcNoNarrow : 0u;
+    }();
     BatchArgs b = a;
     b.hy_flags = diag;
+    // NARROW needs the buffer sizes (a fused batch: run_batch passes them): the
+    // kernel then rebuilds a piece's pointer from the buffer base's high word
+    auto one_window = [](const void* base, uint64_t bytes) {
+      const uint64_t lo = (uint64_t)(uintptr_t)base, hi = lo + (bytes ? bytes - 1 : 0);
+      return (lo >> 32) == (hi >> 32);
+    };
+    const bool narrow = !no_narrow && a.fused && one_window(a.in, a.in_bytes) &&
+                        one_window(a.out, a.out_bytes);
     // TLSGPU_CC_ORDER (A/B): 0 (default) tile fill after the stores, 1
     // LATE_STORES (131 VGPRs, 3 waves per SIMD), 2 LATE_STORES held to 4 waves
     // per SIMD (5 spilled VGPRs).  2 measured +0.6 % on C in the clock dip of
@@ -734,9 +782,12 @@ int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, h
     } else if (order == 2) {
       if (seal) hipLaunchKernelGGL((chacha_tls_late4_kernel<true>), grid, block, pad, s, b);
       else hipLaunchKernelGGL((chacha_tls_late4_kernel<false>), grid, block, pad, s, b);
-    } else {
+    } else if (narrow) {
       if (seal) hipLaunchKernelGGL((chacha_tls_kernel<true>), grid, block, pad, s, b);
       else hipLaunchKernelGGL((chacha_tls_kernel<false>), grid, block, pad, s, b);
+    } else {
+      if (seal) hipLaunchKernelGGL((chacha_tls_wide_kernel<true>), grid, block, pad, s, b);
+      else hipLaunchKernelGGL((chacha_tls_wide_kernel<false>), grid, block, pad, s, b);
     }
   }
   if (old) {
