@@ -253,20 +253,20 @@ __device__ __forceinline__ void cc_block_lds(uint32_t x[16], const uint8_t* key,
 
 // One wave: records r = (first record of the wave) + lane, one per lane
 // (t1_enc.c:832-975 for the ChaCha suites, e_chacha20poly1305.c:124-286).
-// The staged loop and the record's end.  NARROW (round 5): every source and
-// destination pointer shares its high 32 bits with its buffer's base (one
-// uniform word per side), so a piece's pointer is one ds_bpermute of the low
-// word instead of two.
+// The staged loop and the record's end.  NARROW (round 5): every record's
+// offset in its buffer fits 32 bits, so a piece's pointer is one ds_bpermute
+// of that offset (plus the buffer base) instead of two of the 64-bit pointer.
 template <bool SEAL, bool LATE_STORES, bool NARROW>
 __device__ __forceinline__ void cc_tls_body(const BatchArgs& a, uint32_t r, uint32_t lane, uint8_t* tile,
                                             uint8_t* key, bool active, uint32_t n, uint32_t tag_len,
                                             uint32_t c13, uint32_t c14, uint32_t c15,
-                                            const uint8_t* src, uint8_t* dst, uint32_t src_hi,
-                                            uint32_t dst_hi, Poly& p) {
-  auto ptr_of = [&](const void* q, uint32_t hi, uint32_t rr) -> uint64_t {
-    if (NARROW)
-      return ((uint64_t)hi << 32) | (uint32_t)__shfl((int)(uint32_t)(uintptr_t)q, (int)rr);
-    return shfl64((uint64_t)(uintptr_t)q, rr);
+                                            uint64_t src_v, uint64_t dst_v, Poly& p) {
+  // src_v / dst_v: the record's pointers, or with NARROW its 32-bit offsets in
+  // the caller's buffers (an active record lies inside them, each at most
+  // 4 GiB; an inactive lane's value is never used: its length shuffles as 0)
+  auto ptr_of = [&](uint64_t v, const void* base, uint32_t rr) -> uint64_t {
+    if (NARROW) return (uint64_t)(uintptr_t)base + (uint32_t)__shfl((int)(uint32_t)v, (int)rr);
+    return shfl64(v, rr);
   };
   // pieces this lane moves: records 8k + lane/8, piece (lane % 8 - record/2) % 8
   // of each step; the records' pointers and lengths are fetched with ds_bpermute
@@ -284,7 +284,7 @@ __device__ __forceinline__ void cc_tls_body(const BatchArgs& a, uint32_t r, uint
       const uint32_t off = base + 16u * (((lane % kCcP) - (rr >> 1)) & 7u);
       const uint32_t snk = __shfl(n, (int)rr);
       // ds_bpermute outside the branch: an inactive source lane reads as 0
-      const uint64_t srck = ptr_of(src, src_hi, rr);
+      const uint64_t srck = ptr_of(src_v, a.in, rr);
       v[k] = make_uint4(0, 0, 0, 0);
       if (off < snk && !(a.hy_flags & kCcDiagNoLoads)) {
         const uint8_t* sp = (const uint8_t*)(uintptr_t)srck + off;
@@ -367,7 +367,7 @@ __device__ __forceinline__ void cc_tls_body(const BatchArgs& a, uint32_t r, uint
       const uint32_t rr = kCcR * k + lane / kCcP;
       const uint32_t off = base + 16u * (((lane % kCcP) - (rr >> 1)) & 7u);
       const uint32_t snk = __shfl(n, (int)rr);
-      const uint64_t dstk = ptr_of(dst, dst_hi, rr);
+      const uint64_t dstk = ptr_of(dst_v, a.out, rr);
       uint4* tslot = reinterpret_cast<uint4*>(tile + 1024u * k + 16u * lane);
       uint4 v = make_uint4(0, 0, 0, 0);
       if (LATE_STORES) {
@@ -396,6 +396,8 @@ __device__ __forceinline__ void cc_tls_body(const BatchArgs& a, uint32_t r, uint
     }
   }
   if (!active) return;
+  const uint8_t* src = NARROW ? a.in + (uint32_t)src_v : (const uint8_t*)(uintptr_t)src_v;
+  uint8_t* dst = NARROW ? a.out + (uint32_t)dst_v : (uint8_t*)(uintptr_t)dst_v;
   poly_block(p, 13u, 0, n, 0, 1u << 24);  // le64(ad_len) || le64(ct_len)
   uint32_t mac[4];
   poly_finish(p, mac);
@@ -494,12 +496,14 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
     poly_init(p, ks);
     poly_block(p, sq_hi, sq_lo, ad2, n & 0xFF, 1u << 24);  // 13-B AD, pad16
   }
-  // NARROW (the launch's choice, launch_chacha): the batch's input and output
-  // buffers each lie in one 4 GiB window, so every pointer's high word is the
-  // buffer base's
+  // NARROW (the launch's choice, launch_chacha): a fused batch whose buffers
+  // are at most 4 GiB each, so a record's offset fits 32 bits
   cc_tls_body<SEAL, LATE_STORES, NARROW>(a, r, lane, tile, key, active, n, tag_len, c13, c14, c15,
-                                         src, dst, (uint32_t)((uintptr_t)a.in >> 32),
-                                         (uint32_t)((uintptr_t)a.out >> 32), p);
+                                         NARROW ? (uint64_t)(uint32_t)(src - a.in)
+                                                : (uint64_t)(uintptr_t)src,
+                                         NARROW ? (uint64_t)(uint32_t)(dst - a.out)
+                                                : (uint64_t)(uintptr_t)dst,
+                                         p);
 }
 
 __device__ __forceinline__ void cc_state(uint32_t st[16], const DevSession* S) {
@@ -615,7 +619,7 @@ __global__ __launch_bounds__(kCcThreads) void chacha_tls_wide_kernel(BatchArgs a
   cc_tls_wave<SEAL, false>(a, blockIdx.x * blockDim.x + threadIdx.x, lane, tiles[wave], keys[wave]);
 }
 // the same with 32-bit pointer shuffles (NARROW: cc_tls_body) — what a fused
-// batch (bounds known, buffers in one 4 GiB window each) runs: C +0.6 %
+// batch (bounds known, buffers of at most 4 GiB) runs: C +0.6 %
 // (profiles/r05ap_ab_cc_narrow.txt); 64-bit shuffles otherwise
 template <bool SEAL>
 __global__ __launch_bounds__(kCcThreads) void chacha_tls_kernel(BatchArgs a) {
@@ -759,14 +763,11 @@ int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, h
     }();
     BatchArgs b = a;
     b.hy_flags = diag;
-    // NARROW needs the buffer sizes (a fused batch: run_batch passes them): the
-    // kernel then rebuilds a piece's pointer from the buffer base's high word
-    auto one_window = [](const void* base, uint64_t bytes) {
-      const uint64_t lo = (uint64_t)(uintptr_t)base, hi = lo + (bytes ? bytes - 1 : 0);
-      return (lo >> 32) == (hi >> 32);
-    };
-    const bool narrow = !no_narrow && a.fused && one_window(a.in, a.in_bytes) &&
-                        one_window(a.out, a.out_bytes);
+    // NARROW needs the buffer sizes (a fused batch: run_batch passes them, and
+    // the kernel runs only records inside them): a piece's pointer is then the
+    // buffer base + a 32-bit offset
+    const bool narrow = !no_narrow && a.fused && a.in_bytes <= (1ull << 32) &&
+                        a.out_bytes <= (1ull << 32);
     // TLSGPU_CC_ORDER (A/B): 0 (default) tile fill after the stores, 1
     // LATE_STORES (131 VGPRs, 3 waves per SIMD), 2 LATE_STORES held to 4 waves
     // per SIMD (5 spilled VGPRs).  2 measured +0.6 % on C in the clock dip of
