@@ -703,7 +703,8 @@ EDGE_LENGTHS = [0, 1, 15, 16, 17, 63, 64, 65, 991, 992, 993, 1023, 1024, 1025, 1
                 4096, 4097, 16383, 16384, 16385]
 
 
-@pytest.mark.parametrize("seed", range(12))
+# TLSGPU_FUZZ_SEEDS=<n> widens the sweep for a soak run (default 12 seeds)
+@pytest.mark.parametrize("seed", range(int(os.environ.get("TLSGPU_FUZZ_SEEDS", "12"))))
 def test_batch_random_differential(ta, engine, oracle, seed):
     rnd = random.Random(9000 + seed)
     kinds = [rnd.choice(list(KINDS.values())) for _ in range(rnd.randint(1, 9))]
