@@ -206,6 +206,8 @@ constexpr uint32_t kCcKeys = kWave * 32;       // the lanes' ChaCha keys, 2 KiB 
 constexpr uint32_t kCcDiagNoLoads = 1, kCcDiagNoStores = 2, kCcDiagNoCompute = 4;
 // TLSGPU_CC_NARROW=0 (A/B): 64-bit pointer shuffles even when NARROW applies
 constexpr uint32_t kCcNoNarrow = 8;  // (host-side only)
+// TLSGPU_CC_UKEY=0 (A/B): keys from LDS even for one-session waves
+constexpr uint32_t kCcNoUkey = 16;
 
 // tile offset of piece q (0..7) of row r
 __device__ __forceinline__ uint32_t cc_slot(uint32_t r, uint32_t q) {
@@ -251,14 +253,40 @@ __device__ __forceinline__ void cc_block_lds(uint32_t x[16], const uint8_t* key,
   x[12] += c12; x[13] += c13; x[14] += c14; x[15] += c15;
 }
 
+// The same block with the key words of a wave-uniform session read through
+// the constant address space (s_load: SGPRs, no LDS reads; UKEY below).
+__device__ __forceinline__ void cc_block_sk(uint32_t x[16], cu32c* k, uint32_t c12, uint32_t c13,
+                                            uint32_t c14, uint32_t c15) {
+  x[0] = 0x61707865u; x[1] = 0x3320646eu; x[2] = 0x79622d32u; x[3] = 0x6b206574u;
+#pragma unroll
+  for (int i = 0; i < 8; i++) x[4 + i] = k[i];
+  x[12] = c12; x[13] = c13; x[14] = c14; x[15] = c15;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    CC_QR(x[0], x[4], x[8], x[12]);
+    CC_QR(x[1], x[5], x[9], x[13]);
+    CC_QR(x[2], x[6], x[10], x[14]);
+    CC_QR(x[3], x[7], x[11], x[15]);
+    CC_QR(x[0], x[5], x[10], x[15]);
+    CC_QR(x[1], x[6], x[11], x[12]);
+    CC_QR(x[2], x[7], x[8], x[13]);
+    CC_QR(x[3], x[4], x[9], x[14]);
+  }
+  x[0] += 0x61707865u; x[1] += 0x3320646eu; x[2] += 0x79622d32u; x[3] += 0x6b206574u;
+#pragma unroll
+  for (int i = 0; i < 8; i++) x[4 + i] += k[i];
+  x[12] += c12; x[13] += c13; x[14] += c14; x[15] += c15;
+}
+
 // One wave: records r = (first record of the wave) + lane, one per lane
 // (t1_enc.c:832-975 for the ChaCha suites, e_chacha20poly1305.c:124-286).
 // The staged loop and the record's end.  NARROW (round 5): every record's
 // offset in its buffer fits 32 bits, so a piece's pointer is one ds_bpermute
 // of that offset (plus the buffer base) instead of two of the 64-bit pointer.
-template <bool SEAL, bool LATE_STORES, bool NARROW>
+template <bool SEAL, bool LATE_STORES, bool NARROW, bool UKEY = false>
 __device__ __forceinline__ void cc_tls_body(const BatchArgs& a, uint32_t r, uint32_t lane, uint8_t* tile,
-                                            uint8_t* key, bool active, uint32_t n, uint32_t tag_len,
+                                            uint8_t* key, cu32c* ukey, bool active, uint32_t n,
+                                            uint32_t tag_len,
                                             uint32_t c13, uint32_t c14, uint32_t c15,
                                             uint64_t src_v, uint64_t dst_v, Poly& p) {
   // src_v / dst_v: the record's pointers, or with NARROW its 32-bit offsets in
@@ -330,7 +358,8 @@ __device__ __forceinline__ void cc_tls_body(const BatchArgs& a, uint32_t r, uint
         if (o64 >= n) break;
         ctr += 1;  // data blocks count from 1 (chacha-merged.c:230-236; TLS records < 2^32 blocks)
         uint32_t ks[16];
-        cc_block_lds(ks, key, ctr, c13, c14, c15);
+        if (UKEY) cc_block_sk(ks, ukey, ctr, c13, c14, c15);
+        else cc_block_lds(ks, key, ctr, c13, c14, c15);
 #pragma unroll
         for (int q = 0; q < 4; q++) {
           const uint32_t o = o64 + 16 * q;
@@ -442,6 +471,7 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
   const uint8_t* src = nullptr;
   uint8_t* dst = nullptr;
   uint32_t sq_hi = 0, sq_lo = 0;
+  uint32_t sess = 0xFFFFFFFFu;
   if (r < a.n) {
     const tlsgpu_record d = reinterpret_cast<const tlsgpu_record*>(a.descs)[r];
     // fused (round 5, engine.cpp run_batch: a batch of RFC ChaCha sessions
@@ -467,6 +497,7 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
           a.status[r] = TLSGPU_REC_PUBLIC_INVALID;
         } else {
           active = true;
+          sess = d.session;
           n = SEAL ? len : len - tag_len;
           src = a.in + d.in_off;
           dst = a.out + d.out_off;
@@ -498,12 +529,23 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
   }
   // NARROW (the launch's choice, launch_chacha): a fused batch whose buffers
   // are at most 4 GiB each, so a record's offset fits 32 bits
-  cc_tls_body<SEAL, LATE_STORES, NARROW>(a, r, lane, tile, key, active, n, tag_len, c13, c14, c15,
-                                         NARROW ? (uint64_t)(uint32_t)(src - a.in)
-                                                : (uint64_t)(uintptr_t)src,
-                                         NARROW ? (uint64_t)(uint32_t)(dst - a.out)
-                                                : (uint64_t)(uintptr_t)dst,
-                                         p);
+  const uint64_t sv = NARROW ? (uint64_t)(uint32_t)(src - a.in) : (uint64_t)(uintptr_t)src;
+  const uint64_t dv = NARROW ? (uint64_t)(uint32_t)(dst - a.out) : (uint64_t)(uintptr_t)dst;
+  // UKEY (NARROW kernels): every active lane's record is of one session, so
+  // the key words come from that session through s_load, not from LDS
+  const uint64_t act = __ballot(active);
+  const int l0 = act ? __ffsll((long long)act) - 1 : 0;
+  const uint32_t sid0 = __builtin_amdgcn_readlane(sess, l0);
+  const bool ukey = NARROW && act != 0 && !__any(active && sess != sid0) &&
+                    !(a.hy_flags & kCcNoUkey);
+  if (ukey) {
+    cu32c* k = (cu32c*)(const uint32_t*)a.sessions[sid0].chacha_key;
+    cc_tls_body<SEAL, LATE_STORES, NARROW, true>(a, r, lane, tile, key, k, active, n, tag_len, c13,
+                                                 c14, c15, sv, dv, p);
+  } else {
+    cc_tls_body<SEAL, LATE_STORES, NARROW, false>(a, r, lane, tile, key, nullptr, active, n,
+                                                  tag_len, c13, c14, c15, sv, dv, p);
+  }
 }
 
 __device__ __forceinline__ void cc_state(uint32_t st[16], const DevSession* S) {
@@ -761,8 +803,12 @@ int launch_chacha(const BatchArgs& a, bool seal, bool raw, bool rfc, bool old, h
       const char* e = getenv("TLSGPU_CC_NARROW");
       return e && *e == '0' ? kCcNoNarrow : 0u;
     }();
+    static const uint32_t no_ukey = [] {
+      const char* e = getenv("TLSGPU_CC_UKEY");
+      return e && *e == '0' ? kCcNoUkey : 0u;
+    }();
     BatchArgs b = a;
-    b.hy_flags = diag;
+    b.hy_flags = diag | no_ukey;
     // NARROW needs the buffer sizes (a fused batch: run_batch passes them, and
     // the kernel runs only records inside them): a piece's pointer is then the
     // buffer base + a 32-bit offset
