@@ -531,12 +531,12 @@ __device__ void cc_tls_wave(const BatchArgs& a, uint32_t r, uint32_t lane, uint8
   // are at most 4 GiB each, so a record's offset fits 32 bits
   const uint64_t sv = NARROW ? (uint64_t)(uint32_t)(src - a.in) : (uint64_t)(uintptr_t)src;
   const uint64_t dv = NARROW ? (uint64_t)(uint32_t)(dst - a.out) : (uint64_t)(uintptr_t)dst;
-  // UKEY (NARROW kernels): every active lane's record is of one session, so
+  // UKEY: every active lane's record is of one session, so
   // the key words come from that session through s_load, not from LDS
   const uint64_t act = __ballot(active);
   const int l0 = act ? __ffsll((long long)act) - 1 : 0;
   const uint32_t sid0 = __builtin_amdgcn_readlane(sess, l0);
-  const bool ukey = NARROW && act != 0 && !__any(active && sess != sid0) &&
+  const bool ukey = act != 0 && !__any(active && sess != sid0) &&
                     !(a.hy_flags & kCcNoUkey);
   if (ukey) {
     cu32c* k = (cu32c*)(const uint32_t*)a.sessions[sid0].chacha_key;
