@@ -367,6 +367,14 @@ def test_batch_misaligned(ta, engine, oracle, name):
                    in_shift=3, out_shift=5, seed=12)
 
 
+def test_batch_chacha_interleaved_sessions(ta, engine, oracle):
+    """RFC 7539 sessions only (the fused staged kernel) with the records of 5
+    sessions interleaved: most waves hold several sessions and read their keys
+    from LDS, the grouped cases above take the one-session s_load keys (UKEY)."""
+    _run_seal_open(ta, engine, oracle, [po.CHACHA20_POLY1305] * 5,
+                   [0, 1, 15, 16, 17, 64, 65, 1400, 1401, 4096, 16384], grouped=False, seed=15)
+
+
 def test_batch_interleaved_sessions_mixed_kinds(ta, engine, oracle):
     kinds = [po.AES_128_GCM, po.AES_256_GCM, po.CHACHA20_POLY1305, po.AES_128_GCM,
              po.CHACHA20_POLY1305_OLD, po.AES_256_GCM]
