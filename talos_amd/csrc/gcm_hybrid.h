@@ -1078,7 +1078,10 @@ __global__ __launch_bounds__(NT, 1) void gcm_hy_kernel(BatchArgs a,
           // over the final records, so the run's tail ends together instead of
           // one straggler per SIMD running alone before the barrier
           const uint32_t left = run_end - r;
-          if (!BSW && !PACK && left <= 3 * kWaves) {
+#ifndef TG_TAIL_WIN
+#define TG_TAIL_WIN 3  // tail window in claims of kWaves records (A/B: TG_TAIL_WIN=2/4)
+#endif
+          if (!BSW && !PACK && left <= TG_TAIL_WIN * kWaves) {
             if (left <= kWaves) __builtin_amdgcn_s_setprio(3);
             else if (left <= 2 * kWaves) __builtin_amdgcn_s_setprio(2);
             else __builtin_amdgcn_s_setprio(1);
