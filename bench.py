@@ -265,7 +265,7 @@ def main():
     from talos_amd.workload import Workload, zipf_lengths
 
     world, rank, local = env_rank()
-    if choose_split(args.split, world, args.devices) == "group" and args.mode == "device":
+    if choose_split(args.split, world, args.devices, args.gpus) == "group" and args.mode == "device":
         return group_mode(args, world, rank)
     ta.load_library()
     eng = ta.Engine(device_for(local, ta.device_count()))  # first GPU runtime user
@@ -442,12 +442,13 @@ def main():
     eng.close()
 
 
-def choose_split(split: str | None, world: int, devices: str) -> str:
-    """The multi-GPU split a run measures: the C ABI's group split for N > 1
-    ranks or an explicit device list, one engine per rank otherwise."""
+def choose_split(split: str | None, world: int, devices: str, gpus: int = 1) -> str:
+    """The multi-GPU split a run measures: the C ABI's group split for N > 1 GPUs
+    — asked for by --gpus N (with or without a launcher), by N > 1 ranks or by
+    an explicit device list — one engine per rank otherwise."""
     if split:
         return split
-    return "group" if world > 1 or devices else "ranks"
+    return "group" if world > 1 or gpus > 1 or devices else "ranks"
 
 
 def group_devices(devices: str, gpus: int, world: int) -> list[int]:
@@ -459,6 +460,20 @@ def group_devices(devices: str, gpus: int, world: int) -> list[int]:
             raise SystemExit(f"bad --devices {devices!r}")
         return out
     return list(range(max(gpus, world, 1)))
+
+
+def check_devices(devices: list[int], visible: int, explicit: bool) -> None:
+    """A run that asks for N GPUs measures N distinct GPUs or fails: exit
+    non-zero when a member device is not visible.  An explicit --devices list
+    may repeat an id on purpose (the '0,0' one-GPU rehearsal), never name an
+    invisible one."""
+    if visible <= 0:
+        raise SystemExit("no GPU visible")
+    if max(devices) >= visible:
+        raise SystemExit(f"{len(devices)} GPUs asked for (devices {devices}) but only {visible} "
+                         "visible: refusing to measure fewer")
+    if not explicit and len(set(devices)) != len(devices):
+        raise SystemExit(f"duplicate devices {devices}")
 
 
 def group_mode(args, world, rank):
@@ -483,6 +498,7 @@ def group_mode(args, world, rank):
         return
     ta.load_library()
     devices = group_devices(args.devices, args.gpus, world)
+    check_devices(devices, ta.device_count(), bool(args.devices))
     n = len(devices)
     cfg = "E" if args.config in ("B", "E") else args.config
     if cfg != "E":
@@ -541,8 +557,12 @@ def group_mode(args, world, rank):
     for wl in wls:
         wl.verify_open()
     total_len = sum(int(wl.lengths.sum()) for wl in wls)
-    value = total_len * args.steps / wall_s / GIB
-    per_launch_s = max(dev_ms) / 1e3 / args.steps
+    # the same timing method as N = 1: HIP events around the K steps on each
+    # member's stream; the slowest member sets the step time (max over GPUs,
+    # as max over ranks); wall clock as a second field
+    slowest_s = max(dev_ms) / 1e3
+    value = total_len * args.steps / slowest_s / GIB
+    per_launch_s = slowest_s / args.steps
     algo = sum(algo_bytes_per_record(kind_name, int(l), op) for l in wls[0].lengths.tolist())
     algo_rd = sum(algo_bytes_per_record(kind_name, int(l), op, True)
                   for l in wls[0].lengths.tolist())
@@ -551,7 +571,9 @@ def group_mode(args, world, rank):
     line = {
         "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": n,
         "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(wall_s * 1e3 / args.steps, 4),
+        "ms_per_step": round(slowest_s * 1e3 / args.steps, 4),
+        "wall_ms_per_step": round(wall_s * 1e3 / args.steps, 4),
+        "wall_value": round(total_len * args.steps / wall_s / GIB, 3),
         "member_device_ms_per_step": [round(x / args.steps, 4) for x in dev_ms],
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (counter-SplitMix64 plaintexts sealed on device; 1/1024 tampered)",
@@ -571,8 +593,10 @@ def group_mode(args, world, rank):
                      "read_achieved": round(algo_rd / per_launch_s / 1e9, 1),
                      "read_frac": round(algo_rd / per_launch_s / 1e9 / HBM_PEAK_GBS, 4),
                      "kernel": kernel, "traffic_source": traffic_src,
-                     "timing": "per GPU: HIP events on the slowest member's stream; value: "
-                               "wall clock around the K group calls + tlsgpu_group_sync"},
+                     "timing": "HIP events around the K steps on every member's stream; "
+                               "value and ms_per_step from the slowest member (as N = 1 from "
+                               "its one stream); wall_value: wall clock around the K group "
+                               "calls + tlsgpu_group_sync"},
     }
     if n == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(kind_name, rec_len, op)

@@ -1646,9 +1646,11 @@ static hipEvent_t slot_event(tlsgpu_sessions* t, uint32_t slot) {
 // arguments, and the area is zeroed once its copy has finished
 // (sweep_key_areas after the thread's next synchronised call, or when the
 // area is reused).  TLSGPU_EVP_DEVICE_INSTALL=1 keeps the device install.
+// A host without AES-NI or PCLMUL builds no host image (session_host.cpp: no
+// table-driven key schedule on the CPU) and takes the device install too.
 static const bool g_device_install = [] {
   const char* v = getenv("TLSGPU_EVP_DEVICE_INSTALL");
-  return v && *v && *v != '0';
+  return (v && *v && *v != '0') || !host_crypto_ok();
 }();
 
 static int install_one(tlsgpu_sessions* t, uint32_t slot, const tlsgpu_session_params& p,

@@ -371,6 +371,7 @@ constexpr uint32_t kGcmTableUploadBytes = offsetof(DevGcmTables, bsrk);
 #endif
 // session_host.cpp: the image install_body writes, built on the host (the
 // bitsliced masks only when a kernel of this build reads them)
+bool host_crypto_ok();  // AES-NI + PCLMUL present: the host image can be built
 bool host_session_image(const tlsgpu_session_params& p, DevSession* s, DevGcmTables* t,
                         bool bitsliced_masks = kGcmTableUploadBytes > offsetof(DevGcmTables, bsrk));
 int launch_check_bounds(const tlsgpu_record* recs, tlsgpu_record* safe, uint32_t n,

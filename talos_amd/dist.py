@@ -17,10 +17,18 @@ def env_rank():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def device_for(local_rank: int, visible: int) -> int:
-    """GPU of a local rank (wraps when fewer GPUs than ranks are visible)."""
+def device_for(local_rank: int, visible: int, allow_shared: bool | None = None) -> int:
+    """GPU of a local rank.  Fewer visible GPUs than ranks is an error (a run
+    asked for N GPUs must measure N, not wrap onto fewer), unless sharing is
+    asked for explicitly: `allow_shared` or TLSGPU_ALLOW_SHARED_GPU=1 (the
+    N-ranks-on-one-GPU rehearsal), which wraps."""
     if visible <= 0:
         raise RuntimeError("no GPU visible")
+    if allow_shared is None:
+        allow_shared = os.environ.get("TLSGPU_ALLOW_SHARED_GPU", "") == "1"
+    if local_rank >= visible and not allow_shared:
+        raise RuntimeError(f"local rank {local_rank} needs GPU {local_rank}, but only {visible} "
+                           "visible (TLSGPU_ALLOW_SHARED_GPU=1 to share GPUs on purpose)")
     return local_rank % visible
 
 

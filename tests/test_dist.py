@@ -29,11 +29,17 @@ def test_shard_zipf_balanced_and_disjoint():
         assert max(per) - min(per) <= 2 * 16384
 
 
-def test_device_for_wraps():
+def test_device_for_refuses_fewer_gpus(monkeypatch):
+    monkeypatch.delenv("TLSGPU_ALLOW_SHARED_GPU", raising=False)
     assert [device_for(r, 8) for r in range(8)] == list(range(8))
-    assert [device_for(r, 1) for r in range(4)] == [0, 0, 0, 0]
+    with pytest.raises(RuntimeError):
+        device_for(1, 1)           # rank 1 of a 2-GPU run on a 1-GPU box: no silent wrap
     with pytest.raises(RuntimeError):
         device_for(0, 0)
+    # sharing only on explicit request (the N-ranks-on-one-GPU rehearsal)
+    assert [device_for(r, 1, allow_shared=True) for r in range(4)] == [0, 0, 0, 0]
+    monkeypatch.setenv("TLSGPU_ALLOW_SHARED_GPU", "1")
+    assert device_for(3, 2) == 1
 
 
 def _free_port():
@@ -82,13 +88,46 @@ def test_bench_split_plumbing():
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
     assert bench.choose_split(None, 1, "") == "ranks"
+    assert bench.choose_split(None, 1, "", 1) == "ranks"
     assert bench.choose_split(None, 8, "") == "group"
     assert bench.choose_split(None, 1, "0,0") == "group"
     assert bench.choose_split("ranks", 8, "") == "ranks"
     assert bench.choose_split("group", 1, "") == "group"
+    # `python bench.py --gpus 8` with no launcher (world 1) measures 8 GPUs
+    assert bench.choose_split(None, 1, "", 8) == "group"
     assert bench.group_devices("", 1, 1) == [0]
     assert bench.group_devices("", 4, 1) == [0, 1, 2, 3]
     assert bench.group_devices("", 1, 8) == list(range(8))
+    assert bench.group_devices("", 8, 1) == list(range(8))
     assert bench.group_devices("0,0", 1, 1) == [0, 0]
     with pytest.raises(SystemExit):
         bench.group_devices("-1", 1, 1)
+    # fewer visible GPUs than asked for: exit non-zero, never wrap
+    bench.check_devices(list(range(8)), 8, False)
+    with pytest.raises(SystemExit):
+        bench.check_devices(list(range(8)), 1, False)
+    with pytest.raises(SystemExit):
+        bench.check_devices([0, 1], 1, True)
+    bench.check_devices([0, 0], 1, True)      # the explicit one-GPU rehearsal
+
+
+def test_bench_gpus8_without_launcher_parses_to_group(monkeypatch, capsys):
+    """`python bench.py --gpus 8` (the driver's BENCH command shape at N = 8,
+    no torch.distributed.run) reaches group_mode over devices 0..7."""
+    import importlib.util
+    import sys
+    spec = importlib.util.spec_from_file_location(
+        "bench_g8", os.path.join(os.path.dirname(os.path.dirname(__file__)), "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    seen = {}
+
+    def fake_group_mode(args, world, rank):
+        seen.update(world=world, rank=rank,
+                    devices=bench.group_devices(args.devices, args.gpus, world))
+    monkeypatch.setattr(bench, "group_mode", fake_group_mode)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "20", "--warmup", "5"])
+    bench.main()
+    assert seen == {"world": 1, "rank": 0, "devices": list(range(8))}

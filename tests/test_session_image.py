@@ -213,3 +213,24 @@ def test_host_image_equals_device_install(ta, engine):
         used = 1024 + (TABLES_USED if p.aead in (po.AES_128_GCM, po.AES_256_GCM) else 0)
         assert bytes(dev)[:used] == host[:used], (i, p.aead)
     table.close()
+
+
+def test_host_key_setup_is_aesni_pclmul():
+    """the host key schedule, H and the GHASH powers
+    are computed by AES-NI / PCLMUL instructions (as the reference's
+    aesni_set_encrypt_key and gcm_init_clmul, e_aes.c:1397-1402,
+    gcm128.c:709-715), and the host image code holds no key-indexed table: its
+    object file references no S-box or T-table symbol."""
+    import shutil
+    import subprocess
+    objdump = shutil.which("objdump") or "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    obj = os.path.join(ROOT, "talos_amd", "build", "session_host.cpp.o")
+    if not os.path.exists(obj):
+        pytest.skip("talos_amd/build/session_host.cpp.o not built")
+    # host code only: the x86-64 text of the object
+    dis = subprocess.run([objdump, "-d", "--no-show-raw-insn", obj], check=True,
+                         capture_output=True, text=True).stdout
+    for insn in ("aeskeygenassist", "aesenc", "aesenclast", "pclmul"):
+        assert insn in dis, insn
+    syms = subprocess.run([objdump, "-t", obj], check=True, capture_output=True, text=True).stdout
+    assert "Sbox" not in syms and "kTe" not in syms and "rem_4bit" not in syms
