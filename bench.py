@@ -8,7 +8,10 @@ One step = one tlsgpu_open_batch over the whole resident batch (64 Ki records,
 Inputs are synthetic (counter-SplitMix64 plaintexts, 1024 sessions x 64 records,
 1/1024 records tampered), sealed on the device beforehand by the validated
 sealer; the first step's outputs are verified before the warm-up steps (so the
-GPU is busy up to the timed region) and the last timed step's after it.
+GPU is busy up to the timed region) and the last timed step's after it.  Before
+the W warm-up steps an untimed settle (--settle-ms, default 100 ms of
+back-to-back steps) lets the GPU clock leave the dip a fresh sustained load
+causes, so the K timed steps measure the steady state.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config B|C|D]
                   [--sessions S] [--interleave] [--mode device|host|wire|copy]
@@ -228,6 +231,14 @@ def main():
     # (B: warm-up 3 / 10 / 30 / 60 / 100 -> 953 / 1,028 / 1,065 / 1,053 / 1,069
     # GiB/s; profiles/r05ag_bench_warm_start.txt); a warm-up is untimed
     ap.add_argument("--warmup", type=int, default=30)
+    # untimed settle before the W warm-up steps: back-to-back steps until the
+    # GPU's clock has left the dip a fresh sustained load causes (2.07 -> 1.61
+    # GHz, back to ~2.3 GHz after ~30 ms; profiles/r05ag_bench_warm_start.txt:
+    # W = 3 / 10 / 30 / 60 / 100 -> 953 / 1,028 / 1,065 / 1,053 / 1,069 GiB/s),
+    # so that K timed steps measure the steady state whatever W the caller picks
+    ap.add_argument("--settle-ms", type=float, default=100.0,
+                    help="untimed back-to-back steps for at least this long before the "
+                         "warm-up (0: none)")
     ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
     ap.add_argument("--records", type=int, default=0, help="override records per GPU")
     ap.add_argument("--sessions", type=int, default=0,
@@ -330,6 +341,7 @@ def main():
     step()
     eng.sync()
     wl.verify_open()
+    settled = settle(step, eng.sync, args.settle_ms)
     for _ in range(max(1, args.warmup)):
         step()
 
@@ -394,6 +406,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "settle": settled,
         "ms_per_step": round(elapsed_s * 1e3 / args.steps, 4),
         "wall_ms_per_step": round(wall_s * 1e3 / args.steps, 4),
         "higher_is_better": True,
@@ -440,6 +453,21 @@ def main():
     wl.free()
     cp.close()
     eng.close()
+
+
+def settle(step, sync, ms: float) -> dict:
+    """Untimed back-to-back steps for >= `ms` of wall time (synchronising every
+    8 steps to read the clock): the GPU's power governor leaves the clock dip
+    of a fresh sustained load before the warm-up and the timed region."""
+    if ms <= 0:
+        return {"ms": 0.0, "steps": 0}
+    n, t0 = 0, time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        for _ in range(8):
+            step()
+        n += 8
+        sync()
+    return {"ms": round((time.perf_counter() - t0) * 1e3, 1), "steps": n}
 
 
 def choose_split(split: str | None, world: int, devices: str, gpus: int = 1) -> str:
@@ -541,6 +569,7 @@ def group_mode(args, world, rank):
     for wl in wls:
         wl.verify_open()
     evs = [(ta.Event(m), ta.Event(m)) for m in members]
+    settled = settle(lambda: gs.batch(shard_arr, seal=False), g.sync, args.settle_ms)
     for _ in range(max(1, args.warmup)):
         gs.batch(shard_arr, seal=False)
     g.sync()
@@ -570,7 +599,7 @@ def group_mode(args, world, rank):
     traffic, traffic_src = load_traffic("B", kernel)
     line = {
         "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": n,
-        "steps": args.steps, "warmup": args.warmup,
+        "steps": args.steps, "warmup": args.warmup, "settle": settled,
         "ms_per_step": round(slowest_s * 1e3 / args.steps, 4),
         "wall_ms_per_step": round(wall_s * 1e3 / args.steps, 4),
         "wall_value": round(total_len * args.steps / wall_s / GIB, 3),

@@ -443,9 +443,13 @@ int tlsgpu_evp_call_stats(uint64_t *seal_calls, uint64_t *open_calls);
  * before the first EVP call.  With it on, EVP_AEAD_CTX_init launches nothing
  * (the session image is built on the host and installed by the context's
  * first call) and EVP_AEAD_CTX_cleanup scrubs the slot through the server.
- * tlsgpu_evp_doorbell_stats: jobs served and instances launched so far. */
+ * tlsgpu_evp_doorbell_stats: jobs served and instances launched so far.
+ * tlsgpu_evp_doorbell_scrub_stats (round 6): scrub jobs served, and times a
+ * server workgroup other than the scrubbing one zeroed its LDS copy of a
+ * scrubbed key (the scrub ring). */
 int tlsgpu_evp_set_doorbell(unsigned groups, unsigned lifetime_ms);
 int tlsgpu_evp_doorbell_stats(uint64_t *jobs, uint64_t *launches);
+int tlsgpu_evp_doorbell_scrub_stats(uint64_t *scrubs, uint64_t *flushes);
 /* tlsgpu_evp_doorbell_warm: launch a server instance now on every EVP device
  * whose queued instance would stop polling within half a lifetime (what the
  * next call would do), e.g. before a burst of calls.  No-op with the doorbell

@@ -159,6 +159,7 @@ def load_library(path: str = LIBPATH) -> C.CDLL:
         "tlsgpu_evp_context_slot": (i32, [vp, C.POINTER(C.c_void_p), C.POINTER(C.c_uint32)]),
         "tlsgpu_evp_set_doorbell": (i32, [C.c_uint, C.c_uint]),
         "tlsgpu_evp_doorbell_stats": (i32, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+        "tlsgpu_evp_doorbell_scrub_stats": (i32, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
         "tlsgpu_evp_doorbell_warm": (i32, []),
         "tlsgpu_evp_shutdown": (i32, []),
         "tlsgpu_sessions_debug_read": (i32, [vp, u32, vp, C.c_size_t]),
@@ -729,6 +730,14 @@ def evp_doorbell_stats() -> tuple[int, int]:
     _check(load_library().tlsgpu_evp_doorbell_stats(C.byref(j), C.byref(l)),
            "tlsgpu_evp_doorbell_stats")
     return j.value, l.value
+
+
+def evp_doorbell_scrub_stats() -> tuple[int, int]:
+    """(scrub jobs served, LDS flushes by the other server workgroups)."""
+    n, f = C.c_uint64(), C.c_uint64()
+    _check(load_library().tlsgpu_evp_doorbell_scrub_stats(C.byref(n), C.byref(f)),
+           "tlsgpu_evp_doorbell_scrub_stats")
+    return n.value, f.value
 
 
 def evp_batch_stats() -> tuple[int, int]:

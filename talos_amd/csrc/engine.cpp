@@ -1280,6 +1280,7 @@ static size_t evp_device_count() {
 static size_t evp_pick() { return g_evp_rr.fetch_add(1) % evp_device_count(); }
 
 struct EvpBatcher;
+constexpr int kImagePoisoned = 3;
 struct AeadState {
   tlsgpu_sessions* sess;  // the device table holding the context's session
   uint32_t slot;          // session id in sess
@@ -1294,7 +1295,8 @@ struct AeadState {
   // (session_host.cpp) in a pinned image buffer, installed by the context's
   // first call — posted with the doorbell job, or one upload kernel ahead of a
   // launched job — so EVP_AEAD_CTX_init launches nothing.  0: on the device
-  // (or no image), 1: image waiting, 2: a call is installing it
+  // (or no image), 1: image waiting, 2: a call is installing it,
+  // kImagePoisoned: an install job went unanswered (image and slot leaked)
   mutable std::atomic<int> image{0};
   uint8_t* img_h = nullptr;  // pinned image (host / device views)
   uint8_t* img_d = nullptr;
@@ -1493,18 +1495,67 @@ static std::once_flag g_call_streams_once[kMaxDev];
 static bool g_call_streams_ok[kMaxDev];
 static std::atomic<uint32_t> g_call_thread_seq{0};
 
+// Pinned staging chunks (round 6): a thread's
+// per-call staging is one kStageChunk of pinned host memory carved from
+// kStageSlab-byte slabs (one hipHostMalloc per 32 threads), enough for any TLS
+// record job ([RawJob | nonce | ad | 16 KiB + 2 KiB in | status | out] <=
+// 40 KiB); a thread that makes a larger EVP call grows to its own allocation.
+// Chunks go back to the free list without a HIP call (a thread's exit makes
+// none), so the pinned bytes are bounded by the peak number
+// of calling threads x 64 KiB.  No device buffer unless a path needs one (the
+// zero-copy per-call path, the default, reads and writes the pinned chunk).
+constexpr size_t kStageChunk = 64u << 10;
+constexpr size_t kStageSlab = 2u << 20;
+struct StageChunks {
+  std::mutex mu;
+  std::vector<std::pair<uint8_t*, uint8_t*>> free;  // (host, device view)
+  std::atomic<uint64_t> slabs{0};
+};
+static StageChunks g_stage_chunks[kMaxDev];
+static bool stage_chunk_take(int dev, uint8_t** h, uint8_t** d) {
+  StageChunks& c = g_stage_chunks[dev];
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (!c.free.empty()) {
+      *h = c.free.back().first;
+      *d = c.free.back().second;
+      c.free.pop_back();
+      return true;
+    }
+  }
+  uint8_t *hs = nullptr, *ds = nullptr;
+  if (hipHostMalloc((void**)&hs, kStageSlab, hipHostMallocDefault) != hipSuccess) return false;
+  if (hipHostGetDevicePointer((void**)&ds, hs, 0) != hipSuccess) ds = nullptr;
+  c.slabs.fetch_add(1, std::memory_order_relaxed);
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    for (size_t i = 1; i < kStageSlab / kStageChunk; i++)
+      c.free.emplace_back(hs + i * kStageChunk, ds ? ds + i * kStageChunk : nullptr);
+  }
+  *h = hs;
+  *d = ds;
+  return true;
+}
+static void stage_chunk_give(int dev, uint8_t* h, uint8_t* d) {
+  std::lock_guard<std::mutex> lk(g_stage_chunks[dev].mu);
+  g_stage_chunks[dev].free.emplace_back(h, d);
+}
+
 // One per (thread, device): buffers, stream and event belong to that device.
 struct Staging {
   int device = -1;
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
-  uint8_t* d_buf = nullptr;
+  uint8_t* d_buf = nullptr;  // device buffer (only the staged, non-zero-copy paths)
   uint8_t* h_buf = nullptr;
   uint8_t* h_dev = nullptr;  // h_buf as the device addresses it (zero-copy calls)
-  size_t cap = 0;
-  // pinned key areas (round 5): EVP_AEAD_CTX_init builds the slot's image here
+  size_t cap = 0;            // bytes of h_buf (kStageChunk: a pooled chunk)
+  size_t dcap = 0;           // bytes of d_buf
+  // key areas (round 5; round 6: buffers from the shared pinned image pool,
+  // not per thread): install_one builds the slot's image here
   // (session_host.cpp) and one kernel copies it into the slot; `dirty` until
-  // the copy is known done (its event), then zeroed (explicit_bzero analogue)
+  // the copy is known done (its event), then zeroed and given back to the pool
+  // (explicit_bzero analogue, image_give)
   struct KeyArea {
     uint8_t* h = nullptr;
     uint8_t* dev = nullptr;
@@ -1515,32 +1566,29 @@ struct Staging {
   static constexpr size_t kKeyAreaBytes = sizeof(DevSession) + sizeof(DevGcmTables);
   KeyArea keys[kKeyAreas];
   uint32_t key_next = 0;
+  void give_key_area(KeyArea& k) {
+    image_give(device, k.h, k.dev);  // zeroes it
+    k.h = k.dev = nullptr;
+    k.dirty = false;
+  }
   // the next key area (waiting for and zeroing its previous image if needed)
   KeyArea* take_key_area() {
     KeyArea& k = keys[key_next++ % kKeyAreas];
-    if (!k.h) {
-      if (hipHostMalloc((void**)&k.h, kKeyAreaBytes, hipHostMallocDefault) != hipSuccess ||
-          hipHostGetDevicePointer((void**)&k.dev, k.h, 0) != hipSuccess ||
-          hipEventCreateWithFlags(&k.ev, hipEventDisableTiming) != hipSuccess) {
-        if (k.h) (void)hipHostFree(k.h);
-        k.h = nullptr;
-        return nullptr;
-      }
+    if (!k.ev && hipEventCreateWithFlags(&k.ev, hipEventDisableTiming) != hipSuccess) {
+      k.ev = nullptr;
+      return nullptr;
     }
     if (k.dirty) {
       if (hipEventSynchronize(k.ev) != hipSuccess) return nullptr;
-      explicit_bzero(k.h, kKeyAreaBytes);
-      k.dirty = false;
+      give_key_area(k);
     }
+    if (!image_take(device, &k.h, &k.dev)) return nullptr;
     return &k;
   }
-  // zero every key area whose copy has finished (no wait)
+  // zero and give back every key area whose copy has finished (no wait)
   void sweep_key_areas() {
     for (KeyArea& k : keys)
-      if (k.dirty && hipEventQuery(k.ev) == hipSuccess) {
-        explicit_bzero(k.h, kKeyAreaBytes);
-        k.dirty = false;
-      }
+      if (k.dirty && hipEventQuery(k.ev) == hipSuccess) give_key_area(k);
   }
   bool any_dirty_key_area() const {
     for (const KeyArea& k : keys)
@@ -1550,16 +1598,23 @@ struct Staging {
   ~Staging() {
     if (device >= 0) (void)hipSetDevice(device);  // the buffers' and the event's device
     if (d_buf) (void)hipFree(d_buf);
-    if (h_buf) (void)hipHostFree(h_buf);
+    release_host();
     if (done) (void)hipEventDestroy(done);
+  }
+  void release_host() {
+    if (h_buf && cap == kStageChunk) stage_chunk_give(device, h_buf, h_dev);
+    else if (h_buf) (void)hipHostFree(h_buf);
+    h_buf = h_dev = nullptr;
+    cap = 0;
   }
   // A job that may still run on the device owns the buffers (a doorbell post
   // nobody answered): forget them without freeing, the next ensure allocates.
   void abandon() {
     d_buf = h_buf = h_dev = nullptr;
-    cap = 0;
+    cap = dcap = 0;
   }
-  bool ensure(int dev, size_t bytes) {
+  // `bytes` of pinned staging (and of device staging when `dev_buf`) on `dev`
+  bool ensure(int dev, size_t bytes, bool dev_buf = false) {
     if (dev < 0 || dev >= kMaxDev || hipSetDevice(dev) != hipSuccess) return false;
     if (!stream) {
       std::call_once(g_call_streams_once[dev], [dev] {
@@ -1574,16 +1629,32 @@ struct Staging {
       stream = g_call_streams[dev][g_call_thread_seq.fetch_add(1) % kCallStreams];
     }
     device = dev;
-    if (cap >= bytes) return true;
-    if (d_buf) (void)hipFree(d_buf);
-    if (h_buf) (void)hipHostFree(h_buf);
-    d_buf = h_buf = nullptr;
-    cap = 0;
-    size_t want = bytes < (1u << 20) ? (1u << 20) : bytes;
-    if (hipMalloc(&d_buf, want) != hipSuccess) return false;
-    if (hipHostMalloc((void**)&h_buf, want, hipHostMallocDefault) != hipSuccess) return false;
-    if (hipHostGetDevicePointer((void**)&h_dev, h_buf, 0) != hipSuccess) h_dev = nullptr;
-    cap = want;
+    if (cap < bytes) {
+      release_host();  // this thread's calls are synchronous: nothing in flight
+      if (bytes <= kStageChunk) {
+        if (!stage_chunk_take(dev, &h_buf, &h_dev)) return false;
+        cap = kStageChunk;
+      } else {
+        const size_t want = (bytes + kStageChunk - 1) & ~(kStageChunk - 1);
+        if (hipHostMalloc((void**)&h_buf, want, hipHostMallocDefault) != hipSuccess) {
+          h_buf = nullptr;
+          return false;
+        }
+        if (hipHostGetDevicePointer((void**)&h_dev, h_buf, 0) != hipSuccess) h_dev = nullptr;
+        cap = want;
+      }
+    }
+    if (dev_buf && dcap < bytes) {
+      if (d_buf) (void)hipFree(d_buf);
+      d_buf = nullptr;
+      dcap = 0;
+      const size_t want = (bytes + kStageChunk - 1) & ~(kStageChunk - 1);
+      if (hipMalloc(&d_buf, want) != hipSuccess) {
+        d_buf = nullptr;
+        return false;
+      }
+      dcap = want;
+    }
     return true;
   }
 };
@@ -1619,6 +1690,9 @@ static Staging* stage_for(int dev) {
       g_stage_pool[dev].pop_back();
     }
   }
+  // an exited thread's installs may have left images in its key areas
+  // (ADVICE r05): zero the ones whose copies are done before reuse
+  if (st && st->any_dirty_key_area()) st->sweep_key_areas();
   if (!st) st = new (std::nothrow) Staging();
   return st;
 }
@@ -1810,7 +1884,17 @@ extern "C" void EVP_AEAD_CTX_cleanup(EVP_AEAD_CTX* ctx) {
   if (ctx->aead == nullptr) return;
   auto* st = (AeadState*)ctx->aead_state;
   if (st) {
-    if (st->image.load(std::memory_order_acquire) == 1) {
+    const int img = st->image.load(std::memory_order_acquire);
+    if (img == kImagePoisoned) {
+      // an install job that never answered may still copy the image into the
+      // slot: leak both (never reused, as stg->abandon() leaks staging) —
+      // no scrub either, its synchronous fallback would wait on that device
+      delete st;
+      ctx->aead_state = nullptr;
+      ctx->aead = nullptr;
+      return;
+    }
+    if (img == 1) {
       // deferred and never called: no key material reached the device
       image_give(st->sess->eng->device, st->img_h, st->img_d);
     } else if (!doorbell_scrub(st)) {
@@ -1942,6 +2026,7 @@ struct EvpServer {
   // TLSGPU_EVP_DOORBELL_TRACE=1: per-slot device timestamps (pinned) and their
   // sums, printed at exit: pick -> slot loaded -> job done -> released (ticks
   // of 10 ns), and the caller's post -> done-seen wall time (ns)
+  uint64_t* d_scrubs = nullptr;  // HBM: the scrub ring (ServerArgs::scrubs)
   uint64_t* trace = nullptr;
   uint64_t* d_trace = nullptr;
   std::atomic<uint64_t> tr_n{0}, tr_load{0}, tr_job{0}, tr_rel{0}, tr_host_ns{0};
@@ -1992,6 +2077,12 @@ static const uint64_t g_doorbell_yield_ns = [] {
 
 // Test hook (tests/test_evp_doorbell.py): sleep this long between a call's
 // server_ensure and its post, as a caller descheduled there would.
+// Test hook (TLSGPU_TEST_FAIL_INSTALLS=k): the first k calls that claim a
+// deferred install fail before posting it (waiters must re-claim).
+static std::atomic<int> g_test_fail_installs{[] {
+  const char* v = getenv("TLSGPU_TEST_FAIL_INSTALLS");
+  return v ? atoi(v) : 0;
+}()};
 static const unsigned g_test_post_delay_us = [] {
   const char* v = getenv("TLSGPU_TEST_DOORBELL_POST_DELAY_US");
   return v && *v ? (unsigned)strtoul(v, nullptr, 10) : 0u;
@@ -2105,13 +2196,29 @@ static volatile sig_atomic_t g_exit_phase = 0;
 // TLSGPU_CRASH_TRACE=1: a fatal signal prints the exit phase and a native
 // backtrace before the default action (Python's faulthandler, when enabled
 // after the library loaded, chains to this handler after its own dump).
+// Async-signal-safe: fixed strings and a hand-rolled integer
+// formatter through write(2); backtrace() was called once at install, so the
+// unwinder (libgcc) is loaded before any fault and the handler does not
+// dlopen or malloc.
+static void write_str(const char* p) { (void)!write(2, p, strlen(p)); }
+static void write_int(long v) {
+  char d[24];
+  int i = (int)sizeof d;
+  const bool neg = v < 0;
+  unsigned long u = neg ? 0ul - (unsigned long)v : (unsigned long)v;
+  do {
+    d[--i] = (char)('0' + u % 10);
+    u /= 10;
+  } while (u && i > 1);
+  if (neg) d[--i] = '-';
+  (void)!write(2, d + i, sizeof d - (size_t)i);
+}
 static void crash_report(int sig) {
-  char buf[192];
-  const int n = snprintf(buf, sizeof buf,
-                         "tlsgpu: fatal signal %d in exit phase %d (0 running, 1 main-thread exit "
-                         "guard, 2 atexit, 3 library destructor)\n",
-                         sig, (int)g_exit_phase);
-  if (n > 0) (void)!write(2, buf, (size_t)n);
+  write_str("tlsgpu: fatal signal ");
+  write_int(sig);
+  write_str(" in exit phase ");
+  write_int((long)g_exit_phase);
+  write_str(" (0 running, 1 main-thread exit guard, 2 atexit, 3 library destructor)\n");
   void* fr[64];
   backtrace_symbols_fd(fr, backtrace(fr, 64), 2);
   signal(sig, SIG_DFL);
@@ -2120,6 +2227,8 @@ static void crash_report(int sig) {
 __attribute__((constructor)) static void install_crash_report() {
   const char* v = getenv("TLSGPU_CRASH_TRACE");
   if (!v || !*v || *v == '0') return;
+  void* warm[2];
+  (void)backtrace(warm, 2);  // loads the unwinder now, not inside the handler
   struct sigaction sa;
   memset(&sa, 0, sizeof sa);
   sa.sa_handler = crash_report;
@@ -2220,7 +2329,9 @@ static EvpServer* evp_server(size_t k, tlsgpu_engine* e) {
   if (hipHostMalloc((void**)&stop, 4096, hipHostMallocDefault) != hipSuccess ||
       hipHostGetDevicePointer((void**)&sv->d_slots, h, 0) != hipSuccess ||
       hipHostGetDevicePointer((void**)&sv->d_stop, stop, 0) != hipSuccess ||
-      hipStreamCreateWithFlags(&sv->stream, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&sv->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc((void**)&sv->d_scrubs, 8 * (kScrubRing + 2)) != hipSuccess ||
+      hipMemset(sv->d_scrubs, 0, 8 * (kScrubRing + 2)) != hipSuccess) {
     (void)hipHostFree(h);
     if (stop) (void)hipHostFree(stop);
     return nullptr;
@@ -2267,6 +2378,7 @@ static bool server_ensure(EvpServer* sv) {
   a.stop = sv->d_stop;
   a.lifetime = sv->lifetime_ns / 10;  // 100 MHz realtime ticks
   a.trace = reinterpret_cast<unsigned long long*>(sv->d_trace);
+  a.scrubs = reinterpret_cast<unsigned long long*>(sv->d_scrubs);
   a.exited = sv->d_stop + kExitedWord;
   a.seq = sv->launch_seq + 1;
   const uint32_t cover = (hi + kWave - 1) / kWave;
@@ -2363,6 +2475,23 @@ extern "C" int tlsgpu_evp_doorbell_stats(uint64_t* jobs, uint64_t* launches) {
   return TLSGPU_OK;
 }
 
+extern "C" int tlsgpu_evp_doorbell_scrub_stats(uint64_t* scrubs, uint64_t* flushes) {
+  uint64_t n = 0, f = 0;
+  for (EvpServer* sv : g_servers)
+    if (sv && sv->d_scrubs) {
+      uint64_t w[2] = {0, 0};
+      if (hipSetDevice(sv->device) != hipSuccess ||
+          hipMemcpy(&w[0], sv->d_scrubs, 8, hipMemcpyDeviceToHost) != hipSuccess ||
+          hipMemcpy(&w[1], sv->d_scrubs + 1 + kScrubRing, 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(TLSGPU_EHIP, "scrub stats");
+      n += w[0];
+      f += w[1];
+    }
+  if (scrubs) *scrubs = n;
+  if (flushes) *flushes = f;
+  return TLSGPU_OK;
+}
+
 // One EVP call on the GPU: 1 = success, 0 = authentication failure / rejected
 // by the kernel (output zero-filled), -1 = runtime failure.
 static int gpu_call(const AeadState* st, bool seal, unsigned char* out, size_t* out_len,
@@ -2407,8 +2536,9 @@ static bool event_spin(hipEvent_t ev) {
 
 // Post the job written into `slot` (the caller's doorbell slot on server sv,
 // EVP device k) and wait for its answer.  1: served; 0: not served and never
-// will be (shutdown) — take the launched path; -1: failure (launch failed, or
-// no answer in 10 s: the slot is then retired and the staging abandoned).
+// will be (shutdown) — take the launched path; -1: failure, nothing posted
+// (launch failed); -2: posted but no answer in 10 s (the job may still run:
+// the slot is retired and the staging abandoned).
 static int doorbell_post_wait(EvpServer* sv, DoorbellSlot* slot, uint32_t* seq, size_t k,
                               Staging* stg, uint64_t* t0_out) {
   if (!server_ensure(sv)) {
@@ -2441,7 +2571,7 @@ static int doorbell_post_wait(EvpServer* sv, DoorbellSlot* slot, uint32_t* seq, 
         // (never freed, never reused)
         t_slots.slot[k] = -1;
         stg->abandon();
-        return -1;
+        return -2;
       }
       if (waited > g_doorbell_yield_ns) sched_yield();  // let other callers post
     }
@@ -2459,8 +2589,10 @@ static bool deferred_install_ok(int kind) {
 }
 
 // EVP_AEAD_CTX_cleanup through the doorbell (round 5): a scrub job zeroes the
-// slot on the device and the server's LDS copies of this key, synchronously —
-// no launch.  false: no server / slot for this thread (the caller scrubs on a
+// slot on the device and the serving workgroup's LDS copies of this key,
+// synchronously — no launch; the other server workgroups zero theirs when
+// they next look at the scrub ring (round 6, evp_server.hip: before their
+// next job, or within 16 idle polls).  false: no server / slot for this thread (the caller scrubs on a
 // stream instead).
 static bool doorbell_scrub(const AeadState* st) {
   if (st->batcher || !g_evp_zerocopy || !doorbell_enabled() ||
@@ -2504,12 +2636,18 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
   }
   // a deferred install (EVP_AEAD_CTX_init, round 5): one caller installs the
   // image with its call, concurrent first callers wait for it; a failed call
-  // leaves the image waiting for the next one
+  // leaves the image waiting (1) for the next caller — a waiter that sees it
+  // back at 1 claims it itself.  Once the image's address has
+  // reached the device (a posted doorbell job, a queued upload) a failure
+  // poisons the context instead (3, kImagePoisoned): the job may still run, so
+  // the image buffer and the slot are never handed to anyone else, and every
+  // later call fails (a doorbell timeout).
   struct InstallClaim {
     const AeadState* st;
     bool active = false;
+    bool posted = false;  // the device may read the image from now on
     ~InstallClaim() {
-      if (active) st->image.store(1, std::memory_order_release);
+      if (active) st->image.store(posted ? kImagePoisoned : 1, std::memory_order_release);
     }
     void done() {  // on the device: the image buffer goes back, zeroed
       active = false;
@@ -2518,18 +2656,27 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
     }
   } claim{st};
   if (st->image.load(std::memory_order_acquire) != 0) {
-    int expect = 1;
-    if (st->image.compare_exchange_strong(expect, 2, std::memory_order_acq_rel)) {
-      claim.active = true;
-      // the slot's previous owner's scrub, if it went through a stream
-      if (hipEventQuery(st->slot_ev) != hipSuccess && hipEventSynchronize(st->slot_ev) != hipSuccess)
-        return -1;
-    } else {
-      for (uint64_t spins = 1; st->image.load(std::memory_order_acquire) != 0; spins++) {
-        __builtin_ia32_pause();
-        if ((spins & 255) == 0) sched_yield();
-        if (spins > (1ull << 34)) return -1;
+    for (uint64_t spins = 1;; spins++) {
+      int expect = 1;
+      if (st->image.compare_exchange_strong(expect, 2, std::memory_order_acq_rel)) {
+        claim.active = true;
+        // the slot's previous owner's scrub, if it went through a stream
+        if (hipEventQuery(st->slot_ev) != hipSuccess &&
+            hipEventSynchronize(st->slot_ev) != hipSuccess)
+          return -1;
+        if (g_test_fail_installs.load(std::memory_order_relaxed) > 0 &&
+            g_test_fail_installs.fetch_sub(1) > 0) {  // test hook: the claimer fails
+          usleep(20000);  // with the other first callers waiting on it
+          return -1;
+        }
+        break;
       }
+      if (expect == 0) break;               // installed by the caller that claimed it
+      if (expect == kImagePoisoned) return -1;
+      // 2: another caller is installing right now
+      __builtin_ia32_pause();
+      if ((spins & 255) == 0) sched_yield();
+      if (spins > (1ull << 34)) return -1;
     }
   }
   auto al = [](size_t v) { return (v + 15) & ~(size_t)15; };
@@ -2544,6 +2691,7 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
   // status and output to the pinned staging buffer itself — no H2D / D2H
   // launches around a one-record batch; TLSGPU_EVP_ZEROCOPY=0 stages through HBM
   const bool zc = g_evp_zerocopy && stg->h_dev;
+  if (!zc && !stg->ensure(e->device, total, true)) return -1;
   uint8_t* d = zc ? stg->h_dev : stg->d_buf;
   uint8_t* h = stg->h_buf;
   hipStream_t s = stg->stream;
@@ -2606,6 +2754,7 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
       slot->key_id = st->key_id;
       uint64_t t0 = 0;
       const int pr = doorbell_post_wait(sv, slot, seq, st->evp_dev, stg, &t0);
+      if (pr == -2) claim.posted = true;  // unanswered: the job may still copy the image
       if (pr < 0) return -1;
       if (pr == 0) goto launched;
       if (claim.active) claim.done();
@@ -2650,11 +2799,13 @@ launched:
   a.status = reinterpret_cast<int32_t*>(d + o_status);
   a.n_sessions = st->sess->capacity;
   // a deferred install on the launched path: one upload kernel ahead of the job
-  if (claim.active && (hipStreamWaitEvent(s, st->slot_ev, 0) != hipSuccess ||
-                       launch_upload_session(st->img_d, st->sess->d_sess + st->slot,
-                                             st->sess->d_gcm + st->slot,
-                                             st->img_tables ? kGcmTableUploadBytes : 0u, s) != 0))
-    return -1;
+  if (claim.active) {
+    if (hipStreamWaitEvent(s, st->slot_ev, 0) != hipSuccess) return -1;
+    claim.posted = true;  // queued from here on, whatever fails after it
+    if (launch_upload_session(st->img_d, st->sess->d_sess + st->slot, st->sess->d_gcm + st->slot,
+                              st->img_tables ? kGcmTableUploadBytes : 0u, s) != 0)
+      return -1;
+  }
   int rc = gcm ? launch_gcm(a, seal, true, st->kind == TLSGPU_AES_128_GCM ? 10 : 14, 1, s)
                : launch_chacha(a, seal, true, true, true, s);
   if (rc) return -1;
@@ -2820,7 +2971,7 @@ int run_program(GpuGcm* g, const Step* steps, int nsteps) {
     total += al(steps[i].out ? steps[i].len : 0);
   }
   Staging* stg = stage_for(e->device);
-  if (!stg || !stg->ensure(e->device, total)) return -100;
+  if (!stg || !stg->ensure(e->device, total, true)) return -100;
   uint8_t* b = stg->d_buf;
   hipStream_t s = stg->stream;
   std::vector<GcmStreamOp> ops(nsteps);

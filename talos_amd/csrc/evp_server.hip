@@ -70,6 +70,7 @@ __device__ __forceinline__ const uint8_t* tg_stage_src() { return s_lds + SRV_ST
 namespace tg {
 
 constexpr uint32_t kSrvExit = 0xFFFFFFFFu;
+constexpr uint32_t kSrvFlush = 0xFFFFFFFEu;  // zero this workgroup's key copies (a scrub elsewhere)
 // DoorbellSlot::op beyond bit 0 (seal), bits 8-15 (10 / 14 AES rounds, 20
 // ChaCha) and bit 16 (inline nonce / AAD) — engine.cpp writes the same bits
 constexpr uint32_t kOpInstall = kDoorbellOpInstall;            // the image at inl[0..7] first
@@ -168,10 +169,38 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
   uint32_t cached_key = 0;  // key id whose GCM tables are in LDS (0: none)
   uint32_t sess_key = 0;    // wave 0: key id whose DevSession is at SRV_SESS_OFF
   unsigned long long t_pick = 0, t_loaded = 0;  // trace (wave 0)
+  // Scrubs served by other workgroups (round 6): each scrub job
+  // appends its key id to a ring in HBM; wave 0 reads the new entries before
+  // each pick and every 16 polls, and when one names a key whose tables or
+  // DevSession this workgroup holds in LDS, the workgroup zeroes them
+  // (kSrvFlush).  A ring lapped since the last look flushes whatever is held.
+  unsigned long long scrub_seen =
+      __hip_atomic_load(s.scrubs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  auto scrubbed_here = [&]() -> bool {  // wave 0, wave-uniform
+    const unsigned long long top =
+        __hip_atomic_load(s.scrubs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool hit = false;
+    while (scrub_seen < top) {
+      const unsigned long long e = __hip_atomic_load(s.scrubs + 1 + scrub_seen % kScrubRing,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long tag = e >> 32;
+      if (tag == (scrub_seen + 1) % (1ull << 32)) {
+        const uint32_t key = (uint32_t)e;
+        hit = hit || (key != 0 && (key == cached_key || key == sess_key));
+        scrub_seen++;
+      } else if (tag > (scrub_seen + 1) % (1ull << 32)) {  // lapped: flush what is held
+        hit = hit || cached_key != 0 || sess_key != 0;
+        scrub_seen = top;
+      } else {
+        break;  // the entry is still being written: look again next time
+      }
+    }
+    return hit;
+  };
   for (;;) {
     if (wave == 0) {
-      uint32_t pick = kSrvExit;
-      for (uint32_t polls = 0;; polls++) {
+      uint32_t pick = scrubbed_here() ? kSrvFlush : kSrvExit;
+      for (uint32_t polls = 0; pick == kSrvExit; polls++) {
         // the lifetime first, busy or not: a workgroup that kept serving past
         // it would hold the next instance (queued on the same stream) off the
         // GPU, and with it the slots of workgroups that had already exited
@@ -183,12 +212,20 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
           t_pick = __builtin_amdgcn_s_memrealtime();
           break;
         }
-        // the stop word every 16 polls (each poll is a PCIe read)
-        if ((polls & 15) == 15 && sys_load(s.stop) != 0) break;
+        // the stop word every 16 polls (each poll is a PCIe read), and the
+        // scrub ring (HBM)
+        if ((polls & 15) == 15) {
+          if (sys_load(s.stop) != 0) break;
+          if (scrubbed_here()) {
+            pick = kSrvFlush;
+            break;
+          }
+        }
         __builtin_amdgcn_s_sleep(1);
       }
       if (lane == 0) *sel = pick;
-      if (pick != kSrvExit) {
+      if (pick == kSrvFlush) sess_key = 0;  // zeroed below by every wave
+      if (pick != kSrvExit && pick != kSrvFlush) {
         // the whole slot in one wave load (the job, its nonce and AAD: no
         // further PCIe round trip for them) into LDS; inline nonce / AAD are
         // then addressed in that copy
@@ -231,6 +268,20 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
     __syncthreads();
     const uint32_t k = __builtin_amdgcn_readfirstlane(*sel);
     if (k == kSrvExit) break;
+    if (k == kSrvFlush) {  // the key copies a scrub on another workgroup named
+      const uint4 z = make_uint4(0, 0, 0, 0);
+      for (uint32_t i = threadIdx.x; i < (R4_OFF - KT_OFF) / 16; i += kThreads)
+        if (KT_OFF + 16 * i < AES_OFF || KT_OFF + 16 * i >= SH_OFF)
+          reinterpret_cast<uint4*>(s_lds + KT_OFF)[i] = z;
+      if (threadIdx.x < sizeof(DevSession) / 16)
+        reinterpret_cast<uint4*>(s_lds + SRV_SESS_OFF)[threadIdx.x] = z;
+      cached_key = 0;
+      if (threadIdx.x == 0)
+        __hip_atomic_fetch_add(s.scrubs + 1 + kScrubRing, 1ull, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      continue;
+    }
     DoorbellSlot* sl = s.slots + k;
     const DoorbellSlot* c = reinterpret_cast<const DoorbellSlot*>(s_lds + SRV_SLOT_OFF);
     const uint32_t post = __builtin_amdgcn_readfirstlane(c->post);
@@ -296,7 +347,16 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
       }
       if (threadIdx.x < kS) reinterpret_cast<uint4*>(s_lds + SRV_SESS_OFF)[threadIdx.x] = z;
       __syncthreads();
-      if (threadIdx.x == 0) a.status[0] = 0;
+      if (threadIdx.x == 0) {
+        a.status[0] = 0;
+        if (key != 0) {  // the other workgroups' copies: the scrub ring
+          const unsigned long long idx = __hip_atomic_fetch_add(
+              s.scrubs, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(s.scrubs + 1 + idx % kScrubRing,
+                             (((idx + 1) % (1ull << 32)) << 32) | key, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
     }
     const bool hit = key != 0 && key == cached_key;
     // the table cache is keyed only on a job that really loaded (or kept)

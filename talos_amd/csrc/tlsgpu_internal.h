@@ -339,7 +339,10 @@ struct ServerArgs {
   unsigned long long* trace;    // null, or pinned [nslots][kTraceWords]: realtime at pick,
                                 // slot loaded, GCM job marks 0..6, job done, answer
                                 // released (TLSGPU_EVP_DOORBELL_TRACE)
+  unsigned long long* scrubs;   // HBM [1 + kScrubRing + 1]: scrub count, the ring of
+                                // scrubbed key ids ((index + 1) << 32 | key), flushes done
 };
+constexpr uint32_t kScrubRing = 256;
 constexpr int kTraceWords = 16;  // + the last working wave's marks 7, 8 at [11], [12]
 int launch_evp_server(const ServerArgs& a, int groups, hipStream_t s);
 int launch_session_install_arg(DevSession* sessions, DevGcmTables* tables,

@@ -325,6 +325,24 @@ hipError_t hipMemsetD32Async(hipDeviceptr_t p, int v, size_t n, hipStream_t s) {
 }
 
 // the audit's own entry points (tests/test_device_affinity.py)
+// live bytes of pinned host memory and of device memory (all devices), and
+// the number of live pinned allocations
+void devstub_mem(uint64_t* pinned, uint64_t* device, uint64_t* pinned_allocs) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  uint64_t p = 0, d = 0, np = 0;
+  for (const auto& kv : g_allocs) {
+    if (kv.second.pinned) {
+      p += kv.second.size;
+      np++;
+    } else {
+      d += kv.second.size;
+    }
+  }
+  if (pinned) *pinned = p;
+  if (device) *device = d;
+  if (pinned_allocs) *pinned_allocs = np;
+}
+
 int devstub_report(char* buf, size_t n, uint64_t* checked, uint64_t* pinned_cross) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (pinned_cross) *pinned_cross = g_pinned_cross;

@@ -127,3 +127,49 @@ def test_deferred_install_and_doorbell_scrub(groups, threads):
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
     jobs = int(r.stdout.split()[-2])
     assert jobs > 0, r.stdout
+
+
+_CHILD_FAIL = r"""
+import os, random, sys, threading, time
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, os.path.join(sys.argv[1], "oracle"))
+import talos_amd as ta, pyoracle as po
+orc = po.Oracle()
+res, errors = [], []
+for kind in (po.AES_128_GCM, po.CHACHA20_POLY1305):
+    key = bytes(range(9, 9 + po.KEY_LEN[kind]))
+    ctx, octx = ta.EvpAead(kind, key), orc.aead(kind, key)
+    bar = threading.Barrier(8)
+    def first(t):
+        try:
+            rnd = random.Random(t)
+            nonce, pt, ad = rnd.randbytes(12), rnd.randbytes(1400), rnd.randbytes(13)
+            bar.wait()
+            ok, got, _ = ctx.seal(nonce, pt, ad)
+            if ok:
+                assert (1, got) == orc.seal(octx, nonce, pt, ad)[:2], kind
+            res.append(ok)
+        except Exception as exc:
+            errors.append(repr(exc))
+    t0 = time.time()
+    ths = [threading.Thread(target=first, args=(t,)) for t in range(8)]
+    [t.start() for t in ths]; [t.join() for t in ths]
+    print("kind", kind, "calls", len(res), "ok", sum(res), "s", round(time.time() - t0, 2))
+    ctx.cleanup()
+assert not errors, errors[:2]
+print("OK", sum(res), len(res))
+"""
+
+
+def test_failed_install_claim_is_retaken_by_waiters():
+    """the call that claims a context's deferred install
+    fails (test hook TLSGPU_TEST_FAIL_INSTALLS=1: the first claim only) while
+    seven other first callers wait on it.  The waiters must take the install
+    over at once — not spin until their 2^34-iteration cap — and every call
+    but the failed one must return the oracle's bytes."""
+    env = dict(os.environ, TLSGPU_EVP_DOORBELL="64", TLSGPU_TEST_FAIL_INSTALLS="1")
+    env.pop("TLSGPU_EVP_BATCH_US", None)
+    r = subprocess.run([sys.executable, "-c", _CHILD_FAIL, ROOT], env=env,
+                       capture_output=True, text=True, timeout=90)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
+    ok, calls = map(int, r.stdout.split()[-2:])
+    assert calls == 16 and ok == 15, r.stdout       # exactly the one forced failure

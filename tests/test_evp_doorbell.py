@@ -123,3 +123,60 @@ def test_evp_doorbell_busy_workgroup_yields_to_next_instance():
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
     worst = float(r.stdout.split()[-1])
     assert worst < 0.5, f"a call waited {worst:.3f} s behind a busy workgroup"
+
+
+_CHILD_SCRUB = r"""
+import os, random, sys, threading, time
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, os.path.join(sys.argv[1], "oracle"))
+import talos_amd as ta, pyoracle as po
+ta.load_library()
+orc = po.Oracle()
+N = 8
+errors, ctxs = [], [None] * N
+b1, b2 = threading.Barrier(N), threading.Barrier(N)
+def worker(t):
+    rnd = random.Random(900 + t)
+    try:
+        for rnd_i in range(6):
+            kind = [po.AES_128_GCM, po.AES_256_GCM][(t + rnd_i) % 2]
+            key = rnd.randbytes(po.KEY_LEN[kind])
+            ctx, octx = ta.EvpAead(kind, key), orc.aead(kind, key)
+            t_end = time.time() + 0.05   # past a few 20-ms server lifetimes: one workgroup per slot
+            while True:
+                nonce, pt, ad = rnd.randbytes(12), rnd.randbytes(1400), rnd.randbytes(13)
+                ok, got, _ = ctx.seal(nonce, pt, ad)
+                assert (ok, got) == tuple(orc.seal(octx, nonce, pt, ad)[:2]), (t, rnd_i)
+                if time.time() > t_end:
+                    break
+            ctxs[t] = ctx
+            b1.wait()
+            ctxs[(t + 1) % N].cleanup()   # scrub a context another thread's workgroup cached
+            b2.wait()
+    except Exception as exc:
+        errors.append(repr(exc))
+        b1.abort(); b2.abort()
+ths = [threading.Thread(target=worker, args=(t,)) for t in range(N)]
+[t.start() for t in ths]; [t.join() for t in ths]
+assert not errors, errors[:2]
+time.sleep(0.1)                # idle workgroups look at the ring every 16 polls
+scrubs, flushes = ta.evp_doorbell_scrub_stats()
+print("SCRUBS", scrubs, "FLUSHES", flushes)
+"""
+
+
+def test_scrub_reaches_other_server_workgroups():
+    """EVP_AEAD_CTX_cleanup's scrub job zeroes the serving
+    workgroup's LDS copies of the key; the other server workgroups that cached
+    the same key's tables zero theirs through the scrub ring (evp_server.hip,
+    kSrvFlush).  Eight threads each use a context on their own doorbell slot
+    (one workgroup each, once an instance is launched for 8 callers), then
+    each cleans up its neighbour's context: at least one of those scrubs runs
+    on a workgroup other than the one holding the key, and that one flushes."""
+    env = dict(os.environ, TLSGPU_EVP_DOORBELL="64", TLSGPU_EVP_DOORBELL_MS="20")
+    env.pop("TLSGPU_EVP_BATCH_US", None)
+    r = subprocess.run([sys.executable, "-c", _CHILD_SCRUB, ROOT], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "SCRUBS" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
+    w = r.stdout.split()
+    scrubs, flushes = int(w[w.index("SCRUBS") + 1]), int(w[w.index("FLUSHES") + 1])
+    assert scrubs >= 6 * 8 and flushes >= 1, r.stdout
