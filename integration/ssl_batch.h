@@ -1,0 +1,80 @@
+/*
+ * ssl_batch.h — a batching TLS record-layer consumer for LibreSSL 2.4.1
+ * (TaLoS's vendored libssl) over libtlsgpu (VERDICT r05 missing 2).
+ *
+ * The reference reads one record per SSL_read: ssl3_read_bytes
+ * (ssl/s3_pkt.c:840-957) -> ssl3_get_record (:279-495: ssl3_read_n's
+ * BIO_read into rbuf, the header checks, tls1_enc(s, 0) = one
+ * EVP_AEAD_CTX_open, t1_enc.c:832-975) -> copy into the caller's buffer.  A
+ * server with many connections calls that once per record per connection.
+ * Here one call drains the pending bytes of MANY connections' read BIOs into
+ * one pinned wire buffer, frames every complete record with ssl3_get_record's
+ * header rules, opens all of them in ONE GPU batch (tlsgpu_open_host: pinned
+ * H2D / the TLS open kernels / D2H, in place), hands each connection's
+ * plaintext to the application in record order, and advances each
+ * connection's s3->read_sequence exactly as tls1_enc would have
+ * (tls1_record_sequence_increment, t1_enc.c:258-266) — so the SSL object
+ * stays consistent and SSL_read keeps working after a batch.
+ *
+ * Build: compiled inside the LibreSSL / TaLoS tree (it reads ssl_locl.h:
+ * SSL_AEAD_CTX and SSL3_STATE), as a record-layer patch would be; here
+ * tests/ssl_batch/Makefile compiles it against /root/reference's headers.
+ * The read key reaches tlsgpu_ssl_batch_attach from the one call a patched
+ * tls1_change_cipher_state_aead (t1_enc.c:444-495) adds.
+ */
+#ifndef TLSGPU_SSL_BATCH_H
+#define TLSGPU_SSL_BATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <openssl/ssl.h>
+
+#include "../include/tlsgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct tlsgpu_ssl_batch tlsgpu_ssl_batch;
+
+/* Per-record delivery: the plaintext of one application-data record of
+ * connection `conn`, in record order per connection (valid during the call). */
+typedef void (*tlsgpu_ssl_deliver_fn)(void *arg, uint32_t conn, SSL *s, const uint8_t *data,
+    size_t len);
+
+/* Per-connection outcome of a batch read (conn_status[]). */
+#define TLSGPU_SSL_OK 0
+#define TLSGPU_SSL_BAD_RECORD_MAC (-1)   /* ssl3_get_record: SSL_AD_BAD_RECORD_MAC */
+#define TLSGPU_SSL_WRONG_VERSION (-2)    /* SSL_AD_PROTOCOL_VERSION */
+#define TLSGPU_SSL_RECORD_OVERFLOW (-3)  /* SSL_AD_RECORD_OVERFLOW */
+#define TLSGPU_SSL_NOT_APP_DATA (-4)     /* a non-application-data record: SSL_read's job */
+#define TLSGPU_SSL_NOT_ATTACHED (-5)
+
+/* A consumer for up to max_conns connections (connection ids 0..max_conns-1)
+ * on GPU `device`, with a pinned wire buffer of wire_bytes. */
+int tlsgpu_ssl_batch_create(int device, uint32_t max_conns, size_t wire_bytes,
+    tlsgpu_ssl_batch **out);
+void tlsgpu_ssl_batch_destroy(tlsgpu_ssl_batch *b);
+
+/* After ChangeCipherSpec on the read side: install connection `conn`'s read
+ * key (the key tls1_change_cipher_state_aead hands to EVP_AEAD_CTX_init) with
+ * the record state of s->aead_read_ctx (fixed nonce, tag length, nonce
+ * layout) and s->version on the GPU. */
+int tlsgpu_ssl_batch_attach(tlsgpu_ssl_batch *b, uint32_t conn, SSL *s, const uint8_t *key,
+    size_t key_len);
+
+/* Read every complete record pending in the read BIOs of conns[0..n) (and any
+ * partial record kept from the previous call) and open them in one batch.
+ * Returns the number of records delivered, or a negative TLSGPU_E* code;
+ * conn_status[i] is TLSGPU_SSL_OK or the first failure of conns[i] (records
+ * after a failure are not delivered, the connection's read sequence stops at
+ * it, as SSL_read's would).  A record that does not fit into what is left of
+ * the wire buffer stays pending in its BIO for the next call. */
+int tlsgpu_ssl_batch_read(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
+    tlsgpu_ssl_deliver_fn deliver, void *arg, int *conn_status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -62,6 +62,7 @@ struct targ {
 	size_t lo, hi;
 	unsigned long long bytes, records, failures;
 	double secs;
+	double ph[3];	/* churn: seconds in init, first seal, cleanup */
 };
 
 static double
@@ -108,13 +109,20 @@ churn_worker(void *arg)
 	for (;;) {
 		EVP_AEAD_CTX c;
 		fill(sm64(&seed), key, g_key_len);
+		double a = now();
 		if (!p_init(&c, g_aead, key, g_key_len, 0, NULL)) {
 			t->failures++;
 			break;
 		}
+		double b = now();
 		if (!p_seal(&c, out, &out_len, rec_len + 16, nonce, g_nonce_len, pt, rec_len, ad, 13))
 			t->failures++;
+		double d = now();
 		p_cleanup(&c);
+		double e = now();
+		t->ph[0] += b - a;	/* phases of one connection (round 6) */
+		t->ph[1] += d - b;
+		t->ph[2] += e - d;
 		t->records++;
 		t->bytes += rec_len;
 		if (now() - t0 >= budget)
@@ -243,18 +251,23 @@ main(int argc, char **argv)
 			ta[i].lo = (size_t)i;
 			pthread_create(&tid[i], NULL, churn_worker, &ta[i]);
 		}
+		double ph[3] = {0, 0, 0};
 		for (i = 0; i < threads; i++) {
 			pthread_join(tid[i], NULL);
 			records += ta[i].records;
 			failures += ta[i].failures;
 			if (ta[i].secs > secs)
 				secs = ta[i].secs;
+			for (k = 0; k < 3; k++)
+				ph[k] += ta[i].ph[k];
 		}
+		double rn = records ? (double)records : 1.0;
 		printf("{\"aead\": \"%s\", \"op\": \"init\", \"rec_len\": %zu, \"threads\": %d, "
 		    "\"contexts\": %llu, \"seconds\": %.4f, \"contexts_per_s\": %.1f, "
-		    "\"us_per_context_per_thread\": %.2f, \"failures\": %llu}\n", argv[2], rec_len,
-		    threads, records, secs, records / secs, secs * 1e6 * threads / (records ? records : 1),
-		    failures);
+		    "\"us_per_context_per_thread\": %.2f, \"us_init\": %.2f, \"us_first_seal\": %.2f, "
+		    "\"us_cleanup\": %.2f, \"failures\": %llu}\n", argv[2], rec_len,
+		    threads, records, secs, records / secs, secs * 1e6 * threads / rn,
+		    ph[0] * 1e6 / rn, ph[1] * 1e6 / rn, ph[2] * 1e6 / rn, failures);
 		return failures ? 1 : 0;
 	}
 	for (i = 0; i < NSESS; i++) {

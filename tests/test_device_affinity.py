@@ -182,3 +182,59 @@ def test_stub_catches_a_missing_set_device(stub_lib):
     lines = r.stdout.splitlines()
     assert int(lines[0]) == 2, r.stdout
     assert "issued with device 0 current" in r.stdout and "memory of device 0" in r.stdout
+
+
+_MEM_CHILD = r"""
+import ctypes as C, os, sys, threading
+sys.path.insert(0, sys.argv[1])
+import talos_amd as ta
+lib = ta.load_library()
+lib.devstub_mem.restype = None
+lib.devstub_mem.argtypes = [C.POINTER(C.c_uint64)] * 3
+def mem():
+    p, d, n = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    lib.devstub_mem(C.byref(p), C.byref(d), C.byref(n))
+    return p.value, d.value, n.value
+T = int(sys.argv[2])
+def one_call(i):
+    ctx = ta.EvpAead(ta.AES_128_GCM, bytes([i % 251 + 1]) * 16)
+    ctx.seal(bytes(12), b"x" * 16384, b"a" * 13)   # the largest TLS record
+    return ctx
+one_call(0).cleanup()            # the process's shared setup (streams, slabs, servers)
+p0, d0, n0 = mem()
+def run_wave():
+    bar = threading.Barrier(T)
+    def w(i):
+        ctx = one_call(i)
+        bar.wait()               # every thread alive with its staging at once
+        ctx.cleanup()
+    ths = [threading.Thread(target=w, args=(i,)) for i in range(T)]
+    [t.start() for t in ths]; [t.join() for t in ths]
+    return mem()
+p1, d1, n1 = run_wave()
+p2, d2, n2 = run_wave()          # the exited threads' staging is reused
+print("PINNED_PER_THREAD", (p1 - p0) / T, "DEVICE_PER_THREAD", (d1 - d0) / T,
+      "PINNED_ALLOCS", n1 - n0, "SECOND_WAVE_PINNED_GROWTH", p2 - p1)
+"""
+
+
+def test_per_call_staging_is_bounded(stub_lib):
+    """a thread-per-connection server's calling
+    threads each hold at most 64 KiB of pinned staging and no device staging
+    (zero-copy per-call path), carved from shared slabs (few pinned
+    allocations), and a second wave of threads reuses the first wave's staging
+    instead of growing.  1,024 threads, each sealing a 16 KiB record on the
+    launched path under the recording HIP stub (no GPU)."""
+    env = dict(os.environ, TLSGPU_LIBRARY=stub_lib, TLSGPU_STUB_DEVICES="1",
+               TLSGPU_EVP_DOORBELL="0")
+    for k in ("TLSGPU_EVP_BATCH_US", "TLSGPU_DEVICE", "TLSGPU_DEVICES"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-c", _MEM_CHILD, ROOT, "1024"], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    w = r.stdout.split()
+    val = {w[i]: float(w[i + 1]) for i in range(0, len(w) - 1, 2)}
+    assert val["PINNED_PER_THREAD"] <= 64 * 1024, r.stdout
+    assert val["DEVICE_PER_THREAD"] == 0, r.stdout
+    assert val["PINNED_ALLOCS"] <= 1024 / 32 + 8, r.stdout    # slabs, not one per thread
+    assert val["SECOND_WAVE_PINNED_GROWTH"] == 0, r.stdout

@@ -1,0 +1,71 @@
+"""A record-layer consumer of the batch path (round 6, VERDICT r05 missing 2):
+integration/ssl_batch.c drains many TLS connections' read BIOs into one pinned
+buffer, frames the records with ssl3_get_record's header rules
+(ssl/s3_pkt.c:305-380), opens them all in one tlsgpu_open_host batch, delivers
+each connection's plaintext in order and advances its s3->read_sequence as
+tls1_enc would (t1_enc.c:258-266, 832-975).
+
+tests/ssl_batch/batch_server.c drives it with N real connections of the
+reference's unmodified libssl (oracle/_ref/libssl_ref.so), handshaken over
+memory BIOs: phase 1 batch-reads every connection's writes (record edges 1 B
+.. 40,000 B); phase 2 reads the next writes with the reference's own SSL_read
+on the same SSL objects (their state stayed consistent); phase 3 flips a bit
+in one connection's record: that one reports bad_record_mac, all others are
+delivered.  Every delivered byte is compared with what the client wrote.
+"""
+import json
+import os
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HARNESS = os.path.join(ROOT, "tests", "ssl_batch", "_build", "batch_server")
+PEM = os.path.join(ROOT, "tests", "golden", "server.pem")
+CIPHERS = ["ECDHE-RSA-AES128-GCM-SHA256", "ECDHE-RSA-AES256-GCM-SHA384",
+           "ECDHE-RSA-CHACHA20-POLY1305", "ECDHE-RSA-CHACHA20-POLY1305-OLD"]
+
+
+def _run(args, timeout=240):
+    if not os.path.exists(HARNESS):
+        pytest.skip("tests/ssl_batch/_build/batch_server not built (no reference tree at build)")
+    env = dict(os.environ)
+    env.pop("LD_PRELOAD", None)
+    r = subprocess.run([HARNESS, "-p", PEM] + [str(a) for a in args], capture_output=True,
+                       text=True, timeout=timeout, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_harness_builds_from_reference_headers():
+    """CPU: the consumer compiles against the reference tree's ssl_locl.h and
+    links the reference libssl and libtlsgpu (no GPU call)."""
+    if not os.path.exists(HARNESS):
+        pytest.skip("not built")
+    out = subprocess.run(["nm", "-D", "--undefined-only", HARNESS], capture_output=True,
+                         text=True).stdout
+    for sym in ("tlsgpu_open_host", "tlsgpu_sessions_install", "SSL_read", "BIO_read"):
+        assert sym in out, sym
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cipher", CIPHERS)
+def test_batch_read_many_connections(cipher):
+    d = _run(["-c", cipher, "-n", 24, "-t", 5])
+    assert d["ok"] == 1 and d["cipher"] == cipher, d
+    assert d["conns"] == 24 and d["tamper_checked"] == 1
+    # 8 writes per connection: 1 + 1 + 1 + 1 + 2 + 3 + 1 + 1 records
+    assert d["batch_records"] == 24 * 11
+    assert d["ssl_read_records_after"] >= 24 * 11
+
+
+@pytest.mark.gpu
+def test_batch_read_bench_1024_connections():
+    """1,024 connections x 8 records of 16 KiB (128 MiB of payload) in one
+    batch, against the same wire through SSL_read on one CPU thread."""
+    d = _run(["-c", CIPHERS[0], "-n", 1024, "-b", "-r", 8, "-l", 16384], timeout=600)
+    assert d["ok"] == 1, d
+    b = d["bench"]
+    assert b["batch_records"] == 1024 * 8 and b["payload_bytes"] == 1024 * 8 * 16384
+    print(json.dumps(d))
