@@ -148,6 +148,30 @@ __device__ __forceinline__ void srv_leave(const ServerArgs& s) {
   }
 }
 
+// The 64 KiB GHASH byte-position table (KT_OFF) from the 128 basis entries
+// H^64 * x^q already in LDS: load_session_tables' arithmetic with the basis
+// read from LDS (a broadcast) instead of HBM.  Wave j builds byte position j.
+__device__ void build_kt_from_lds(const uint4* basis) {
+  const uint32_t bl = threadIdx.x & 63;
+  const uint32_t j = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 16 waves, 16 positions
+  uint32_t lo[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < 6; k++) {  // bit k of the byte <-> x^(8j + 7 - k)
+    const uint32_t msk = 0u - ((bl >> k) & 1u);
+    const uint4 b = basis[8 * j + 7 - k];
+    lo[0] ^= b.x & msk; lo[1] ^= b.y & msk; lo[2] ^= b.z & msk; lo[3] ^= b.w & msk;
+  }
+  const uint4 b6 = basis[8 * j + 1], b7 = basis[8 * j + 0];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint32_t m6 = (q & 1) ? 0xFFFFFFFFu : 0u, m7 = (q & 2) ? 0xFFFFFFFFu : 0u;
+    const uint4 v = make_uint4(lo[0] ^ (b6.x & m6) ^ (b7.x & m7), lo[1] ^ (b6.y & m6) ^ (b7.y & m7),
+                               lo[2] ^ (b6.z & m6) ^ (b7.z & m7), lo[3] ^ (b6.w & m6) ^ (b7.w & m7));
+    *reinterpret_cast<uint4*>(s_lds + KT_OFF + (bl + 64u * q) * 256 + j * 16) = v;
+  }
+}
+static_assert(kThreads == 16 * kWave, "one wave per byte position");
+
 __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
   // an instance that only starts after the stop word was set (queued behind
   // the one the process was using at exit) leaves at once
@@ -309,19 +333,46 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
       uint4* dtab = reinterpret_cast<uint4*>(const_cast<DevGcmTables*>(
           reinterpret_cast<const DevGcmTables*>(c->gcm_tables) + sid));
       constexpr uint32_t kS = sizeof(DevSession) / 16;
-      const uint32_t nw = kS + ((c->op & kOpInstallTables) ? kGcmTableUploadBytes / 16 : 0u);
+      constexpr uint32_t kB = sizeof(DevGcmTables::basis) / 16;  // 128 basis entries
+      const bool tables = (c->op & kOpInstallTables) != 0;
+      const uint32_t nw = kS + (tables ? kGcmTableUploadBytes / 16 : 0u);
+      static_assert(kS + kGcmTableUploadBytes / 16 <= 2 * kThreads, "two image words per thread");
+      // round 6: the GCM tables go into this workgroup's LDS straight from the
+      // image as it arrives over PCIe (the Shoup tables to SH_OFF, the basis to
+      // a scratch area the byte table is then built from), beside the HBM copy
+      // — not written to HBM and read back (the connection's first call paid
+      // ~16 µs for that round trip, profiles/r06b_evp_churn.jsonl); both of a
+      // thread's image words are loaded before either is stored
+      const uint4* basis_lds = reinterpret_cast<const uint4*>(s_lds + SRV_STAGE_OFF);
       if (sid < a.n_sessions) {
-        for (uint32_t i = threadIdx.x; i < nw; i += kThreads) {
-          const uint4 v = img[i];
+        const uint32_t i0 = threadIdx.x, i1 = threadIdx.x + kThreads;
+        uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0;
+        if (i0 < nw) v0 = img[i0];
+        if (i1 < nw) v1 = img[i1];
+        auto put = [&](uint32_t i, const uint4& v) {
           if (i < kS) {
             dsess[i] = v;
             reinterpret_cast<uint4*>(s_lds + SRV_SESS_OFF)[i] = v;
-          } else {
-            dtab[i - kS] = v;
+            return;
           }
-        }
+          const uint32_t t = i - kS;
+          dtab[t] = v;
+          if (t < kB) {
+            reinterpret_cast<uint4*>(s_lds + SRV_STAGE_OFF)[t] = v;
+          } else if (t < kB + kPowMax * 16) {
+            const uint32_t k = t - kB;  // 16 (e - 1) + v, as load_session_tables
+            *reinterpret_cast<uint4*>(s_lds + sh_base(1 + (k >> 4)) + (k & 15u) * 256u) = v;
+          }
+        };
+        if (i0 < nw) put(i0, v0);
+        if (i1 < nw) put(i1, v1);
       }
-      __threadfence();  // the slot's HBM copy before this job's table loads
+      __syncthreads();  // the basis in LDS
+      if (tables && sid < a.n_sessions) {
+        build_kt_from_lds(basis_lds);
+        cached_key = key;  // this job's tables are in LDS: gcm_raw_job skips the load
+      }
+      __threadfence();  // the slot's HBM copy before any later reader
       __syncthreads();
     }
     if (op >> 8 == kOpScrub) {
