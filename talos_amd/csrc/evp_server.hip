@@ -335,41 +335,56 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
       constexpr uint32_t kS = sizeof(DevSession) / 16;
       constexpr uint32_t kB = sizeof(DevGcmTables::basis) / 16;  // 128 basis entries
       const bool tables = (c->op & kOpInstallTables) != 0;
-      const uint32_t nw = kS + (tables ? kGcmTableUploadBytes / 16 : 0u);
-      static_assert(kS + kGcmTableUploadBytes / 16 <= 2 * kThreads, "two image words per thread");
-      // round 6: the GCM tables go into this workgroup's LDS straight from the
-      // image as it arrives over PCIe (the Shoup tables to SH_OFF, the basis to
-      // a scratch area the byte table is then built from), beside the HBM copy
-      // — not written to HBM and read back (the connection's first call paid
-      // ~16 µs for that round trip, profiles/r06b_evp_churn.jsonl); both of a
-      // thread's image words are loaded before either is stored
-      const uint4* basis_lds = reinterpret_cast<const uint4*>(s_lds + SRV_STAGE_OFF);
-      if (sid < a.n_sessions) {
-        const uint32_t i0 = threadIdx.x, i1 = threadIdx.x + kThreads;
-        uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0;
-        if (i0 < nw) v0 = img[i0];
-        if (i1 < nw) v1 = img[i1];
-        auto put = [&](uint32_t i, const uint4& v) {
-          if (i < kS) {
-            dsess[i] = v;
-            reinterpret_cast<uint4*>(s_lds + SRV_SESS_OFF)[i] = v;
-            return;
-          }
-          const uint32_t t = i - kS;
-          dtab[t] = v;
-          if (t < kB) {
-            reinterpret_cast<uint4*>(s_lds + SRV_STAGE_OFF)[t] = v;
-          } else if (t < kB + kPowMax * 16) {
-            const uint32_t k = t - kB;  // 16 (e - 1) + v, as load_session_tables
-            *reinterpret_cast<uint4*>(s_lds + sh_base(1 + (k >> 4)) + (k & 15u) * 256u) = v;
-          }
-        };
-        if (i0 < nw) put(i0, v0);
-        if (i1 < nw) put(i1, v1);
+      // round 6: only what the tables are made of crosses PCIe — the
+      // DevSession, the basis H^64 * x^q and each power's Shoup entry m[8] =
+      // H^e (257 words instead of the image's 1,225) — and the workgroup
+      // builds its LDS tables and the slot's HBM copy from them: the byte
+      // table from the basis, each power's 16 Shoup entries from H^e by three
+      // multiplications by x (the linear span of gcm128.c's gcm_init_4bit
+      // table, session_host.cpp shoup_table).  The connection's first call
+      // paid ~16 us for the whole image through HBM (profiles/r06b_*).
+      uint4* basis_lds = reinterpret_cast<uint4*>(s_lds + SRV_STAGE_OFF);
+      uint4* pow_lds = basis_lds + kB;  // H^1 .. H^65 (Shoup m[8] entries)
+      static_assert(SRV_STAGE_OFF + 16 * (kB + kPowMax) <= SRV_MARK_OFF, "install scratch");
+      const uint32_t nw = kS + (tables ? kB + kPowMax : 0u);
+      if (sid < a.n_sessions && threadIdx.x < nw) {
+        const uint32_t i = threadIdx.x;
+        const uint32_t src = i < kS + kB ? i : kS + kB + 16u * (i - kS - kB) + 8u;
+        const uint4 v = img[src];
+        if (i < kS) {
+          dsess[i] = v;
+          reinterpret_cast<uint4*>(s_lds + SRV_SESS_OFF)[i] = v;
+        } else if (i < kS + kB) {
+          dtab[i - kS] = v;
+          basis_lds[i - kS] = v;
+        } else {
+          pow_lds[i - kS - kB] = v;
+        }
       }
-      __syncthreads();  // the basis in LDS
+      static_assert(kS + kB + kPowMax <= kThreads, "one image word per thread");
+      __syncthreads();  // the basis and the powers in LDS
       if (tables && sid < a.n_sessions) {
         build_kt_from_lds(basis_lds);
+        // Shoup entry v of power e: m[v] = [v&8] y ^ [v&4] y.x ^ [v&2] y.x^2 ^
+        // [v&1] y.x^3, BE words (x = a right shift in gcm128.c's bit order)
+        for (uint32_t t = threadIdx.x; t < kPowMax * 16; t += kThreads) {
+          const uint32_t e = t >> 4, vsel = t & 15u;
+          const uint4 y = pow_lds[e];
+          uint32_t w[4] = {y.x, y.y, y.z, y.w}, m[4] = {0, 0, 0, 0};
+#pragma unroll
+          for (int k = 3; k >= 0; k--) {  // bit k of v <-> y.x^(3 - k)
+            const uint32_t msk = 0u - ((vsel >> k) & 1u);
+            m[0] ^= w[0] & msk; m[1] ^= w[1] & msk; m[2] ^= w[2] & msk; m[3] ^= w[3] & msk;
+            const uint32_t carry = 0u - (w[3] & 1u);
+            w[3] = (w[3] >> 1) | (w[2] << 31);
+            w[2] = (w[2] >> 1) | (w[1] << 31);
+            w[1] = (w[1] >> 1) | (w[0] << 31);
+            w[0] = (w[0] >> 1) ^ (carry & 0xE1000000u);
+          }
+          const uint4 mv = make_uint4(m[0], m[1], m[2], m[3]);
+          *reinterpret_cast<uint4*>(s_lds + sh_base(1 + e) + vsel * 256u) = mv;
+          dtab[kB + t] = mv;
+        }
         cached_key = key;  // this job's tables are in LDS: gcm_raw_job skips the load
       }
       __threadfence();  // the slot's HBM copy before any later reader

@@ -35,6 +35,9 @@ faulthandler.enable()
 sys.path.insert(0, sys.argv[1]); sys.path.insert(0, os.path.join(sys.argv[1], "oracle"))
 import talos_amd as ta, pyoracle as po
 lib = ta.load_library()
+lib.tlsgpu_session_image.restype = C.c_int
+lib.tlsgpu_session_image.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+IMG = 1024 + 2048 + 65 * 256 + 15 * 512
 orc = po.Oracle()
 errors = []
 def check(ctx, octx, rnd, kind):
@@ -67,6 +70,15 @@ for kind in kinds:
     buf = (C.c_uint8 * 2048)()
     assert lib.tlsgpu_sessions_debug_read(t_, slot.value, buf, 2048) == 0
     assert any(bytes(buf)), "installed slot reads zero"
+    # round 6: the doorbell install builds the slot's Shoup tables on the
+    # device from H^e; the slot must hold exactly the host image's bytes
+    used = 1024 + (2048 + 65 * 256 if kind != po.CHACHA20_POLY1305 else 0)
+    full = (C.c_uint8 * used)()
+    assert lib.tlsgpu_sessions_debug_read(t_, slot.value, full, used) == 0
+    img = (C.c_uint8 * IMG)()
+    prm = ta.SessionParams(kind, key, b"", tag_len=16, version=0x0303).to_c()
+    assert lib.tlsgpu_session_image(C.byref(prm), img, IMG) == 0
+    assert bytes(full) == bytes(img)[:used], (kind, "doorbell-installed slot differs from the host image")
     ctx.cleanup()
     assert lib.tlsgpu_sessions_debug_read(t_, slot.value, buf, 2048) == 0
     assert not any(bytes(buf)), (kind, "key material left after cleanup")
