@@ -21,6 +21,7 @@
 
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "ssl_locl.h" /* SSL_AEAD_CTX, SSL3_STATE (the reference tree's own header) */
 
@@ -43,7 +44,25 @@ struct tlsgpu_ssl_batch {
 	int32_t *status;          /* pinned */
 	uint32_t rec_cap;
 	uint32_t *first, *count;  /* per position in conns[]: its descriptors */
+	double t_gather, t_open, t_deliver;  /* the last call's phases, seconds */
 };
+
+static double
+now_s(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+void
+tlsgpu_ssl_batch_times(const tlsgpu_ssl_batch *b, double *gather_s, double *open_s,
+    double *deliver_s)
+{
+	*gather_s = b->t_gather;
+	*open_s = b->t_open;
+	*deliver_s = b->t_deliver;
+}
 
 int
 tlsgpu_ssl_batch_create(int device, uint32_t max_conns, size_t wire_bytes, tlsgpu_ssl_batch **out)
@@ -172,6 +191,8 @@ tlsgpu_ssl_batch_read(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
 	int delivered = 0, rc;
 	if (!b || (n && (!conns || !conn_status)))
 		return TLSGPU_EINVAL;
+	const double t0 = now_s();
+	b->t_gather = b->t_open = b->t_deliver = 0;
 	for (uint32_t i = 0; i < n; i++) {
 		const uint32_t id = conns[i];
 		struct conn *c = id < b->cap ? &b->c[id] : NULL;
@@ -241,12 +262,16 @@ tlsgpu_ssl_batch_read(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
 		}
 		used = p;
 	}
+	const double t1 = now_s();
+	b->t_gather = t1 - t0;
 	if (nrec == 0)
 		return 0;
 	/* 3. one batch for every connection's records, in place */
 	if ((rc = tlsgpu_open_host(b->t, b->recs, nrec, b->wire, used, b->wire, used,
 	    b->status)) != TLSGPU_OK)
 		return rc;
+	const double t2 = now_s();
+	b->t_open = t2 - t1;
 	/* 4. deliver in record order per connection; the read sequence advances
 	 *    over every record opened (a failed one ends the connection's batch) */
 	for (uint32_t i = 0; i < n; i++) {
@@ -267,5 +292,6 @@ tlsgpu_ssl_batch_read(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
 		}
 		seq_store(c->s->s3->read_sequence, seq_load(c->s->s3->read_sequence) + k);
 	}
+	b->t_deliver = now_s() - t2;
 	return delivered;
 }

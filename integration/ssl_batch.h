@@ -74,6 +74,11 @@ int tlsgpu_ssl_batch_attach(tlsgpu_ssl_batch *b, uint32_t conn, SSL *s, const ui
 int tlsgpu_ssl_batch_read(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
     tlsgpu_ssl_deliver_fn deliver, void *arg, int *conn_status);
 
+/* The last tlsgpu_ssl_batch_read's phases (wall clock, seconds): gather +
+ * framing, the GPU batch (tlsgpu_open_host: H2D, kernels, D2H), delivery. */
+void tlsgpu_ssl_batch_times(const tlsgpu_ssl_batch *b, double *gather_s, double *open_s,
+    double *deliver_s);
+
 #ifdef __cplusplus
 }
 #endif

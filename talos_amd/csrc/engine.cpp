@@ -2064,6 +2064,7 @@ struct EvpServer {
   std::atomic<uint64_t> tr_n{0}, tr_load{0}, tr_job{0}, tr_rel{0}, tr_host_ns{0};
   std::atomic<uint64_t> tr_marks_n{0}, tr_phase[8] = {};  // GCM jobs: loaded -> mark 0 .. 6 -> done
   std::atomic<uint64_t> tr_last[4] = {};  // since loaded: wave 0 blocks / shoup, last wave blocks / shoup
+  std::atomic<uint64_t> tr_inst_n{0}, tr_inst[2] = {};  // install jobs: loaded -> image read -> tables built
 };
 static EvpServer* g_servers[kMaxEvpDevices] = {};
 // the servers whose setup succeeded, read without the lock on every call (a
@@ -2340,6 +2341,10 @@ static void print_doorbell_trace() {
                       "\"last_wave_blocks\": %.2f, \"last_wave_shoup\": %.2f}}}\n",
               sv->tr_last[0].load() * 0.01 / m, sv->tr_last[1].load() * 0.01 / m,
               sv->tr_last[2].load() * 0.01 / m, sv->tr_last[3].load() * 0.01 / m);
+      if (const uint64_t ni = sv->tr_inst_n.load())
+        fprintf(stderr, "{\"doorbell_install_us\": {\"jobs\": %llu, \"image_read\": %.2f, "
+                        "\"tables_built\": %.2f}}\n", (unsigned long long)ni,
+                sv->tr_inst[0].load() * 0.01 / ni, sv->tr_inst[1].load() * 0.01 / ni);
     }
   }
 }
@@ -2959,6 +2964,11 @@ static int gpu_call_impl(const AeadState* st, bool seal, unsigned char* out, siz
           sv->tr_last[1].fetch_add(tr[6] - tr[1], std::memory_order_relaxed);
           sv->tr_last[2].fetch_add(lw_b, std::memory_order_relaxed);
           sv->tr_last[3].fetch_add(lw_s, std::memory_order_relaxed);
+          if (tr[13] >= tr[1] && tr[14] >= tr[13] && tr[13] != 0) {  // an install job (round 6)
+            sv->tr_inst_n.fetch_add(1, std::memory_order_relaxed);
+            sv->tr_inst[0].fetch_add(tr[13] - tr[1], std::memory_order_relaxed);
+            sv->tr_inst[1].fetch_add(tr[14] - tr[13], std::memory_order_relaxed);
+          }
         }
       }
       const int32_t status = *reinterpret_cast<const int32_t*>(h + o_status);

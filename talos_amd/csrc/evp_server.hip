@@ -82,7 +82,7 @@ constexpr uint32_t SRV_SLOT_OFF = PLAN_OFF + 512;     // LDS copy of the picked 
 static_assert(PLAN_OFF + 288 <= SRV_SLOT_OFF, "server LDS plan");
 static_assert(SRV_SLOT_OFF + sizeof(DoorbellSlot) <= SRV_STAGE_OFF, "server LDS plan");
 static_assert(SRV_STAGE_OFF + 4096 <= SRV_MARK_OFF, "server LDS plan");
-static_assert(SRV_MARK_OFF + 80 <= LDS_BYTES, "server LDS plan");
+static_assert(SRV_MARK_OFF + 88 <= SRV_MARK_OFF + 128, "11 job marks before the session copy");
 // the GCM job's DevSession, copied into LDS once per installed key: the job's
 // session reads (kind, rounds, tag_len, round keys) are then LDS reads, not
 // one dependent HBM round trip each (round-4 trace: parse + setup ≈ 2.3 µs)
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
           sess_key = key;
         }
       }
-      if (lane < 9) reinterpret_cast<unsigned long long*>(s_lds + SRV_MARK_OFF)[lane] = 0;
+      if (lane < 11) reinterpret_cast<unsigned long long*>(s_lds + SRV_MARK_OFF)[lane] = 0;
       __builtin_amdgcn_s_waitcnt(0);
       t_loaded = __builtin_amdgcn_s_memrealtime();
     }
@@ -363,6 +363,7 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
       }
       static_assert(kS + kB + kPowMax <= kThreads, "one image word per thread");
       __syncthreads();  // the basis and the powers in LDS
+      TG_JOB_MARK(9);
       if (tables && sid < a.n_sessions) {
         build_kt_from_lds(basis_lds);
         // Shoup entry v of power e: m[v] = [v&8] y ^ [v&4] y.x ^ [v&2] y.x^2 ^
@@ -387,8 +388,10 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
         }
         cached_key = key;  // this job's tables are in LDS: gcm_raw_job skips the load
       }
-      __threadfence();  // the slot's HBM copy before any later reader
+      // the slot's HBM copy reaches other readers through the job's release
+      // (every wave's stores complete before `done`, below): no fence here
       __syncthreads();
+      TG_JOB_MARK(10);
     }
     if (op >> 8 == kOpScrub) {
       // EVP_AEAD_CTX_cleanup (e_aes.c:1415-1422 explicit_bzero analogue): the
@@ -464,6 +467,8 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(tr + 11, mk[7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(tr + 12, mk[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(tr + 13, mk[9], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(tr + 14, mk[10], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       __atomic_thread_fence(__ATOMIC_RELEASE);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

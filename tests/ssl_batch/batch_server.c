@@ -411,6 +411,8 @@ main(int argc, char **argv)
 		double t0 = now();
 		r = tlsgpu_ssl_batch_read(B, bids, (uint32_t)nb, on_deliver, P, st);
 		double t1 = now();
+		double tg, to, td;
+		tlsgpu_ssl_batch_times(B, &tg, &to, &td);
 		long gbytes = 0;
 		for (int i = 0; i < nb; i++) {
 			if (st[i] != TLSGPU_SSL_OK)
@@ -439,10 +441,13 @@ main(int argc, char **argv)
 			ok = 0;
 		printf(", \"bench\": {\"records_per_conn\": %d, \"record_len\": %d, \"payload_bytes\": %ld, "
 		    "\"batch_records\": %d, \"batch_s\": %.6f, \"batch_GiBps\": %.3f, "
+		    "\"batch_phases_s\": {\"gather\": %.6f, \"gpu_open_host\": %.6f, \"deliver\": %.6f}, "
+		    "\"gpu_open_host_GiBps\": %.3f, "
 		    "\"ssl_read_cpu1_s\": %.6f, \"ssl_read_cpu1_GiBps\": %.3f, "
 		    "\"timing\": \"wall clock: tlsgpu_ssl_batch_read (BIO gather + pinned H2D + open + "
 		    "D2H + delivery copy) vs SSL_read over the same wire on one thread\"}",
-		    brec, blen, bytes, r, t1 - t0, bytes / (t1 - t0) / 1073741824.0, t3 - t2,
+		    brec, blen, bytes, r, t1 - t0, bytes / (t1 - t0) / 1073741824.0, tg, to, td,
+		    bytes / to / 1073741824.0, t3 - t2,
 		    cbytes / (t3 - t2) / 1073741824.0);
 		free(msg);
 	}
