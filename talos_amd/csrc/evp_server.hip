@@ -48,6 +48,9 @@ constexpr uint32_t kSrvStageMax = 4096;
 constexpr uint32_t kSrvStageWave = 12;  // waves 12..15 copy (idle: a 4 KiB job has <= 4 ranges)
 }
 #define TG_JOB_STAGE 1
+// the server issues a GCM job's input staging itself, before the job's
+// install (round 6): the two PCIe reads then overlap
+#define TG_JOB_STAGE_EARLY 1
 namespace tg {
 __device__ __forceinline__ bool tg_stage_ok(const RawJob* J) {
   const uint32_t n = J->in_len;
@@ -148,20 +151,26 @@ __device__ __forceinline__ void srv_leave(const ServerArgs& s) {
   }
 }
 
-// The 64 KiB GHASH byte-position table (KT_OFF) from the 128 basis entries
-// H^64 * x^q already in LDS: load_session_tables' arithmetic with the basis
-// read from LDS (a broadcast) instead of HBM.  Wave j builds byte position j.
-__device__ void build_kt_from_lds(const uint4* basis) {
+// The 64 KiB GHASH byte-position table (KT_OFF) from its one-bit entries,
+// already in place: load_session_tables' arithmetic, with basis entry
+// x^(8j + 7 - k) read as T[1 << k][j].  Wave j builds byte position j; the
+// one-bit entries are rewritten with the values they hold.
+__device__ void build_kt_in_place() {
   const uint32_t bl = threadIdx.x & 63;
   const uint32_t j = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 16 waves, 16 positions
+  auto one_bit = [&](int k) {
+    return *reinterpret_cast<const uint4*>(s_lds + KT_OFF + (1u << k) * 256 + j * 16);
+  };
   uint32_t lo[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int k = 0; k < 6; k++) {  // bit k of the byte <-> x^(8j + 7 - k)
     const uint32_t msk = 0u - ((bl >> k) & 1u);
-    const uint4 b = basis[8 * j + 7 - k];
+    const uint4 b = one_bit(k);
     lo[0] ^= b.x & msk; lo[1] ^= b.y & msk; lo[2] ^= b.z & msk; lo[3] ^= b.w & msk;
   }
-  const uint4 b6 = basis[8 * j + 1], b7 = basis[8 * j + 0];
+  const uint4 b6 = one_bit(6), b7 = one_bit(7);
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): every one-bit read before any write
+  __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int q = 0; q < 4; q++) {
     const uint32_t m6 = (q & 1) ? 0xFFFFFFFFu : 0u, m7 = (q & 2) ? 0xFFFFFFFFu : 0u;
@@ -321,6 +330,10 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
     const uint32_t sid = __builtin_amdgcn_readfirstlane(c->job.session);
     if (((op >> 8) == 10 || (op >> 8) == 14) && sid < a.n_sessions && key != 0)  // GCM: LDS copy
       a.sessions = reinterpret_cast<const DevSession*>(s_lds + SRV_SESS_OFF) - sid;
+    // a GCM job's input into LDS by waves 12-15 now (gcm_raw_job's staging,
+    // TG_JOB_STAGE_EARLY): its PCIe read overlaps the install's
+    if (((op >> 8) == 10 || (op >> 8) == 14) && tg_stage_ok(&c->job))
+      tg_stage_issue(&c->job, wave, threadIdx.x & 63);
     if (c->op & kOpInstall) {
       // EVP_AEAD_CTX_init's deferred install (round 5, engine.cpp): the image
       // the host built (session_host.cpp) goes from pinned memory into the
@@ -343,9 +356,11 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
       // multiplications by x (the linear span of gcm128.c's gcm_init_4bit
       // table, session_host.cpp shoup_table).  The connection's first call
       // paid ~16 us for the whole image through HBM (profiles/r06b_*).
-      uint4* basis_lds = reinterpret_cast<uint4*>(s_lds + SRV_STAGE_OFF);
-      uint4* pow_lds = basis_lds + kB;  // H^1 .. H^65 (Shoup m[8] entries)
-      static_assert(SRV_STAGE_OFF + 16 * (kB + kPowMax) <= SRV_MARK_OFF, "install scratch");
+      // no scratch: basis entry q = H^64 x^q IS the byte table's entry for
+      // the one-bit byte 1 << (7 - q % 8) at position q / 8, and H^e IS its
+      // Shoup table's entry m[8]: phase 1 puts them there, phase 2 derives
+      // the rest of both tables from them (rewriting those entries with the
+      // same values)
       const uint32_t nw = kS + (tables ? kB + kPowMax : 0u);
       if (sid < a.n_sessions && threadIdx.x < nw) {
         const uint32_t i = threadIdx.x;
@@ -355,22 +370,23 @@ __global__ __launch_bounds__(kThreads, 1) void evp_server_kernel(ServerArgs s) {
           dsess[i] = v;
           reinterpret_cast<uint4*>(s_lds + SRV_SESS_OFF)[i] = v;
         } else if (i < kS + kB) {
-          dtab[i - kS] = v;
-          basis_lds[i - kS] = v;
+          const uint32_t q = i - kS;
+          dtab[q] = v;
+          *reinterpret_cast<uint4*>(s_lds + KT_OFF + (1u << (7 - (q & 7))) * 256 + (q >> 3) * 16) = v;
         } else {
-          pow_lds[i - kS - kB] = v;
+          *reinterpret_cast<uint4*>(s_lds + sh_base(1 + (i - kS - kB)) + 8u * 256u) = v;
         }
       }
       static_assert(kS + kB + kPowMax <= kThreads, "one image word per thread");
-      __syncthreads();  // the basis and the powers in LDS
+      __syncthreads();  // the one-bit byte entries and the powers in LDS
       TG_JOB_MARK(9);
       if (tables && sid < a.n_sessions) {
-        build_kt_from_lds(basis_lds);
+        build_kt_in_place();
         // Shoup entry v of power e: m[v] = [v&8] y ^ [v&4] y.x ^ [v&2] y.x^2 ^
         // [v&1] y.x^3, BE words (x = a right shift in gcm128.c's bit order)
         for (uint32_t t = threadIdx.x; t < kPowMax * 16; t += kThreads) {
           const uint32_t e = t >> 4, vsel = t & 15u;
-          const uint4 y = pow_lds[e];
+          const uint4 y = *reinterpret_cast<const uint4*>(s_lds + sh_base(1 + e) + 8u * 256u);
           uint32_t w[4] = {y.x, y.y, y.z, y.w}, m[4] = {0, 0, 0, 0};
 #pragma unroll
           for (int k = 3; k >= 0; k--) {  // bit k of v <-> y.x^(3 - k)

@@ -71,7 +71,9 @@ __device__ __forceinline__ bool gcm_raw_job(const BatchArgs& a, uint32_t r,
   __syncthreads();
   TG_JOB_MARK(0);
   const bool staged = !TLS && TG_JOB_STAGE && tg_stage_ok(J);
+#ifndef TG_JOB_STAGE_EARLY
   if (staged) tg_stage_issue(J, wave, lane);
+#endif
   RecCtx rc;
   if (TLS) {
     // every wave parses (same descriptor): a publicly invalid record returns
