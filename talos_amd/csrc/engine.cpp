@@ -2537,6 +2537,7 @@ static DoorbellSlot* thread_scrub_slot(EvpServer* sv, size_t k, uint32_t** seq) 
 }
 
 static void slab_give(size_t dk, tlsgpu_sessions* t, uint32_t slot);
+constexpr uint32_t kScrubSweepBatch = 32;  // pending scrubs before an init sweeps
 // Give back the session slots whose cleanup scrub has been answered; wait up to
 // `wait_ns` for the others (relaunching the server when an instance left before
 // picking a post up).  With `only`, just the entries of that (table, slot).
@@ -2546,7 +2547,14 @@ static void sweep_scrubs(EvpServer* sv, uint64_t wait_ns, const tlsgpu_sessions*
   for (;;) {
     bool left = false, overdue = false;
     {
-      std::lock_guard<std::mutex> lk(sv->pend_mu);
+      // no wait asked: another thread's sweep does the work (init and cleanup
+      // of many threads must not queue on this lock)
+      std::unique_lock<std::mutex> lk(sv->pend_mu, std::defer_lock);
+      if (wait_ns == 0) {
+        if (!lk.try_lock()) return;
+      } else {
+        lk.lock();
+      }
       auto& v = sv->pending;
       for (size_t i = 0; i < v.size();) {
         const auto& e = v[i];
@@ -2588,10 +2596,14 @@ static bool doorbell_scrub_async(const AeadState* st) {
   DoorbellSlot* ds = thread_scrub_slot(sv, st->evp_dev, &seq);
   if (!ds) return false;
   const uint64_t t0 = mono_ns();
-  while (__atomic_load_n(&ds->done, __ATOMIC_ACQUIRE) != *seq) {  // the previous scrub
+  for (uint64_t spins = 1; __atomic_load_n(&ds->done, __ATOMIC_ACQUIRE) != *seq; spins++) {
+    // the previous scrub on this slot (normally answered long ago)
     if (mono_ns() - t0 > 10000000000ull) return false;
-    sweep_scrubs(sv, 0);
     __builtin_ia32_pause();
+    if ((spins & 255) == 0) {
+      sweep_scrubs(sv, 0);  // relaunches the server if an instance left before picking it up
+      sched_yield();
+    }
   }
   if (!server_ensure(sv)) return false;
   const uint32_t idx = (uint32_t)(ds - sv->slots);
@@ -2620,7 +2632,9 @@ static bool doorbell_scrub_async(const AeadState* st) {
 static void evp_sweep_scrubs_for(size_t dk) {
   if (dk >= (size_t)kMaxEvpDevices) return;
   EvpServer* sv = g_ready_servers[dk].load(std::memory_order_acquire);
-  if (sv && sv->npending.load(std::memory_order_relaxed) != 0) sweep_scrubs(sv, 0);
+  // answered scrubs' slots go back in batches: a sweep per init cost 16
+  // calling threads ~10 us of lock hand-offs each (profiles/r06f_evp_churn)
+  if (sv && sv->npending.load(std::memory_order_relaxed) >= kScrubSweepBatch) sweep_scrubs(sv, 0);
 }
 static void evp_wait_scrub_of(const tlsgpu_sessions* t, uint32_t slot) {
   for (size_t k = 0; k < (size_t)kMaxEvpDevices; k++) {
