@@ -1301,6 +1301,7 @@ struct AeadState {
   uint8_t* img_h = nullptr;  // pinned image (host / device views)
   uint8_t* img_d = nullptr;
   bool img_tables = false;   // the image has GCM tables
+  bool img_compact = false;  // ... only m[8] = H^e of each Shoup table (round 6)
   hipEvent_t slot_ev = nullptr;  // the slot's event: its previous owner's scrub
 };
 
@@ -1798,8 +1799,13 @@ static int defer_install(AeadState* st, const tlsgpu_session_params& p) {
   st->slot_ev = slot_event(t, st->slot);  // its previous owner's scrub, if launched
   if (!st->slot_ev) return fail(TLSGPU_EHIP, "slot event");
   if (!image_take(t->eng->device, &st->img_h, &st->img_d)) return fail(TLSGPU_ENOMEM, "session image");
+  // compact (round 6): the doorbell install reads m[8] = H^e of each Shoup
+  // table and expands the rest on the device; a launched first call
+  // completes the image on the host before its upload
   st->img_tables = host_session_image(p, reinterpret_cast<DevSession*>(st->img_h),
-                                      reinterpret_cast<DevGcmTables*>(st->img_h + sizeof(DevSession)));
+                                      reinterpret_cast<DevGcmTables*>(st->img_h + sizeof(DevSession)),
+                                      kGcmTableUploadBytes > offsetof(DevGcmTables, bsrk), true);
+  st->img_compact = st->img_tables;
   st->installed = st->slot_ev;
   st->install_pending.store(false, std::memory_order_release);  // nothing queued
   st->image.store(1, std::memory_order_release);
@@ -3007,6 +3013,8 @@ launched:
   // a deferred install on the launched path: one upload kernel ahead of the job
   if (claim.active) {
     if (hipStreamWaitEvent(s, st->slot_ev, 0) != hipSuccess) return -1;
+    if (st->img_compact)  // the upload copies whole Shoup tables
+      host_image_complete(reinterpret_cast<DevGcmTables*>(st->img_h + sizeof(DevSession)));
     claim.posted = true;  // queued from here on, whatever fails after it
     if (launch_upload_session(st->img_d, st->sess->d_sess + st->slot, st->sess->d_gcm + st->slot,
                               st->img_tables ? kGcmTableUploadBytes : 0u, s) != 0)

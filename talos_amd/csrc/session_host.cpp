@@ -182,7 +182,7 @@ bool host_crypto_ok() { return cpu_has_aesni_pclmul(); }
 // The caller's buffers may hold anything; every byte install_body writes is
 // written here.
 bool host_session_image(const tlsgpu_session_params& p, DevSession* s, DevGcmTables* t,
-                        bool bitsliced_masks) {
+                        bool bitsliced_masks, bool compact) {
   memset(s, 0, sizeof(*s));
   const bool gcm = p.aead == TLSGPU_AES_128_GCM || p.aead == TLSGPU_AES_256_GCM;
   const bool cc = p.aead == TLSGPU_CHACHA20_POLY1305 || p.aead == TLSGPU_CHACHA20_POLY1305_OLD;
@@ -229,8 +229,12 @@ bool host_session_image(const tlsgpu_session_params& p, DevSession* s, DevGcmTab
   // H^1 .. H^65 and their Shoup tables; basis[q] = H^64 * x^q
   U128 pw = H, m[16];
   for (int e = 1; e <= kPowMax; e++) {
-    shoup_table(pw, m);
-    for (int v = 0; v < 16; v++) store_be(t->shoup[e - 1][v], m[v]);
+    if (compact) {  // m[8] = H^e only: the doorbell install expands the rest
+      store_be(t->shoup[e - 1][8], pw);
+    } else {
+      shoup_table(pw, m);
+      for (int v = 0; v < 16; v++) store_be(t->shoup[e - 1][v], m[v]);
+    }
     if (e == 64) {
       U128 b = pw;
       for (int q = 0; q < 128; q++) {
@@ -248,6 +252,19 @@ bool host_session_image(const tlsgpu_session_params& p, DevSession* s, DevGcmTab
   for (auto& x : m) x = U128{0, 0};
   return true;
 #endif
+}
+
+// The Shoup entries of a compact image (host_session_image(..., compact)):
+// each power's 16 entries from its m[8] = H^e, for a path that uploads the
+// whole image (the launched first call, engine.cpp gpu_call_impl).
+void host_image_complete(DevGcmTables* t) {
+  U128 m[16];
+  for (int e = 1; e <= kPowMax; e++) {
+    const uint32_t* w = t->shoup[e - 1][8];
+    const U128 y{((uint64_t)w[0] << 32) | w[1], ((uint64_t)w[2] << 32) | w[3]};
+    shoup_table(y, m);
+    for (int v = 0; v < 16; v++) store_be(t->shoup[e - 1][v], m[v]);
+  }
 }
 
 }  // namespace tg

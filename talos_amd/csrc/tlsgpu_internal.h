@@ -376,7 +376,9 @@ constexpr uint32_t kGcmTableUploadBytes = offsetof(DevGcmTables, bsrk);
 // bitsliced masks only when a kernel of this build reads them)
 bool host_crypto_ok();  // AES-NI + PCLMUL present: the host image can be built
 bool host_session_image(const tlsgpu_session_params& p, DevSession* s, DevGcmTables* t,
-                        bool bitsliced_masks = kGcmTableUploadBytes > offsetof(DevGcmTables, bsrk));
+                        bool bitsliced_masks = kGcmTableUploadBytes > offsetof(DevGcmTables, bsrk),
+                        bool compact = false);
+void host_image_complete(DevGcmTables* t);  // a compact image's Shoup entries
 int launch_check_bounds(const tlsgpu_record* recs, tlsgpu_record* safe, uint32_t n,
                         const DevSession* sessions, uint32_t n_sessions, uint64_t in_bytes,
                         uint64_t out_bytes, bool seal, int32_t* status, uint32_t* ctl,
