@@ -35,7 +35,7 @@ errors = []
 def worker(t):
     rnd = random.Random(4100 + t)
     try:
-        for i in range(30):
+        for i in range(int(os.environ.get("TLSGPU_SOAK_ITERS", "30"))):
             kind = kinds[(t + i) % len(kinds)]
             key = bytes(rnd.randrange(256) for _ in range(po.KEY_LEN[kind]))
             chacha = kind in (po.CHACHA20_POLY1305, po.CHACHA20_POLY1305_OLD)
@@ -74,10 +74,13 @@ print("OK", jobs, launches)
 
 @pytest.mark.parametrize("threads", [1, 12])
 def test_evp_doorbell_matches_oracle(threads):
+    """TLSGPU_SOAK_ITERS=N: N contexts per thread instead of 30 (a soak run;
+    profiles/r06*_soak_doorbell*)."""
     env = dict(os.environ, TLSGPU_EVP_DOORBELL="4", TLSGPU_EVP_DOORBELL_MS="40", TLSGPU_CRASH_TRACE="1")
     env.pop("TLSGPU_EVP_BATCH_US", None)
+    iters = int(os.environ.get("TLSGPU_SOAK_ITERS", "30"))
     r = subprocess.run([sys.executable, "-c", _CHILD, ROOT, str(threads)], env=env,
-                       capture_output=True, text=True, timeout=110)
+                       capture_output=True, text=True, timeout=110 + iters * 3)
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
 
