@@ -244,12 +244,12 @@ bool host_session_image(const tlsgpu_session_params& p, DevSession* s, DevGcmTab
     }
     pw = gmult_clmul(pw, H);
   }
-  volatile uint8_t* wipe = reinterpret_cast<volatile uint8_t*>(rk);
-  for (size_t i = 0; i < sizeof(rk); i++) wipe[i] = 0;
-  wipe = hb;
-  for (size_t i = 0; i < sizeof(hb); i++) wipe[i] = 0;
-  pw = H = U128{0, 0};
-  for (auto& x : m) x = U128{0, 0};
+  // key material off the stack (explicit_bzero: not removed as dead stores)
+  explicit_bzero(rk, sizeof(rk));
+  explicit_bzero(hb, sizeof(hb));
+  explicit_bzero(&pw, sizeof(pw));
+  explicit_bzero(&H, sizeof(H));
+  explicit_bzero(m, sizeof(m));
   return true;
 #endif
 }
@@ -265,6 +265,7 @@ void host_image_complete(DevGcmTables* t) {
     shoup_table(y, m);
     for (int v = 0; v < 16; v++) store_be(t->shoup[e - 1][v], m[v]);
   }
+  explicit_bzero(m, sizeof(m));
 }
 
 }  // namespace tg
