@@ -476,10 +476,26 @@ def test_batch_packs_long_runs(ta, engine, oracle, gcm_impl):
 LONG_ONLY = [ln for ln in LENGTHS + BS_LENGTHS if ln > 992]
 
 
+@pytest.mark.parametrize("shift,in_place", [(0, False), (3, False), (0, True)])
 @pytest.mark.parametrize("name", ["aes-128-gcm", "aes-256-gcm"])
-def test_batch_queue_no_pack_variant(ta, engine, oracle, gcm_impl, name):
+def test_batch_queue_no_pack_variant(ta, engine, oracle, gcm_impl, name, shift, in_place):
     gcm_impl("queue")
-    _run_seal_open(ta, engine, oracle, [KINDS[name]] * 2, LONG_ONLY, seed=43)
+    _run_seal_open(ta, engine, oracle, [KINDS[name]] * 2, LONG_ONLY, seed=43, in_shift=shift,
+                   in_place=in_place)
+
+
+# Session runs of config-B records with a ragged tail: the run's last claims
+# (the tail-priority window) over long, ragged and misaligned
+# records, every 5th tampered.
+RUN_TAIL = [16384] * 40 + [16383, 4096, 4097, 8191, 5000, 12345, 16385, 20000, 4095, 1000,
+                           16384, 6000, 7000, 9000, 10000, 16384]
+
+
+@pytest.mark.parametrize("shift", [0, lambda i: 5 if i % 7 == 3 else 0])
+@pytest.mark.parametrize("name", ["aes-128-gcm", "aes-256-gcm"])
+def test_batch_queue_run_tails(ta, engine, oracle, gcm_impl, name, shift):
+    gcm_impl("queue")
+    _run_seal_open(ta, engine, oracle, [KINDS[name]] * 3, RUN_TAIL, seed=47, in_shift=shift)
 
 
 def test_batch_queue_mixed_key_sizes_pack_flags(ta, engine, oracle, gcm_impl):
