@@ -16,9 +16,17 @@
  *   4. deliver  per connection, in record order, until its first failure;
  *               read_sequence += records opened (tls1_record_sequence_increment,
  *               t1_enc.c:258-266, once per record as tls1_enc does).
+ *
+ * Pipelined: the connections are taken in groups of about kGroupBytes of wire,
+ * alternating between two halves of the pinned buffer.  A worker thread runs
+ * group k's tlsgpu_open_host while the calling thread delivers group k-1 and
+ * gathers group k+1, so the GPU batch (PCIe in, kernels, PCIe out) overlaps
+ * the host copies.  BIO reads, delivery callbacks and SSL state stay on the
+ * calling thread.
  */
 #include "ssl_batch.h"
 
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -33,19 +41,65 @@ struct conn {
 	size_t pend_len;
 };
 
+/* wire bytes per group: the pipeline's unit (16 MiB: ~0.4 ms of PCIe each way) */
+static const size_t kGroupBytes = (size_t)16 << 20;
+
+struct group {
+	uint32_t i0, i1;          /* positions in conns[] */
+	size_t used;              /* wire bytes */
+	uint32_t nrec;
+};
+
 struct tlsgpu_ssl_batch {
 	tlsgpu_engine *e;
 	tlsgpu_sessions *t;
 	uint32_t cap;
 	struct conn *c;
-	uint8_t *wire;            /* pinned */
-	size_t wire_cap;
-	tlsgpu_record *recs;      /* pinned */
-	int32_t *status;          /* pinned */
-	uint32_t rec_cap;
-	uint32_t *first, *count;  /* per position in conns[]: its descriptors */
-	double t_gather, t_open, t_deliver;  /* the last call's phases, seconds */
+	uint8_t *wire;            /* pinned, nslot slots of slot_cap bytes */
+	size_t wire_cap, slot_cap;
+	tlsgpu_record *recs;      /* pinned, rec_cap per slot */
+	int32_t *status;          /* pinned, rec_cap per slot */
+	uint32_t rec_cap, nslot;
+	uint32_t *first, *count;  /* per position in conns[]: its descriptors in its slot */
+	struct group g[2];
+	double t_gather, t_open, t_deliver;  /* the last call's phases, seconds (overlapped) */
+	/* the GPU worker: runs tlsgpu_open_host on one posted slot at a time */
+	pthread_t worker;
+	int have_worker, quit, posted, done[2], rc[2];
+	pthread_mutex_t mu;
+	pthread_cond_t cv;
 };
+
+static double now_s(void);
+
+static void *
+gpu_worker(void *p)
+{
+	tlsgpu_ssl_batch *b = p;
+	pthread_mutex_lock(&b->mu);
+	for (;;) {
+		while (!b->quit && b->posted < 0)
+			pthread_cond_wait(&b->cv, &b->mu);
+		if (b->quit)
+			break;
+		const int s = b->posted;
+		b->posted = -1;
+		const struct group g = b->g[s];
+		pthread_mutex_unlock(&b->mu);
+		uint8_t *w = b->wire + (size_t)s * b->slot_cap;
+		const double t0 = now_s();
+		const int rc = tlsgpu_open_host(b->t, b->recs + (size_t)s * b->rec_cap, g.nrec, w, g.used,
+		    w, g.used, b->status + (size_t)s * b->rec_cap);
+		const double dt = now_s() - t0;
+		pthread_mutex_lock(&b->mu);
+		b->t_open += dt;
+		b->rc[s] = rc;
+		b->done[s] = 1;
+		pthread_cond_broadcast(&b->cv);
+	}
+	pthread_mutex_unlock(&b->mu);
+	return NULL;
+}
 
 static double
 now_s(void)
@@ -72,19 +126,35 @@ tlsgpu_ssl_batch_create(int device, uint32_t max_conns, size_t wire_bytes, tlsgp
 	if (!b || !max_conns || wire_bytes < SSL3_RT_MAX_PACKET_SIZE)
 		return free(b), TLSGPU_EINVAL;
 	b->cap = max_conns;
+	/* two slots (pipelined) when each still holds two records of the largest size */
+	b->nslot = wire_bytes >= 4 * (size_t)SSL3_RT_MAX_PACKET_SIZE ? 2u : 1u;
+	b->slot_cap = wire_bytes / b->nslot;
 	/* at most one record per 5 + 1 header + fragment bytes: size the
 	 * descriptor arrays for the smallest legal AEAD record (tag only) */
-	b->rec_cap = (uint32_t)(wire_bytes / (SSL3_RT_HEADER_LENGTH + 16) + 1);
+	b->rec_cap = (uint32_t)(b->slot_cap / (SSL3_RT_HEADER_LENGTH + 16) + 1);
+	b->posted = -1;
+	if (pthread_mutex_init(&b->mu, NULL) != 0)
+		return free(b), TLSGPU_ENOMEM;
+	if (pthread_cond_init(&b->cv, NULL) != 0) {
+		pthread_mutex_destroy(&b->mu);
+		return free(b), TLSGPU_ENOMEM;
+	}
 	if ((rc = tlsgpu_engine_create(device, &b->e)) != TLSGPU_OK ||
 	    (rc = tlsgpu_sessions_create(b->e, max_conns, &b->t)) != TLSGPU_OK ||
 	    (rc = tlsgpu_host_alloc(b->e, wire_bytes, (void **)&b->wire)) != TLSGPU_OK ||
-	    (rc = tlsgpu_host_alloc(b->e, sizeof(tlsgpu_record) * (size_t)b->rec_cap,
+	    (rc = tlsgpu_host_alloc(b->e, sizeof(tlsgpu_record) * b->nslot * (size_t)b->rec_cap,
 	        (void **)&b->recs)) != TLSGPU_OK ||
-	    (rc = tlsgpu_host_alloc(b->e, 4 * (size_t)b->rec_cap, (void **)&b->status)) != TLSGPU_OK) {
+	    (rc = tlsgpu_host_alloc(b->e, 4 * (size_t)b->nslot * b->rec_cap,
+	        (void **)&b->status)) != TLSGPU_OK) {
 		tlsgpu_ssl_batch_destroy(b);
 		return rc;
 	}
 	b->wire_cap = wire_bytes;
+	if (pthread_create(&b->worker, NULL, gpu_worker, b) != 0) {
+		tlsgpu_ssl_batch_destroy(b);
+		return TLSGPU_ENOMEM;
+	}
+	b->have_worker = 1;
 	b->c = calloc(max_conns, sizeof(*b->c));
 	b->first = calloc(max_conns, sizeof(uint32_t));
 	b->count = calloc(max_conns, sizeof(uint32_t));
@@ -101,6 +171,15 @@ tlsgpu_ssl_batch_destroy(tlsgpu_ssl_batch *b)
 {
 	if (!b)
 		return;
+	if (b->have_worker) {
+		pthread_mutex_lock(&b->mu);
+		b->quit = 1;
+		pthread_cond_broadcast(&b->cv);
+		pthread_mutex_unlock(&b->mu);
+		pthread_join(b->worker, NULL);
+	}
+	pthread_cond_destroy(&b->cv);
+	pthread_mutex_destroy(&b->mu);
 	if (b->c)
 		for (uint32_t i = 0; i < b->cap; i++)
 			free(b->c[i].pend);
@@ -182,44 +261,147 @@ seq_store(unsigned char *q, uint64_t v)
 		q[i] = (unsigned char)v;
 }
 
+/* Deliver group slot s (its open is done): per connection, in record order,
+ * until its first failure; the read sequence advances over every record
+ * opened (a failed one ends the connection's batch). */
+static int
+deliver_group(tlsgpu_ssl_batch *b, uint32_t s, const uint32_t *conns,
+    tlsgpu_ssl_deliver_fn deliver, void *arg, int *conn_status)
+{
+	const struct group *g = &b->g[s];
+	const tlsgpu_record *recs = b->recs + (size_t)s * b->rec_cap;
+	const int32_t *status = b->status + (size_t)s * b->rec_cap;
+	const uint8_t *w = b->wire + (size_t)s * b->slot_cap;
+	int delivered = 0;
+	for (uint32_t i = g->i0; i < g->i1; i++) {
+		if (conn_status[i] == TLSGPU_SSL_NOT_ATTACHED)
+			continue;
+		struct conn *c = &b->c[conns[i]];
+		uint32_t k = 0;
+		for (; k < b->count[i]; k++) {
+			const tlsgpu_record *r = &recs[b->first[i] + k];
+			const int32_t st = status[b->first[i] + k];
+			if (st < 0) {
+				conn_status[i] = TLSGPU_SSL_BAD_RECORD_MAC;
+				break;
+			}
+			if (deliver)
+				deliver(arg, conns[i], c->s, w + r->out_off, (size_t)st);
+			delivered++;
+		}
+		seq_store(c->s->s3->read_sequence, seq_load(c->s->s3->read_sequence) + k);
+	}
+	return delivered;
+}
+
+/* Wait for slot s's open; its status, or TLSGPU_OK when nothing was posted. */
+static int
+wait_slot(tlsgpu_ssl_batch *b, uint32_t s)
+{
+	pthread_mutex_lock(&b->mu);
+	while (!b->done[s])
+		pthread_cond_wait(&b->cv, &b->mu);
+	const int rc = b->rc[s];
+	pthread_mutex_unlock(&b->mu);
+	return rc;
+}
+
 int
 tlsgpu_ssl_batch_read(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
     tlsgpu_ssl_deliver_fn deliver, void *arg, int *conn_status)
 {
-	size_t used = 0;
-	uint32_t nrec = 0;
-	int delivered = 0, rc;
+	int delivered = 0, err = TLSGPU_OK;
 	if (!b || (n && (!conns || !conn_status)))
 		return TLSGPU_EINVAL;
-	const double t0 = now_s();
 	b->t_gather = b->t_open = b->t_deliver = 0;
+	uint32_t s = 0;           /* the slot being gathered */
+	int inflight = -1;        /* the slot whose open is posted or running */
+	b->g[0] = (struct group){0, 0, 0, 0};
+	/* Close the gathered group: wait for the previous open, post this one,
+	 * deliver the previous one while this one runs, move to the other slot. */
+#define CLOSE_GROUP(next_i)                                                           \
+	do {                                                                          \
+		b->g[s].i1 = (next_i);                                                \
+		int prc = TLSGPU_OK;                                                  \
+		if (inflight >= 0)                                                    \
+			prc = wait_slot(b, (uint32_t)inflight);                       \
+		pthread_mutex_lock(&b->mu);                                           \
+		b->done[s] = 0;                                                       \
+		b->posted = (int)s;                                                   \
+		pthread_cond_broadcast(&b->cv);                                       \
+		pthread_mutex_unlock(&b->mu);                                         \
+		if (inflight >= 0) {                                                  \
+			const double td = now_s();                                    \
+			if (prc != TLSGPU_OK) {                                       \
+				if (err == TLSGPU_OK)                                 \
+					err = prc;                                    \
+			} else                                                        \
+				delivered += deliver_group(b, (uint32_t)inflight, conns, \
+				    deliver, arg, conn_status);                       \
+			b->t_deliver += now_s() - td;                                 \
+		}                                                                     \
+		inflight = (int)s;                                                    \
+		if (b->nslot == 2)                                                    \
+			s ^= 1u;                                                      \
+		else {                                                                \
+			const int rc1 = wait_slot(b, s);                              \
+			inflight = -1;                                                \
+			const double td = now_s();                                    \
+			if (rc1 != TLSGPU_OK) {                                       \
+				if (err == TLSGPU_OK)                                 \
+					err = rc1;                                    \
+			} else                                                        \
+				delivered += deliver_group(b, s, conns, deliver, arg, \
+				    conn_status);                                     \
+			b->t_deliver += now_s() - td;                                 \
+		}                                                                     \
+		b->g[s] = (struct group){(next_i), (next_i), 0, 0};                   \
+	} while (0)
+	double tg = now_s();
 	for (uint32_t i = 0; i < n; i++) {
 		const uint32_t id = conns[i];
 		struct conn *c = id < b->cap ? &b->c[id] : NULL;
-		b->first[i] = nrec;
+		b->first[i] = b->g[s].nrec;
 		b->count[i] = 0;
 		conn_status[i] = TLSGPU_SSL_OK;
 		if (!c || !c->attached) {
 			conn_status[i] = TLSGPU_SSL_NOT_ATTACHED;
 			continue;
 		}
+		/* the group is full, or cannot take this connection's kept bytes and
+		 * what its BIO holds (at least one more record): hand it to the GPU
+		 * and gather into the other slot */
+		BIO *rb = SSL_get_rbio(c->s);
+		const size_t pending = (size_t)BIO_ctrl_pending(rb);
+		const size_t want = c->pend_len + (pending > SSL3_RT_MAX_PACKET_SIZE ? pending :
+		    SSL3_RT_MAX_PACKET_SIZE);
+		if (b->g[s].nrec != 0 && (b->g[s].used >= kGroupBytes ||
+		    b->slot_cap - b->g[s].used < want)) {
+			b->t_gather += now_s() - tg;
+			CLOSE_GROUP(i);
+			tg = now_s();
+			b->first[i] = 0;
+		}
+		uint8_t *w = b->wire + (size_t)s * b->slot_cap;
+		tlsgpu_record *recs = b->recs + (size_t)s * b->rec_cap;
+		size_t used = b->g[s].used;
+		uint32_t nrec = b->g[s].nrec;
 		/* 1. gather: the kept partial record, then the BIO's bytes */
 		const size_t start = used;
-		if (c->pend_len > b->wire_cap - used)
+		if (c->pend_len > b->slot_cap - used)
 			continue;  /* no room this call: the connection waits for the next */
-		memcpy(b->wire + used, c->pend, c->pend_len);
+		memcpy(w + used, c->pend, c->pend_len);
 		used += c->pend_len;
 		c->pend_len = 0;
-		BIO *rb = SSL_get_rbio(c->s);
-		for (int k; used < b->wire_cap &&
-		    (k = BIO_read(rb, b->wire + used, (int)(b->wire_cap - used > 1u << 30 ?
-		    1u << 30 : b->wire_cap - used))) > 0;)
+		for (int k; used < b->slot_cap &&
+		    (k = BIO_read(rb, w + used, (int)(b->slot_cap - used > 1u << 30 ?
+		    1u << 30 : b->slot_cap - used))) > 0;)
 			used += (size_t)k;
 		/* 2. frame (ssl3_get_record's header checks) */
 		const uint64_t seq0 = seq_load(c->s->s3->read_sequence);
 		size_t p = start;
 		while (used - p >= SSL3_RT_HEADER_LENGTH) {
-			const uint8_t *h = b->wire + p;
+			const uint8_t *h = w + p;
 			const unsigned type = h[0], version = (unsigned)h[1] << 8 | h[2];
 			const size_t len = (size_t)h[3] << 8 | h[4];
 			if (version != (unsigned)c->s->version) {
@@ -238,7 +420,7 @@ tlsgpu_ssl_batch_read(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
 			}
 			if (nrec == b->rec_cap)
 				break;
-			tlsgpu_record *r = &b->recs[nrec++];
+			tlsgpu_record *r = &recs[nrec++];
 			r->in_off = p + SSL3_RT_HEADER_LENGTH;
 			r->out_off = r->in_off + c->eiv;
 			r->seq = seq0 + b->count[i];
@@ -253,45 +435,36 @@ tlsgpu_ssl_batch_read(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
 		if (rest) {
 			if (rest > SSL3_RT_MAX_PACKET_SIZE) {
 				uint8_t *q = realloc(c->pend, rest);
-				if (!q)
-					return TLSGPU_ENOMEM;
+				if (!q) {
+					err = TLSGPU_ENOMEM;
+					b->g[s].used = p;
+					b->g[s].nrec = nrec;
+					n = i + 1;  /* stop gathering: drain what is posted */
+					break;
+				}
 				c->pend = q;
 			}
-			memcpy(c->pend, b->wire + p, rest);
+			memcpy(c->pend, w + p, rest);
 			c->pend_len = rest;
 		}
-		used = p;
+		b->g[s].used = p;
+		b->g[s].nrec = nrec;
 	}
-	const double t1 = now_s();
-	b->t_gather = t1 - t0;
-	if (nrec == 0)
-		return 0;
-	/* 3. one batch for every connection's records, in place */
-	if ((rc = tlsgpu_open_host(b->t, b->recs, nrec, b->wire, used, b->wire, used,
-	    b->status)) != TLSGPU_OK)
-		return rc;
-	const double t2 = now_s();
-	b->t_open = t2 - t1;
-	/* 4. deliver in record order per connection; the read sequence advances
-	 *    over every record opened (a failed one ends the connection's batch) */
-	for (uint32_t i = 0; i < n; i++) {
-		if (conn_status[i] == TLSGPU_SSL_NOT_ATTACHED)
-			continue;
-		struct conn *c = &b->c[conns[i]];
-		uint32_t k = 0;
-		for (; k < b->count[i]; k++) {
-			const tlsgpu_record *r = &b->recs[b->first[i] + k];
-			const int32_t st = b->status[b->first[i] + k];
-			if (st < 0) {
-				conn_status[i] = TLSGPU_SSL_BAD_RECORD_MAC;
-				break;
-			}
-			if (deliver)
-				deliver(arg, conns[i], c->s, b->wire + r->out_off, (size_t)st);
-			delivered++;
-		}
-		seq_store(c->s->s3->read_sequence, seq_load(c->s->s3->read_sequence) + k);
+	b->t_gather += now_s() - tg;
+	if (b->g[s].nrec != 0)
+		CLOSE_GROUP(n);
+	else
+		b->g[s].i1 = n;  /* positions without records: nothing to open */
+	if (inflight >= 0) {
+		const int rc = wait_slot(b, (uint32_t)inflight);
+		const double td = now_s();
+		if (rc != TLSGPU_OK) {
+			if (err == TLSGPU_OK)
+				err = rc;
+		} else
+			delivered += deliver_group(b, (uint32_t)inflight, conns, deliver, arg, conn_status);
+		b->t_deliver += now_s() - td;
 	}
-	b->t_deliver = now_s() - t2;
-	return delivered;
+#undef CLOSE_GROUP
+	return err != TLSGPU_OK ? err : delivered;
 }

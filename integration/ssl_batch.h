@@ -52,7 +52,9 @@ typedef void (*tlsgpu_ssl_deliver_fn)(void *arg, uint32_t conn, SSL *s, const ui
 #define TLSGPU_SSL_NOT_ATTACHED (-5)
 
 /* A consumer for up to max_conns connections (connection ids 0..max_conns-1)
- * on GPU `device`, with a pinned wire buffer of wire_bytes. */
+ * on GPU `device`, with a pinned wire buffer of wire_bytes (two pipeline
+ * slots of wire_bytes / 2 when that holds 2 records of the largest size
+ * each) and one worker thread that runs the GPU batches. */
 int tlsgpu_ssl_batch_create(int device, uint32_t max_conns, size_t wire_bytes,
     tlsgpu_ssl_batch **out);
 void tlsgpu_ssl_batch_destroy(tlsgpu_ssl_batch *b);
@@ -65,17 +67,22 @@ int tlsgpu_ssl_batch_attach(tlsgpu_ssl_batch *b, uint32_t conn, SSL *s, const ui
     size_t key_len);
 
 /* Read every complete record pending in the read BIOs of conns[0..n) (and any
- * partial record kept from the previous call) and open them in one batch.
- * Returns the number of records delivered, or a negative TLSGPU_E* code;
- * conn_status[i] is TLSGPU_SSL_OK or the first failure of conns[i] (records
- * after a failure are not delivered, the connection's read sequence stops at
- * it, as SSL_read's would).  A record that does not fit into what is left of
- * the wire buffer stays pending in its BIO for the next call. */
+ * partial record kept from the previous call; conns[] distinct) and open
+ * them on the GPU: the connections go in groups of about 16 MiB of wire, one
+ * tlsgpu_open_host per group on the worker thread, while the calling thread
+ * delivers the previous group and reads the BIOs of the next (BIO reads,
+ * delivery and SSL state stay on the calling thread).  Returns the number of
+ * records delivered, or a negative TLSGPU_E* code; conn_status[i] is
+ * TLSGPU_SSL_OK or the first failure of conns[i] (records after a failure are
+ * not delivered, the connection's read sequence stops at it, as SSL_read's
+ * would).  Bytes of one connection beyond a slot stay pending in its BIO for
+ * the next call. */
 int tlsgpu_ssl_batch_read(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
     tlsgpu_ssl_deliver_fn deliver, void *arg, int *conn_status);
 
-/* The last tlsgpu_ssl_batch_read's phases (wall clock, seconds): gather +
- * framing, the GPU batch (tlsgpu_open_host: H2D, kernels, D2H), delivery. */
+/* The last tlsgpu_ssl_batch_read's phases (wall clock, seconds, summed over
+ * its groups, so they overlap): gather + framing, the GPU batches
+ * (tlsgpu_open_host: H2D, kernels, D2H, on the worker), delivery. */
 void tlsgpu_ssl_batch_times(const tlsgpu_ssl_batch *b, double *gather_s, double *open_s,
     double *deliver_s);
 

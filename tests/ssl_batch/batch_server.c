@@ -26,7 +26,7 @@
  * by interposing that one call (the real one runs): a patched record layer
  * would call tlsgpu_ssl_batch_attach there instead.
  *
- * usage: batch_server -p server.pem -c CIPHER -n CONNS [-t K] [-b -r R -l L]
+ * usage: batch_server -p server.pem -c CIPHER -n CONNS [-t K] [-b -r R -l L] [-w BYTES]
  * prints one JSON line; exit status 0 only if every check passed.
  */
 #define _GNU_SOURCE
@@ -213,7 +213,8 @@ main(int argc, char **argv)
 {
 	const char *pem = NULL, *cipher = "ECDHE-RSA-AES128-GCM-SHA256";
 	int nconn = 8, tamper = -1, bench = 0, brec = 8, blen = 16384, o;
-	while ((o = getopt(argc, argv, "p:c:n:t:br:l:")) != -1) {
+	size_t wire_opt = 0;
+	while ((o = getopt(argc, argv, "p:c:n:t:br:l:w:")) != -1) {
 		switch (o) {
 		case 'p': pem = optarg; break;
 		case 'c': cipher = optarg; break;
@@ -222,11 +223,13 @@ main(int argc, char **argv)
 		case 'b': bench = 1; break;
 		case 'r': brec = atoi(optarg); break;
 		case 'l': blen = atoi(optarg); break;
+		case 'w': wire_opt = (size_t)atol(optarg); break;
 		default: return 2;
 		}
 	}
 	if (!pem || nconn < 1) {
-		fprintf(stderr, "usage: %s -p server.pem -c cipher -n conns [-t K] [-b -r R -l L]\n",
+		fprintf(stderr, "usage: %s -p server.pem -c cipher -n conns [-t K] [-b -r R -l L] "
+		    "[-w WIRE_BYTES]\n",
 		    argv[0]);
 		return 2;
 	}
@@ -277,6 +280,8 @@ main(int argc, char **argv)
 	size_t wire = (size_t)nconn * 128 * 1024 + (bench ? (size_t)nconn * brec * (blen + 64) : 0);
 	if (wire < (4u << 20))
 		wire = 4u << 20;
+	if (wire_opt)  /* -w: a small pinned buffer, so one read runs many pipeline groups */
+		wire = wire_opt;
 	if (tlsgpu_ssl_batch_create(0, (uint32_t)nconn, wire, &B) != TLSGPU_OK) {
 		fprintf(stderr, "tlsgpu_ssl_batch_create failed\n");
 		return 1;

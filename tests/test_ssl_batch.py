@@ -61,6 +61,19 @@ def test_batch_read_many_connections(cipher):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cipher", CIPHERS[:3])
+def test_batch_read_pipeline_groups(cipher):
+    """A 512 KiB pinned buffer (two 256 KiB slots) for 64 connections: one
+    read runs ~20 pipeline groups, alternating slots (the GPU open of one group
+    beside the delivery of the previous and the gathering of the next), with
+    the tampered connection in the middle; every byte still equals the
+    client's, and SSL_read carries on after it."""
+    d = _run(["-c", cipher, "-n", 64, "-t", 37, "-w", 512 * 1024])
+    assert d["ok"] == 1 and d["tamper_checked"] == 1, d
+    assert d["batch_records"] == 64 * 11
+
+
+@pytest.mark.gpu
 def test_batch_read_bench_1024_connections():
     """1,024 connections x 8 records of 16 KiB (128 MiB of payload) in one
     batch, against the same wire through SSL_read on one CPU thread."""
