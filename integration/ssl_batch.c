@@ -39,6 +39,8 @@ struct conn {
 	uint32_t eiv;             /* explicit nonce bytes in the fragment (8 for GCM) */
 	uint8_t *pend;            /* partial record kept between calls */
 	size_t pend_len;
+	int wattached;            /* write key installed (session cap + id) */
+	uint32_t weiv, wtag;      /* write side: explicit nonce and tag bytes */
 };
 
 /* wire bytes per group: the pipeline's unit (16 MiB: ~0.4 ms of PCIe each way) */
@@ -61,6 +63,11 @@ struct tlsgpu_ssl_batch {
 	int32_t *status;          /* pinned, rec_cap per slot */
 	uint32_t rec_cap, nslot;
 	uint32_t *first, *count;  /* per position in conns[]: its descriptors in its slot */
+	/* write side (allocated at the first tlsgpu_ssl_batch_attach_write) */
+	uint8_t *w_in, *w_out;    /* pinned, slot_cap each */
+	tlsgpu_record *w_recs;    /* pinned, rec_cap */
+	int32_t *w_status;        /* pinned, rec_cap */
+	uint32_t *w_pos;          /* position in conns[] of each write descriptor */
 	struct group g[2];
 	double t_gather, t_open, t_deliver;  /* the last call's phases, seconds (overlapped) */
 	/* the GPU worker: runs tlsgpu_open_host on one posted slot at a time */
@@ -140,7 +147,7 @@ tlsgpu_ssl_batch_create(int device, uint32_t max_conns, size_t wire_bytes, tlsgp
 		return free(b), TLSGPU_ENOMEM;
 	}
 	if ((rc = tlsgpu_engine_create(device, &b->e)) != TLSGPU_OK ||
-	    (rc = tlsgpu_sessions_create(b->e, max_conns, &b->t)) != TLSGPU_OK ||
+	    (rc = tlsgpu_sessions_create(b->e, 2 * max_conns, &b->t)) != TLSGPU_OK ||
 	    (rc = tlsgpu_host_alloc(b->e, wire_bytes, (void **)&b->wire)) != TLSGPU_OK ||
 	    (rc = tlsgpu_host_alloc(b->e, sizeof(tlsgpu_record) * b->nslot * (size_t)b->rec_cap,
 	        (void **)&b->recs)) != TLSGPU_OK ||
@@ -190,7 +197,16 @@ tlsgpu_ssl_batch_destroy(tlsgpu_ssl_batch *b)
 			tlsgpu_host_free(b->e, b->recs);
 		if (b->status)
 			tlsgpu_host_free(b->e, b->status);
+		if (b->w_in)
+			tlsgpu_host_free(b->e, b->w_in);
+		if (b->w_out)
+			tlsgpu_host_free(b->e, b->w_out);
+		if (b->w_recs)
+			tlsgpu_host_free(b->e, b->w_recs);
+		if (b->w_status)
+			tlsgpu_host_free(b->e, b->w_status);
 	}
+	free(b->w_pos);
 	if (b->t)
 		tlsgpu_sessions_destroy(b->t);
 	if (b->e)
@@ -201,15 +217,15 @@ tlsgpu_ssl_batch_destroy(tlsgpu_ssl_batch *b)
 	free(b);
 }
 
-int
-tlsgpu_ssl_batch_attach(tlsgpu_ssl_batch *b, uint32_t conn, SSL *s, const uint8_t *key,
-    size_t key_len)
+/* Install one direction's key in session `slot` from that direction's record
+ * state (the SSL_AEAD_CTX tls1_change_cipher_state_aead filled). */
+static int
+install_direction(tlsgpu_ssl_batch *b, uint32_t slot, SSL *s, const SSL_AEAD_CTX *a,
+    const uint8_t *key, size_t key_len)
 {
-	const SSL_AEAD_CTX *a;
 	tlsgpu_session_params p;
 	int rc;
-	if (!b || conn >= b->cap || !s || !(a = s->aead_read_ctx) || !key ||
-	    (key_len != 16 && key_len != 32) || a->fixed_nonce_len > 12)
+	if (!a || !key || (key_len != 16 && key_len != 32) || a->fixed_nonce_len > 12)
 		return TLSGPU_EINVAL;
 	memset(&p, 0, sizeof(p));
 	/* the suite from the record layer's nonce layout (t1_enc.c:444-495:
@@ -227,21 +243,58 @@ tlsgpu_ssl_batch_attach(tlsgpu_ssl_batch *b, uint32_t conn, SSL *s, const uint8_
 	memcpy(p.fixed_iv, a->fixed_nonce, a->fixed_nonce_len);
 	p.tag_len = a->tag_len;
 	p.version = (uint16_t)s->version;
-	rc = tlsgpu_sessions_install(b->t, conn, 1, &p);
+	rc = tlsgpu_sessions_install(b->t, slot, 1, &p);
 	explicit_bzero(&p, sizeof(p));
 	if (rc != TLSGPU_OK)
 		return rc;
-	{
-		const void *owner = s;  /* TaLoS read hook: the record's SSL* */
-		if ((rc = tlsgpu_sessions_set_owner(b->t, conn, 1, &owner)) != TLSGPU_OK)
-			return rc;
-	}
+	const void *owner = s;  /* TaLoS read / write hooks: the record's SSL* */
+	return tlsgpu_sessions_set_owner(b->t, slot, 1, &owner);
+}
+
+int
+tlsgpu_ssl_batch_attach(tlsgpu_ssl_batch *b, uint32_t conn, SSL *s, const uint8_t *key,
+    size_t key_len)
+{
+	int rc;
+	if (!b || conn >= b->cap || !s)
+		return TLSGPU_EINVAL;
+	const SSL_AEAD_CTX *a = s->aead_read_ctx;
+	if ((rc = install_direction(b, conn, s, a, key, key_len)) != TLSGPU_OK)
+		return rc;
 	if (!b->c[conn].pend && !(b->c[conn].pend = malloc(SSL3_RT_MAX_PACKET_SIZE)))
 		return TLSGPU_ENOMEM;
 	b->c[conn].s = s;
 	b->c[conn].attached = 1;
 	b->c[conn].eiv = a->variable_nonce_in_record ? 8u : 0u;
 	b->c[conn].pend_len = 0;
+	return TLSGPU_OK;
+}
+
+int
+tlsgpu_ssl_batch_attach_write(tlsgpu_ssl_batch *b, uint32_t conn, SSL *s, const uint8_t *key,
+    size_t key_len)
+{
+	int rc;
+	if (!b || conn >= b->cap || !s)
+		return TLSGPU_EINVAL;
+	const SSL_AEAD_CTX *a = s->aead_write_ctx;
+	if (!b->w_in) {  /* the write side's buffers, once */
+		if ((rc = tlsgpu_host_alloc(b->e, b->slot_cap, (void **)&b->w_in)) != TLSGPU_OK ||
+		    (rc = tlsgpu_host_alloc(b->e, b->slot_cap, (void **)&b->w_out)) != TLSGPU_OK ||
+		    (rc = tlsgpu_host_alloc(b->e, sizeof(tlsgpu_record) * (size_t)b->rec_cap,
+		        (void **)&b->w_recs)) != TLSGPU_OK ||
+		    (rc = tlsgpu_host_alloc(b->e, 4 * (size_t)b->rec_cap,
+		        (void **)&b->w_status)) != TLSGPU_OK)
+			return rc;
+		if (!(b->w_pos = malloc(sizeof(uint32_t) * (size_t)b->rec_cap)))
+			return TLSGPU_ENOMEM;
+	}
+	if ((rc = install_direction(b, b->cap + conn, s, a, key, key_len)) != TLSGPU_OK)
+		return rc;
+	b->c[conn].s = s;
+	b->c[conn].wattached = 1;
+	b->c[conn].weiv = a->variable_nonce_in_record ? 8u : 0u;
+	b->c[conn].wtag = a->tag_len;
 	return TLSGPU_OK;
 }
 
@@ -467,4 +520,102 @@ tlsgpu_ssl_batch_read(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
 	}
 #undef CLOSE_GROUP
 	return err != TLSGPU_OK ? err : delivered;
+}
+
+/* Seal the write group in w_recs[0..nrec) and hand each record to its
+ * connection's write BIO with do_ssl3_write's header; write_sequence += the
+ * records written.  Returns the records written, or a negative TLSGPU_E*. */
+static int
+write_group(tlsgpu_ssl_batch *b, uint32_t nrec, size_t in_used, size_t out_used,
+    const uint32_t *conns, int *conn_status)
+{
+	int rc, written = 0;
+	if ((rc = tlsgpu_seal_host(b->t, b->w_recs, nrec, b->w_in, in_used, b->w_out, out_used,
+	    b->w_status)) != TLSGPU_OK)
+		return rc;
+	for (uint32_t r = 0; r < nrec; r++) {
+		const uint32_t i = b->w_pos[r];
+		if (conn_status[i] != TLSGPU_SSL_OK)
+			continue;  /* an earlier record of this connection failed */
+		struct conn *c = &b->c[conns[i]];
+		const int32_t st = b->w_status[r];
+		if (st < 0) {
+			conn_status[i] = TLSGPU_SSL_WRITE_FAILED;
+			continue;
+		}
+		/* the 5-byte header in front of the fragment (s3_pkt.c:662-677, 733) */
+		uint8_t *h = b->w_out + b->w_recs[r].out_off - SSL3_RT_HEADER_LENGTH;
+		h[0] = SSL3_RT_APPLICATION_DATA;
+		h[1] = (uint8_t)(c->s->version >> 8);
+		h[2] = (uint8_t)c->s->version;
+		h[3] = (uint8_t)(st >> 8);
+		h[4] = (uint8_t)st;
+		const int len = SSL3_RT_HEADER_LENGTH + st;
+		if (BIO_write(SSL_get_wbio(c->s), h, len) != len) {
+			conn_status[i] = TLSGPU_SSL_WRITE_FAILED;
+			continue;
+		}
+		seq_store(c->s->s3->write_sequence, seq_load(c->s->s3->write_sequence) + 1);
+		written++;
+	}
+	return written;
+}
+
+int
+tlsgpu_ssl_batch_write(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
+    const uint8_t *const *data, const size_t *len, int *conn_status)
+{
+	if (!b || (n && (!conns || !data || !len || !conn_status)))
+		return TLSGPU_EINVAL;
+	int total = 0;
+	for (uint32_t i = 0; i < n; i++) {
+		const uint32_t id = conns[i];
+		conn_status[i] = id < b->cap && b->c[id].wattached ? TLSGPU_SSL_OK :
+		    TLSGPU_SSL_NOT_ATTACHED;
+	}
+	uint32_t i = 0;
+	size_t off = 0;  /* bytes of conns[i]'s data already framed */
+	while (i < n) {
+		/* frame records (do_ssl3_write: fragments of at most
+		 * SSL3_RT_MAX_PLAIN_LENGTH, s3_pkt.c:531-536) until a buffer fills */
+		size_t in_used = 0, out_used = 0;
+		uint32_t nrec = 0, k = 0, kpos = n;
+		uint64_t seq0 = 0;
+		while (i < n) {
+			if (conn_status[i] != TLSGPU_SSL_OK || off == len[i]) {
+				i++, off = 0;  /* not attached, or done (a zero-length write sends nothing) */
+				continue;
+			}
+			const struct conn *c = &b->c[conns[i]];
+			const size_t frag = len[i] - off > SSL3_RT_MAX_PLAIN_LENGTH ?
+			    SSL3_RT_MAX_PLAIN_LENGTH : len[i] - off;
+			const size_t need = SSL3_RT_HEADER_LENGTH + c->weiv + frag + c->wtag;
+			if (in_used + frag > b->slot_cap || out_used + need > b->slot_cap ||
+			    nrec == b->rec_cap)
+				break;
+			if (kpos != i) {  /* this connection's first record in the group */
+				kpos = i;
+				k = 0;
+				seq0 = seq_load(c->s->s3->write_sequence);
+			}
+			memcpy(b->w_in + in_used, data[i] + off, frag);
+			tlsgpu_record *r = &b->w_recs[nrec];
+			r->in_off = in_used;
+			r->out_off = out_used + SSL3_RT_HEADER_LENGTH;
+			r->seq = seq0 + k++;
+			r->session = b->cap + conns[i];
+			r->len_type = TLSGPU_LEN_TYPE(frag, SSL3_RT_APPLICATION_DATA);
+			b->w_pos[nrec++] = i;
+			in_used += frag;
+			out_used += need;
+			off += frag;
+		}
+		if (nrec == 0)
+			break;  /* nothing framed: every remaining connection is done */
+		const int w = write_group(b, nrec, in_used, out_used, conns, conn_status);
+		if (w < 0)
+			return w;
+		total += w;
+	}
+	return total;
 }

@@ -50,6 +50,7 @@ typedef void (*tlsgpu_ssl_deliver_fn)(void *arg, uint32_t conn, SSL *s, const ui
 #define TLSGPU_SSL_RECORD_OVERFLOW (-3)  /* SSL_AD_RECORD_OVERFLOW */
 #define TLSGPU_SSL_NOT_APP_DATA (-4)     /* a non-application-data record: SSL_read's job */
 #define TLSGPU_SSL_NOT_ATTACHED (-5)
+#define TLSGPU_SSL_WRITE_FAILED (-6)     /* a seal status < 0, or the write BIO refused bytes */
 
 /* A consumer for up to max_conns connections (connection ids 0..max_conns-1)
  * on GPU `device`, with a pinned wire buffer of wire_bytes (two pipeline
@@ -79,6 +80,24 @@ int tlsgpu_ssl_batch_attach(tlsgpu_ssl_batch *b, uint32_t conn, SSL *s, const ui
  * the next call. */
 int tlsgpu_ssl_batch_read(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
     tlsgpu_ssl_deliver_fn deliver, void *arg, int *conn_status);
+
+/* After ChangeCipherSpec on the write side: install connection `conn`'s write
+ * key (the key tls1_change_cipher_state_aead hands to EVP_AEAD_CTX_init for
+ * s->aead_write_ctx) on the GPU. */
+int tlsgpu_ssl_batch_attach_write(tlsgpu_ssl_batch *b, uint32_t conn, SSL *s,
+    const uint8_t *key, size_t key_len);
+
+/* SSL_write for many connections at once: data[i] (len[i] bytes) of conns[i]
+ * (distinct) is cut into records of at most SSL3_RT_MAX_PLAIN_LENGTH
+ * (ssl3_write_bytes / do_ssl3_write, s3_pkt.c:501-762), sealed on the GPU in
+ * tlsgpu_seal_host batches, and written to each connection's write BIO with
+ * the record header, in order; s3->write_sequence advances once per record
+ * (tls1_enc(s, 1), t1_enc.c:258-266), so SSL_write keeps working after it.
+ * Returns the records written, or a negative TLSGPU_E* code; conn_status[i]
+ * is TLSGPU_SSL_OK, TLSGPU_SSL_NOT_ATTACHED or TLSGPU_SSL_WRITE_FAILED (the
+ * connection's records stop at the failure). */
+int tlsgpu_ssl_batch_write(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
+    const uint8_t *const *data, const size_t *len, int *conn_status);
 
 /* The last tlsgpu_ssl_batch_read's phases (wall clock, seconds, summed over
  * its groups, so they overlap): gather + framing, the GPU batches

@@ -13,7 +13,11 @@
  *            (the reference's CPU record layer): the SSL objects are still
  *            consistent after the batch (read_sequence advanced as tls1_enc
  *            would have);
- *   phase 3  (-t K) one bit of connection K's next record is flipped on the
+ *   phase 4  the server writes every connection in one
+ *            tlsgpu_ssl_batch_write (records cut, GPU-sealed, framed into the
+ *            write BIOs) and every client reads it with SSL_read; phase 5:
+ *            the server's own SSL_write after it, read by the clients;
+ *   phase 3  (-t K, after 4 and 5) one bit of connection K's next record is flipped on the
  *            wire: the batch reports K as bad_record_mac, every other
  *            connection is delivered;
  *   -b       bench: after the checks, R records of L bytes per connection,
@@ -342,6 +346,83 @@ main(int argc, char **argv)
 		free(buf);
 		free(exp[i]);
 	}
+	/* phase 4: the server writes every connection in one call
+	 * (tlsgpu_ssl_batch_write: records cut, sealed on the GPU, framed into
+	 * each write BIO); every client reads with the reference's SSL_read.
+	 * Phase 5: the server's own SSL_write on the same SSL objects, read by
+	 * the clients (write_sequence stayed consistent). */
+	long records4 = -1;
+	int write_ok = -1;
+	if (ok) {
+		write_ok = 1;
+		for (int i = 0; i < nconn; i++) {
+			const struct keyrec *k = key_of(&P[i].s->aead_write_ctx->ctx);
+			if (!k || tlsgpu_ssl_batch_attach_write(B, (uint32_t)i, P[i].s, k->key,
+			    k->len) != TLSGPU_OK) {
+				fprintf(stderr, "attach_write %d failed\n", i);
+				return 1;
+			}
+		}
+		const uint8_t **wd = calloc(nconn, sizeof(*wd));
+		size_t *wl = calloc(nconn, sizeof(size_t));
+		int *wst = calloc(nconn, sizeof(int));
+		for (int i = 0; i < nconn; i++) {
+			/* 0 B, single records, the 16 KiB edges, multi-record writes */
+			wl[i] = i % 9 == 4 ? 0 : (size_t)lens[i % NLENS] * (1 + i % 3) + (size_t)(i % 5);
+			unsigned char *d = malloc(wl[i] + 1);
+			fill(d, (long)wl[i], ((uint64_t)4 << 48) | (uint64_t)i);
+			wd[i] = d;
+		}
+		records4 = tlsgpu_ssl_batch_write(B, ids, (uint32_t)nconn, wd, wl, wst);
+		for (int i = 0; i < nconn && write_ok; i++) {
+			if (records4 < 0 || wst[i] != TLSGPU_SSL_OK || pump(P[i].s_out, P[i].c_in) < 0) {
+				fprintf(stderr, "phase 4: connection %d: rc %ld status %d\n", i, records4, wst[i]);
+				write_ok = 0;
+				break;
+			}
+			unsigned char *buf = malloc(wl[i] + 1);
+			size_t got = 0;
+			while (got < wl[i]) {
+				int rc = SSL_read(P[i].c, buf + got, (int)(wl[i] - got));
+				if (rc <= 0) {
+					fprintf(stderr, "phase 4: client %d SSL_read returned %d after %zu of %zu\n",
+					    i, rc, got, wl[i]);
+					ERR_print_errors_fp(stderr);
+					write_ok = 0;
+					break;
+				}
+				got += (size_t)rc;
+			}
+			if (write_ok && memcmp(buf, wd[i], wl[i]) != 0) {
+				fprintf(stderr, "phase 4: client %d payload mismatch\n", i);
+				write_ok = 0;
+			}
+			free(buf);
+		}
+		for (int i = 0; i < nconn && write_ok; i++) {  /* phase 5 */
+			unsigned char msg[1400], back[1400];
+			fill(msg, sizeof(msg), ((uint64_t)5 << 48) | (uint64_t)i);
+			int got = 0, rc = 0;
+			if (SSL_write(P[i].s, msg, sizeof(msg)) != (int)sizeof(msg) ||
+			    pump(P[i].s_out, P[i].c_in) < 0)
+				write_ok = 0;
+			while (write_ok && got < (int)sizeof(msg) &&
+			    (rc = SSL_read(P[i].c, back + got, (int)sizeof(msg) - got)) > 0)
+				got += rc;
+			if (!write_ok || got != (int)sizeof(msg) || memcmp(back, msg, sizeof(msg)) != 0) {
+				fprintf(stderr, "phase 5: connection %d: SSL_write / client SSL_read got %d (rc %d)\n",
+				    i, got, rc);
+				ERR_print_errors_fp(stderr);
+				write_ok = 0;
+			}
+		}
+		for (int i = 0; i < nconn; i++)
+			free((void *)wd[i]);
+		free(wd);
+		free(wl);
+		free(wst);
+		ok = ok && write_ok;
+	}
 	/* phase 3: a flipped bit on connection `tamper` */
 	int tamper_ok = -1;
 	if (ok && tamper >= 0 && tamper < nconn) {
@@ -378,8 +459,9 @@ main(int argc, char **argv)
 		ok = ok && tamper_ok;
 	}
 	printf("{\"cipher\": \"%s\", \"conns\": %d, \"batch_records\": %ld, "
-	    "\"ssl_read_records_after\": %ld, \"tamper_checked\": %d", SSL_get_cipher_name(P[0].c),
-	    nconn, records1, records2, tamper_ok);
+	    "\"ssl_read_records_after\": %ld, \"batch_write_records\": %ld, \"write_checked\": %d, "
+	    "\"tamper_checked\": %d", SSL_get_cipher_name(P[0].c),
+	    nconn, records1, records2, records4, write_ok, tamper_ok);
 	/* bench: R records of L bytes per connection (fresh connections' state is
 	 * not needed: the server reads the same wire twice, from two copies) */
 	if (ok && bench) {

@@ -11,7 +11,11 @@ memory BIOs: phase 1 batch-reads every connection's writes (record edges 1 B
 .. 40,000 B); phase 2 reads the next writes with the reference's own SSL_read
 on the same SSL objects (their state stayed consistent); phase 3 flips a bit
 in one connection's record: that one reports bad_record_mac, all others are
-delivered.  Every delivered byte is compared with what the client wrote.
+delivered.  Every delivered byte is compared with what the client wrote.  The
+write side (tlsgpu_ssl_batch_write): the server writes every connection in one
+call — records cut as do_ssl3_write cuts them, sealed on the GPU, framed into
+each write BIO — and every client's reference SSL_read must return exactly the
+bytes written; the server's own SSL_write then still reads back.
 """
 import json
 import os
@@ -25,6 +29,18 @@ HARNESS = os.path.join(ROOT, "tests", "ssl_batch", "_build", "batch_server")
 PEM = os.path.join(ROOT, "tests", "golden", "server.pem")
 CIPHERS = ["ECDHE-RSA-AES128-GCM-SHA256", "ECDHE-RSA-AES256-GCM-SHA384",
            "ECDHE-RSA-CHACHA20-POLY1305", "ECDHE-RSA-CHACHA20-POLY1305-OLD"]
+
+
+HARNESS_LENS = [1, 17, 1400, 16384, 16385, 40000, 5, 4096]  # batch_server.c lens[]
+
+
+def _write_records(nconn):
+    """Records phase 4's tlsgpu_ssl_batch_write cuts (batch_server.c: wl[i])."""
+    n = 0
+    for i in range(nconn):
+        wl = 0 if i % 9 == 4 else HARNESS_LENS[i % 8] * (1 + i % 3) + i % 5
+        n += -(-wl // 16384)
+    return n
 
 
 def _run(args, timeout=240):
@@ -55,6 +71,9 @@ def test_batch_read_many_connections(cipher):
     d = _run(["-c", cipher, "-n", 24, "-t", 5])
     assert d["ok"] == 1 and d["cipher"] == cipher, d
     assert d["conns"] == 24 and d["tamper_checked"] == 1
+    # the write side: one tlsgpu_ssl_batch_write over all 24, read by the
+    # clients' SSL_read, then the server's own SSL_write after it
+    assert d["write_checked"] == 1 and d["batch_write_records"] == _write_records(24)
     # 8 writes per connection: 1 + 1 + 1 + 1 + 2 + 3 + 1 + 1 records
     assert d["batch_records"] == 24 * 11
     assert d["ssl_read_records_after"] >= 24 * 11
@@ -71,6 +90,8 @@ def test_batch_read_pipeline_groups(cipher):
     d = _run(["-c", cipher, "-n", 64, "-t", 37, "-w", 512 * 1024])
     assert d["ok"] == 1 and d["tamper_checked"] == 1, d
     assert d["batch_records"] == 64 * 11
+    # writes through 256 KiB slots: several seal batches in one call
+    assert d["write_checked"] == 1 and d["batch_write_records"] == _write_records(64)
 
 
 @pytest.mark.gpu
