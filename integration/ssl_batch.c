@@ -63,16 +63,24 @@ struct tlsgpu_ssl_batch {
 	int32_t *status;          /* pinned, rec_cap per slot */
 	uint32_t rec_cap, nslot;
 	uint32_t *first, *count;  /* per position in conns[]: its descriptors in its slot */
-	/* write side (allocated at the first tlsgpu_ssl_batch_attach_write) */
-	uint8_t *w_in, *w_out;    /* pinned, slot_cap each */
-	tlsgpu_record *w_recs;    /* pinned, rec_cap */
-	int32_t *w_status;        /* pinned, rec_cap */
+	/* write side (allocated at the first tlsgpu_ssl_batch_attach_write):
+	 * nslot slots of w_cap plaintext in and w_cap wire out, w_rec_cap records */
+	uint8_t *w_in, *w_out;    /* pinned */
+	tlsgpu_record *w_recs;    /* pinned */
+	int32_t *w_status;        /* pinned */
 	uint32_t *w_pos;          /* position in conns[] of each write descriptor */
+	size_t w_cap;
+	uint32_t w_rec_cap;
+	struct wgroup {
+		uint32_t nrec;
+		size_t in_used, out_used;
+	} wg[2];
 	struct group g[2];
 	double t_gather, t_open, t_deliver;  /* the last call's phases, seconds (overlapped) */
 	/* the GPU worker: runs tlsgpu_open_host on one posted slot at a time */
 	pthread_t worker;
-	int have_worker, quit, posted, done[2], rc[2];
+	/* jobs: 0 / 1 = open read slot 0 / 1, 2 / 3 = seal write slot 0 / 1 */
+	int have_worker, quit, posted, done[4], rc[4];
 	pthread_mutex_t mu;
 	pthread_cond_t cv;
 };
@@ -89,19 +97,28 @@ gpu_worker(void *p)
 			pthread_cond_wait(&b->cv, &b->mu);
 		if (b->quit)
 			break;
-		const int s = b->posted;
+		const int j = b->posted;
 		b->posted = -1;
-		const struct group g = b->g[s];
+		const struct group g = b->g[j & 1];
+		const struct wgroup wgj = b->wg[j & 1];
 		pthread_mutex_unlock(&b->mu);
-		uint8_t *w = b->wire + (size_t)s * b->slot_cap;
+		const size_t s = (size_t)(j & 1);
 		const double t0 = now_s();
-		const int rc = tlsgpu_open_host(b->t, b->recs + (size_t)s * b->rec_cap, g.nrec, w, g.used,
-		    w, g.used, b->status + (size_t)s * b->rec_cap);
+		int rc;
+		if (j < 2) {
+			uint8_t *w = b->wire + s * b->slot_cap;
+			rc = tlsgpu_open_host(b->t, b->recs + s * b->rec_cap, g.nrec, w, g.used, w, g.used,
+			    b->status + s * b->rec_cap);
+		} else {
+			rc = tlsgpu_seal_host(b->t, b->w_recs + s * b->w_rec_cap, wgj.nrec,
+			    b->w_in + s * b->w_cap, wgj.in_used, b->w_out + s * b->w_cap, wgj.out_used,
+			    b->w_status + s * b->w_rec_cap);
+		}
 		const double dt = now_s() - t0;
 		pthread_mutex_lock(&b->mu);
 		b->t_open += dt;
-		b->rc[s] = rc;
-		b->done[s] = 1;
+		b->rc[j] = rc;
+		b->done[j] = 1;
 		pthread_cond_broadcast(&b->cv);
 	}
 	pthread_mutex_unlock(&b->mu);
@@ -278,15 +295,18 @@ tlsgpu_ssl_batch_attach_write(tlsgpu_ssl_batch *b, uint32_t conn, SSL *s, const 
 	if (!b || conn >= b->cap || !s)
 		return TLSGPU_EINVAL;
 	const SSL_AEAD_CTX *a = s->aead_write_ctx;
-	if (!b->w_in) {  /* the write side's buffers, once */
-		if ((rc = tlsgpu_host_alloc(b->e, b->slot_cap, (void **)&b->w_in)) != TLSGPU_OK ||
-		    (rc = tlsgpu_host_alloc(b->e, b->slot_cap, (void **)&b->w_out)) != TLSGPU_OK ||
-		    (rc = tlsgpu_host_alloc(b->e, sizeof(tlsgpu_record) * (size_t)b->rec_cap,
+	if (!b->w_in) {  /* the write side's buffers, once: nslot slots of up to 2 groups */
+		b->w_cap = b->slot_cap < 2 * kGroupBytes ? b->slot_cap : 2 * kGroupBytes;
+		b->w_rec_cap = (uint32_t)(b->w_cap / (SSL3_RT_HEADER_LENGTH + 16) + 1);
+		const size_t ns = b->nslot;
+		if ((rc = tlsgpu_host_alloc(b->e, ns * b->w_cap, (void **)&b->w_in)) != TLSGPU_OK ||
+		    (rc = tlsgpu_host_alloc(b->e, ns * b->w_cap, (void **)&b->w_out)) != TLSGPU_OK ||
+		    (rc = tlsgpu_host_alloc(b->e, ns * sizeof(tlsgpu_record) * b->w_rec_cap,
 		        (void **)&b->w_recs)) != TLSGPU_OK ||
-		    (rc = tlsgpu_host_alloc(b->e, 4 * (size_t)b->rec_cap,
+		    (rc = tlsgpu_host_alloc(b->e, ns * 4 * (size_t)b->w_rec_cap,
 		        (void **)&b->w_status)) != TLSGPU_OK)
 			return rc;
-		if (!(b->w_pos = malloc(sizeof(uint32_t) * (size_t)b->rec_cap)))
+		if (!(b->w_pos = malloc(ns * sizeof(uint32_t) * b->w_rec_cap)))
 			return TLSGPU_ENOMEM;
 	}
 	if ((rc = install_direction(b, b->cap + conn, s, a, key, key_len)) != TLSGPU_OK)
@@ -522,40 +542,38 @@ tlsgpu_ssl_batch_read(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
 	return err != TLSGPU_OK ? err : delivered;
 }
 
-/* Seal the write group in w_recs[0..nrec) and hand each record to its
- * connection's write BIO with do_ssl3_write's header; write_sequence += the
- * records written.  Returns the records written, or a negative TLSGPU_E*. */
+/* Hand write slot s's sealed records to their connections' write BIOs with
+ * do_ssl3_write's header (s3_pkt.c:662-677, 733).  Returns the records
+ * written. */
 static int
-write_group(tlsgpu_ssl_batch *b, uint32_t nrec, size_t in_used, size_t out_used,
-    const uint32_t *conns, int *conn_status)
+emit_write_slot(tlsgpu_ssl_batch *b, uint32_t s, const uint32_t *conns, int *conn_status)
 {
-	int rc, written = 0;
-	if ((rc = tlsgpu_seal_host(b->t, b->w_recs, nrec, b->w_in, in_used, b->w_out, out_used,
-	    b->w_status)) != TLSGPU_OK)
-		return rc;
-	for (uint32_t r = 0; r < nrec; r++) {
-		const uint32_t i = b->w_pos[r];
+	const tlsgpu_record *recs = b->w_recs + (size_t)s * b->w_rec_cap;
+	const int32_t *status = b->w_status + (size_t)s * b->w_rec_cap;
+	const uint32_t *pos = b->w_pos + (size_t)s * b->w_rec_cap;
+	uint8_t *out = b->w_out + (size_t)s * b->w_cap;
+	int written = 0;
+	for (uint32_t r = 0; r < b->wg[s].nrec; r++) {
+		const uint32_t i = pos[r];
 		if (conn_status[i] != TLSGPU_SSL_OK)
 			continue;  /* an earlier record of this connection failed */
-		struct conn *c = &b->c[conns[i]];
-		const int32_t st = b->w_status[r];
+		const struct conn *c = &b->c[conns[i]];
+		const int32_t st = status[r];
+		uint8_t *h = out + recs[r].out_off - SSL3_RT_HEADER_LENGTH;
+		const int len = SSL3_RT_HEADER_LENGTH + st;
 		if (st < 0) {
 			conn_status[i] = TLSGPU_SSL_WRITE_FAILED;
 			continue;
 		}
-		/* the 5-byte header in front of the fragment (s3_pkt.c:662-677, 733) */
-		uint8_t *h = b->w_out + b->w_recs[r].out_off - SSL3_RT_HEADER_LENGTH;
 		h[0] = SSL3_RT_APPLICATION_DATA;
 		h[1] = (uint8_t)(c->s->version >> 8);
 		h[2] = (uint8_t)c->s->version;
 		h[3] = (uint8_t)(st >> 8);
 		h[4] = (uint8_t)st;
-		const int len = SSL3_RT_HEADER_LENGTH + st;
 		if (BIO_write(SSL_get_wbio(c->s), h, len) != len) {
 			conn_status[i] = TLSGPU_SSL_WRITE_FAILED;
 			continue;
 		}
-		seq_store(c->s->s3->write_sequence, seq_load(c->s->s3->write_sequence) + 1);
 		written++;
 	}
 	return written;
@@ -567,21 +585,27 @@ tlsgpu_ssl_batch_write(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
 {
 	if (!b || (n && (!conns || !data || !len || !conn_status)))
 		return TLSGPU_EINVAL;
-	int total = 0;
+	int total = 0, err = TLSGPU_OK;
 	for (uint32_t i = 0; i < n; i++) {
 		const uint32_t id = conns[i];
 		conn_status[i] = id < b->cap && b->c[id].wattached ? TLSGPU_SSL_OK :
 		    TLSGPU_SSL_NOT_ATTACHED;
 	}
-	uint32_t i = 0;
-	size_t off = 0;  /* bytes of conns[i]'s data already framed */
+	uint32_t i = 0, s = 0;
+	size_t off = 0;     /* bytes of conns[i]'s data already framed */
+	int inflight = -1;  /* the write slot being sealed */
 	while (i < n) {
 		/* frame records (do_ssl3_write: fragments of at most
-		 * SSL3_RT_MAX_PLAIN_LENGTH, s3_pkt.c:531-536) until a buffer fills */
+		 * SSL3_RT_MAX_PLAIN_LENGTH, s3_pkt.c:531-536) into slot s until it is
+		 * a group's worth or full; each record takes the connection's next
+		 * write sequence number (advanced here, once per record, as
+		 * tls1_enc(s, 1) does: t1_enc.c:258-266) */
+		uint8_t *in = b->w_in + (size_t)s * b->w_cap;
+		tlsgpu_record *recs = b->w_recs + (size_t)s * b->w_rec_cap;
+		uint32_t *pos = b->w_pos + (size_t)s * b->w_rec_cap;
 		size_t in_used = 0, out_used = 0;
-		uint32_t nrec = 0, k = 0, kpos = n;
-		uint64_t seq0 = 0;
-		while (i < n) {
+		uint32_t nrec = 0;
+		while (i < n && in_used < kGroupBytes) {
 			if (conn_status[i] != TLSGPU_SSL_OK || off == len[i]) {
 				i++, off = 0;  /* not attached, or done (a zero-length write sends nothing) */
 				continue;
@@ -590,32 +614,59 @@ tlsgpu_ssl_batch_write(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
 			const size_t frag = len[i] - off > SSL3_RT_MAX_PLAIN_LENGTH ?
 			    SSL3_RT_MAX_PLAIN_LENGTH : len[i] - off;
 			const size_t need = SSL3_RT_HEADER_LENGTH + c->weiv + frag + c->wtag;
-			if (in_used + frag > b->slot_cap || out_used + need > b->slot_cap ||
-			    nrec == b->rec_cap)
+			if (in_used + frag > b->w_cap || out_used + need > b->w_cap ||
+			    nrec == b->w_rec_cap)
 				break;
-			if (kpos != i) {  /* this connection's first record in the group */
-				kpos = i;
-				k = 0;
-				seq0 = seq_load(c->s->s3->write_sequence);
-			}
-			memcpy(b->w_in + in_used, data[i] + off, frag);
-			tlsgpu_record *r = &b->w_recs[nrec];
+			memcpy(in + in_used, data[i] + off, frag);
+			tlsgpu_record *r = &recs[nrec];
+			const uint64_t seq = seq_load(c->s->s3->write_sequence);
+			seq_store(c->s->s3->write_sequence, seq + 1);
 			r->in_off = in_used;
 			r->out_off = out_used + SSL3_RT_HEADER_LENGTH;
-			r->seq = seq0 + k++;
+			r->seq = seq;
 			r->session = b->cap + conns[i];
 			r->len_type = TLSGPU_LEN_TYPE(frag, SSL3_RT_APPLICATION_DATA);
-			b->w_pos[nrec++] = i;
+			pos[nrec++] = i;
 			in_used += frag;
 			out_used += need;
 			off += frag;
 		}
 		if (nrec == 0)
 			break;  /* nothing framed: every remaining connection is done */
-		const int w = write_group(b, nrec, in_used, out_used, conns, conn_status);
-		if (w < 0)
-			return w;
-		total += w;
+		b->wg[s] = (struct wgroup){nrec, in_used, out_used};
+		/* seal this group on the worker while the previous one is written out */
+		int prc = TLSGPU_OK;
+		if (inflight >= 0)
+			prc = wait_slot(b, 2u + (uint32_t)inflight);
+		pthread_mutex_lock(&b->mu);
+		b->done[2 + s] = 0;
+		b->posted = 2 + (int)s;
+		pthread_cond_broadcast(&b->cv);
+		pthread_mutex_unlock(&b->mu);
+		if (inflight >= 0) {
+			if (prc != TLSGPU_OK)
+				err = err != TLSGPU_OK ? err : prc;
+			else
+				total += emit_write_slot(b, (uint32_t)inflight, conns, conn_status);
+		}
+		inflight = (int)s;
+		if (b->nslot == 2)
+			s ^= 1u;
+		else {
+			const int rc1 = wait_slot(b, 2u + s);
+			inflight = -1;
+			if (rc1 != TLSGPU_OK)
+				err = err != TLSGPU_OK ? err : rc1;
+			else
+				total += emit_write_slot(b, s, conns, conn_status);
+		}
 	}
-	return total;
+	if (inflight >= 0) {
+		const int rc = wait_slot(b, 2u + (uint32_t)inflight);
+		if (rc != TLSGPU_OK)
+			err = err != TLSGPU_OK ? err : rc;
+		else
+			total += emit_write_slot(b, (uint32_t)inflight, conns, conn_status);
+	}
+	return err != TLSGPU_OK ? err : total;
 }

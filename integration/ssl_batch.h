@@ -90,11 +90,15 @@ int tlsgpu_ssl_batch_attach_write(tlsgpu_ssl_batch *b, uint32_t conn, SSL *s,
 /* SSL_write for many connections at once: data[i] (len[i] bytes) of conns[i]
  * (distinct) is cut into records of at most SSL3_RT_MAX_PLAIN_LENGTH
  * (ssl3_write_bytes / do_ssl3_write, s3_pkt.c:501-762), sealed on the GPU in
- * tlsgpu_seal_host batches, and written to each connection's write BIO with
- * the record header, in order; s3->write_sequence advances once per record
- * (tls1_enc(s, 1), t1_enc.c:258-266), so SSL_write keeps working after it.
- * Returns the records written, or a negative TLSGPU_E* code; conn_status[i]
- * is TLSGPU_SSL_OK, TLSGPU_SSL_NOT_ATTACHED or TLSGPU_SSL_WRITE_FAILED (the
+ * tlsgpu_seal_host batches of about 16 MiB (sealed on the worker thread while
+ * the calling thread writes the previous batch out and copies in the next),
+ * and written to each connection's write BIO with the record header, in
+ * order; s3->write_sequence advances once per record (tls1_enc(s, 1),
+ * t1_enc.c:258-266), so SSL_write keeps working after it.  The write BIO must
+ * take every byte (a memory BIO, a blocking socket).  Returns the records
+ * written, or a negative TLSGPU_E* code (the connections' state is then
+ * undefined, as after a fatal SSL_write error); conn_status[i] is
+ * TLSGPU_SSL_OK, TLSGPU_SSL_NOT_ATTACHED or TLSGPU_SSL_WRITE_FAILED (the
  * connection's records stop at the failure). */
 int tlsgpu_ssl_batch_write(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
     const uint8_t *const *data, const size_t *len, int *conn_status);

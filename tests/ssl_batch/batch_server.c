@@ -548,6 +548,54 @@ main(int argc, char **argv)
 		    brec, blen, bytes, r, t1 - t0, bytes / (t1 - t0) / 1073741824.0, tg, to, td,
 		    bytes / to / 1073741824.0, t3 - t2,
 		    cbytes / (t3 - t2) / 1073741824.0);
+		/* write bench: R x L bytes to every connection in one
+		 * tlsgpu_ssl_batch_write, against R SSL_write calls per connection on
+		 * one thread (the reference path); the write BIOs are emptied first
+		 * and in between, so both sides append to empty memory BIOs */
+		const size_t wlen = (size_t)brec * blen;
+		unsigned char *big = malloc(wlen);
+		fill(big, (long)wlen, 6);
+		const uint8_t **wd = malloc(sizeof(*wd) * nconn);
+		size_t *wl = malloc(sizeof(size_t) * nconn);
+		int *wst = malloc(sizeof(int) * nconn);
+		for (int i = 0; i < nconn; i++) {
+			wd[i] = big;
+			wl[i] = wlen;
+			/* grow and touch each write BIO's buffer to the wire size first,
+			 * so neither pass pays the memory BIO's growth */
+			const size_t grow = wlen + (size_t)brec * 64;
+			for (size_t w = 0; w < grow; w += (size_t)blen)
+				BIO_write(P[i].s_out, big, (int)(grow - w < (size_t)blen ? grow - w : (size_t)blen));
+			(void)BIO_reset(P[i].s_out);
+		}
+		double w0 = now();
+		const int wr = tlsgpu_ssl_batch_write(B, bids, (uint32_t)nb, wd, wl, wst);
+		double w1 = now();
+		long wbytes = 0;
+		for (int i = 0; i < nb; i++) {
+			if (wst[i] != TLSGPU_SSL_OK)
+				ok = 0;
+			wbytes += (long)BIO_ctrl_pending(P[bids[i]].s_out);
+			(void)BIO_reset(P[bids[i]].s_out);
+		}
+		double w2 = now();
+		long cw = 0;
+		for (int i = 0; i < nb; i++)
+			for (int k = 0; k < brec; k++)
+				cw += SSL_write(P[bids[i]].s, big + (size_t)k * blen, blen) == blen ? blen : 0;
+		double w3 = now();
+		if (wr != nb * brec || cw != bytes)
+			ok = 0;
+		printf(", \"write_bench\": {\"batch_records\": %d, \"wire_bytes\": %ld, \"batch_s\": %.6f, "
+		    "\"batch_GiBps\": %.3f, \"ssl_write_cpu1_s\": %.6f, \"ssl_write_cpu1_GiBps\": %.3f, "
+		    "\"timing\": \"wall clock: tlsgpu_ssl_batch_write (copy in + pinned H2D + seal + D2H + "
+		    "header + BIO_write) vs SSL_write on one thread, payload GiB/s\"}",
+		    wr, wbytes, w1 - w0, bytes / (w1 - w0) / 1073741824.0, w3 - w2,
+		    bytes / (w3 - w2) / 1073741824.0);
+		free(big);
+		free(wd);
+		free(wl);
+		free(wst);
 		free(msg);
 	}
 	printf(", \"ok\": %d}\n", ok);
