@@ -17,7 +17,10 @@
  *            tlsgpu_ssl_batch_write (records cut, GPU-sealed, framed into the
  *            write BIOs) and every client reads it with SSL_read; phase 5:
  *            the server's own SSL_write after it, read by the clients;
- *   phase 3  (-t K, after 4 and 5) one bit of connection K's next record is flipped on the
+ *   phase 6  every connection's wire cut at an arbitrary byte and fed in
+ *            two parts, one batch read after each (partial records kept
+ *            across calls);
+ *   phase 3  (-t K, after 4-6) one bit of connection K's next record is flipped on the
  *            wire: the batch reports K as bad_record_mac, every other
  *            connection is delivered;
  *   -b       bench: after the checks, R records of L bytes per connection,
@@ -193,8 +196,17 @@ handshake(struct pair *P)
 static const long lens[] = {1, 17, 1400, 16384, 16385, 40000, 5, 4096};
 #define NLENS ((int)(sizeof(lens) / sizeof(lens[0])))
 
+static long client_writes_to(struct pair *P, int i, int ph, unsigned char **exp, int pump_it);
+
 static long
 client_writes(struct pair *P, int i, int ph, unsigned char **exp)
+{
+	return client_writes_to(P, i, ph, exp, 1);
+}
+
+/* the client's writes; pump_it = 0 leaves the wire in the client's out BIO */
+static long
+client_writes_to(struct pair *P, int i, int ph, unsigned char **exp, int pump_it)
 {
 	long total = 0, off = 0;
 	for (int k = 0; k < NLENS; k++)
@@ -207,7 +219,7 @@ client_writes(struct pair *P, int i, int ph, unsigned char **exp)
 			return -1;
 		off += n;
 	}
-	if (pump(P->c_out, P->s_in) < 0)
+	if (pump_it && pump(P->c_out, P->s_in) < 0)
 		return -1;
 	return total;
 }
@@ -423,6 +435,52 @@ main(int argc, char **argv)
 		free(wst);
 		ok = ok && write_ok;
 	}
+	/* phase 6: every connection's wire cut at an arbitrary byte (inside a
+	 * header, a fragment or a tag) and fed in two parts, one batch read
+	 * after each: the partial record kept by the first read completes in
+	 * the second, and the bytes delivered over both equal the writes */
+	int split_ok = -1;
+	if (ok) {
+		split_ok = 1;
+		unsigned char **rest = calloc(nconn, sizeof(*rest));
+		long *rest_len = calloc(nconn, sizeof(long));
+		for (int i = 0; i < nconn; i++) {
+			if ((explen[i] = client_writes_to(&P[i], i, 6, &exp[i], 0)) < 0)
+				return 1;
+			long wl = (long)BIO_ctrl_pending(P[i].c_out);
+			unsigned char *w = malloc(wl + 1);
+			if (BIO_read(P[i].c_out, w, (int)wl) != wl)
+				return 1;
+			const long cut = (long)(((uint64_t)i * 7919u + 13u) % (uint64_t)(wl + 1));
+			BIO_write(P[i].s_in, w, (int)cut);
+			rest_len[i] = wl - cut;
+			rest[i] = malloc(rest_len[i] + 1);
+			memcpy(rest[i], w + cut, rest_len[i]);
+			free(w);
+		}
+		int r1 = tlsgpu_ssl_batch_read(B, ids, (uint32_t)nconn, on_deliver, P, st);
+		for (int i = 0; i < nconn && r1 >= 0; i++) {
+			if (st[i] != TLSGPU_SSL_OK)
+				r1 = -1000 - i;
+			BIO_write(P[i].s_in, rest[i], (int)rest_len[i]);
+		}
+		int r2 = r1 < 0 ? -1 : tlsgpu_ssl_batch_read(B, ids, (uint32_t)nconn, on_deliver, P, st);
+		for (int i = 0; i < nconn; i++) {
+			if (r1 < 0 || r2 < 0 || st[i] != TLSGPU_SSL_OK || P[i].got_len != explen[i] ||
+			    memcmp(P[i].got, exp[i], explen[i]) != 0) {
+				if (split_ok)
+					fprintf(stderr, "phase 6: connection %d: rc %d / %d status %d got %ld of %ld\n",
+					    i, r1, r2, st[i], P[i].got_len, explen[i]);
+				split_ok = 0;
+			}
+			P[i].got_len = 0;
+			free(exp[i]);
+			free(rest[i]);
+		}
+		free(rest);
+		free(rest_len);
+		ok = ok && split_ok;
+	}
 	/* phase 3: a flipped bit on connection `tamper` */
 	int tamper_ok = -1;
 	if (ok && tamper >= 0 && tamper < nconn) {
@@ -460,8 +518,8 @@ main(int argc, char **argv)
 	}
 	printf("{\"cipher\": \"%s\", \"conns\": %d, \"batch_records\": %ld, "
 	    "\"ssl_read_records_after\": %ld, \"batch_write_records\": %ld, \"write_checked\": %d, "
-	    "\"tamper_checked\": %d", SSL_get_cipher_name(P[0].c),
-	    nconn, records1, records2, records4, write_ok, tamper_ok);
+	    "\"split_checked\": %d, \"tamper_checked\": %d", SSL_get_cipher_name(P[0].c),
+	    nconn, records1, records2, records4, write_ok, split_ok, tamper_ok);
 	/* bench: R records of L bytes per connection (fresh connections' state is
 	 * not needed: the server reads the same wire twice, from two copies) */
 	if (ok && bench) {

@@ -15,7 +15,9 @@ delivered.  Every delivered byte is compared with what the client wrote.  The
 write side (tlsgpu_ssl_batch_write): the server writes every connection in one
 call — records cut as do_ssl3_write cuts them, sealed on the GPU, framed into
 each write BIO — and every client's reference SSL_read must return exactly the
-bytes written; the server's own SSL_write then still reads back.
+bytes written; the server's own SSL_write then still reads back.  Every
+connection's wire cut at an arbitrary byte and read in two batch calls: the
+partial record the first keeps completes in the second.
 """
 import json
 import os
@@ -74,6 +76,8 @@ def test_batch_read_many_connections(cipher):
     # the write side: one tlsgpu_ssl_batch_write over all 24, read by the
     # clients' SSL_read, then the server's own SSL_write after it
     assert d["write_checked"] == 1 and d["batch_write_records"] == _write_records(24)
+    # records cut across two reads at arbitrary bytes complete in the second
+    assert d["split_checked"] == 1
     # 8 writes per connection: 1 + 1 + 1 + 1 + 2 + 3 + 1 + 1 records
     assert d["batch_records"] == 24 * 11
     assert d["ssl_read_records_after"] >= 24 * 11
@@ -92,6 +96,7 @@ def test_batch_read_pipeline_groups(cipher):
     assert d["batch_records"] == 64 * 11
     # writes through 256 KiB slots: several seal batches in one call
     assert d["write_checked"] == 1 and d["batch_write_records"] == _write_records(64)
+    assert d["split_checked"] == 1
 
 
 @pytest.mark.gpu
