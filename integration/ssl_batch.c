@@ -337,10 +337,24 @@ seq_store(unsigned char *q, uint64_t v)
 /* Deliver group slot s (its open is done): per connection, in record order,
  * until its first failure; the read sequence advances over every record
  * opened (a failed one ends the connection's batch). */
+/* What a finished slot needs: the call's connections and statuses, and the
+ * read side's delivery callback. */
+struct finish_ctx {
+	const uint32_t *conns;
+	int *conn_status;
+	tlsgpu_ssl_deliver_fn deliver;
+	void *arg;
+	int total;   /* records delivered / written */
+	int err;     /* the first GPU job error */
+};
+typedef int (*finish_fn)(tlsgpu_ssl_batch *b, uint32_t s, struct finish_ctx *f);
+
 static int
-deliver_group(tlsgpu_ssl_batch *b, uint32_t s, const uint32_t *conns,
-    tlsgpu_ssl_deliver_fn deliver, void *arg, int *conn_status)
+deliver_group(tlsgpu_ssl_batch *b, uint32_t s, struct finish_ctx *f)
 {
+	const uint32_t *conns = f->conns;
+	int *conn_status = f->conn_status;
+	const double t0 = now_s();
 	const struct group *g = &b->g[s];
 	const tlsgpu_record *recs = b->recs + (size_t)s * b->rec_cap;
 	const int32_t *status = b->status + (size_t)s * b->rec_cap;
@@ -358,12 +372,13 @@ deliver_group(tlsgpu_ssl_batch *b, uint32_t s, const uint32_t *conns,
 				conn_status[i] = TLSGPU_SSL_BAD_RECORD_MAC;
 				break;
 			}
-			if (deliver)
-				deliver(arg, conns[i], c->s, w + r->out_off, (size_t)st);
+			if (f->deliver)
+				f->deliver(f->arg, conns[i], c->s, w + r->out_off, (size_t)st);
 			delivered++;
 		}
 		seq_store(c->s->s3->read_sequence, seq_load(c->s->s3->read_sequence) + k);
 	}
+	b->t_deliver += now_s() - t0;
 	return delivered;
 }
 
@@ -379,57 +394,76 @@ wait_slot(tlsgpu_ssl_batch *b, uint32_t s)
 	return rc;
 }
 
+/* The two-slot pipeline, shared by reads (worker jobs 0 / 1) and writes
+ * (jobs 2 / 3): slot `s` is being filled on the calling thread while slot
+ * `inflight` is on the GPU. */
+struct pipe {
+	uint32_t s;
+	int inflight;
+};
+
+static void
+post_job(tlsgpu_ssl_batch *b, int j)
+{
+	pthread_mutex_lock(&b->mu);
+	b->done[j] = 0;
+	b->posted = j;
+	pthread_cond_broadcast(&b->cv);
+	pthread_mutex_unlock(&b->mu);
+}
+
+static void
+pipe_finish(tlsgpu_ssl_batch *b, uint32_t slot, int rc, finish_fn fin, struct finish_ctx *f)
+{
+	if (rc != TLSGPU_OK) {
+		if (f->err == TLSGPU_OK)
+			f->err = rc;
+	} else
+		f->total += fin(b, slot, f);
+}
+
+/* Hand the filled slot to the worker, finish the previous one while it runs,
+ * and move to the other slot (one slot: run it and finish it in turn). */
+static void
+pipe_close(tlsgpu_ssl_batch *b, struct pipe *p, int base, finish_fn fin, struct finish_ctx *f)
+{
+	int prc = TLSGPU_OK;
+	if (p->inflight >= 0)
+		prc = wait_slot(b, (uint32_t)(base + p->inflight));
+	post_job(b, base + (int)p->s);
+	if (p->inflight >= 0)
+		pipe_finish(b, (uint32_t)p->inflight, prc, fin, f);
+	p->inflight = (int)p->s;
+	if (b->nslot == 2) {
+		p->s ^= 1u;
+	} else {
+		const int rc = wait_slot(b, (uint32_t)base + p->s);
+		p->inflight = -1;
+		pipe_finish(b, p->s, rc, fin, f);
+	}
+}
+
+static void
+pipe_drain(tlsgpu_ssl_batch *b, struct pipe *p, int base, finish_fn fin, struct finish_ctx *f)
+{
+	if (p->inflight >= 0) {
+		const int rc = wait_slot(b, (uint32_t)(base + p->inflight));
+		pipe_finish(b, (uint32_t)p->inflight, rc, fin, f);
+		p->inflight = -1;
+	}
+}
+
 int
 tlsgpu_ssl_batch_read(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
     tlsgpu_ssl_deliver_fn deliver, void *arg, int *conn_status)
 {
-	int delivered = 0, err = TLSGPU_OK;
 	if (!b || (n && (!conns || !conn_status)))
 		return TLSGPU_EINVAL;
 	b->t_gather = b->t_open = b->t_deliver = 0;
-	uint32_t s = 0;           /* the slot being gathered */
-	int inflight = -1;        /* the slot whose open is posted or running */
+	struct finish_ctx f = {conns, conn_status, deliver, arg, 0, TLSGPU_OK};
+	struct pipe pp = {0, -1};
+	uint32_t s = 0;  /* pp.s: the slot being gathered */
 	b->g[0] = (struct group){0, 0, 0, 0};
-	/* Close the gathered group: wait for the previous open, post this one,
-	 * deliver the previous one while this one runs, move to the other slot. */
-#define CLOSE_GROUP(next_i)                                                           \
-	do {                                                                          \
-		b->g[s].i1 = (next_i);                                                \
-		int prc = TLSGPU_OK;                                                  \
-		if (inflight >= 0)                                                    \
-			prc = wait_slot(b, (uint32_t)inflight);                       \
-		pthread_mutex_lock(&b->mu);                                           \
-		b->done[s] = 0;                                                       \
-		b->posted = (int)s;                                                   \
-		pthread_cond_broadcast(&b->cv);                                       \
-		pthread_mutex_unlock(&b->mu);                                         \
-		if (inflight >= 0) {                                                  \
-			const double td = now_s();                                    \
-			if (prc != TLSGPU_OK) {                                       \
-				if (err == TLSGPU_OK)                                 \
-					err = prc;                                    \
-			} else                                                        \
-				delivered += deliver_group(b, (uint32_t)inflight, conns, \
-				    deliver, arg, conn_status);                       \
-			b->t_deliver += now_s() - td;                                 \
-		}                                                                     \
-		inflight = (int)s;                                                    \
-		if (b->nslot == 2)                                                    \
-			s ^= 1u;                                                      \
-		else {                                                                \
-			const int rc1 = wait_slot(b, s);                              \
-			inflight = -1;                                                \
-			const double td = now_s();                                    \
-			if (rc1 != TLSGPU_OK) {                                       \
-				if (err == TLSGPU_OK)                                 \
-					err = rc1;                                    \
-			} else                                                        \
-				delivered += deliver_group(b, s, conns, deliver, arg, \
-				    conn_status);                                     \
-			b->t_deliver += now_s() - td;                                 \
-		}                                                                     \
-		b->g[s] = (struct group){(next_i), (next_i), 0, 0};                   \
-	} while (0)
 	double tg = now_s();
 	for (uint32_t i = 0; i < n; i++) {
 		const uint32_t id = conns[i];
@@ -451,7 +485,10 @@ tlsgpu_ssl_batch_read(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
 		if (b->g[s].nrec != 0 && (b->g[s].used >= kGroupBytes ||
 		    b->slot_cap - b->g[s].used < want)) {
 			b->t_gather += now_s() - tg;
-			CLOSE_GROUP(i);
+			b->g[s].i1 = i;
+			pipe_close(b, &pp, 0, deliver_group, &f);
+			s = pp.s;
+			b->g[s] = (struct group){i, i, 0, 0};
 			tg = now_s();
 			b->first[i] = 0;
 		}
@@ -509,7 +546,7 @@ tlsgpu_ssl_batch_read(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
 			if (rest > SSL3_RT_MAX_PACKET_SIZE) {
 				uint8_t *q = realloc(c->pend, rest);
 				if (!q) {
-					err = TLSGPU_ENOMEM;
+					f.err = TLSGPU_ENOMEM;
 					b->g[s].used = p;
 					b->g[s].nrec = nrec;
 					n = i + 1;  /* stop gathering: drain what is posted */
@@ -524,30 +561,21 @@ tlsgpu_ssl_batch_read(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
 		b->g[s].nrec = nrec;
 	}
 	b->t_gather += now_s() - tg;
+	b->g[s].i1 = n;  /* a last group without records has nothing to open */
 	if (b->g[s].nrec != 0)
-		CLOSE_GROUP(n);
-	else
-		b->g[s].i1 = n;  /* positions without records: nothing to open */
-	if (inflight >= 0) {
-		const int rc = wait_slot(b, (uint32_t)inflight);
-		const double td = now_s();
-		if (rc != TLSGPU_OK) {
-			if (err == TLSGPU_OK)
-				err = rc;
-		} else
-			delivered += deliver_group(b, (uint32_t)inflight, conns, deliver, arg, conn_status);
-		b->t_deliver += now_s() - td;
-	}
-#undef CLOSE_GROUP
-	return err != TLSGPU_OK ? err : delivered;
+		pipe_close(b, &pp, 0, deliver_group, &f);
+	pipe_drain(b, &pp, 0, deliver_group, &f);
+	return f.err != TLSGPU_OK ? f.err : f.total;
 }
 
 /* Hand write slot s's sealed records to their connections' write BIOs with
  * do_ssl3_write's header (s3_pkt.c:662-677, 733).  Returns the records
  * written. */
 static int
-emit_write_slot(tlsgpu_ssl_batch *b, uint32_t s, const uint32_t *conns, int *conn_status)
+emit_write_slot(tlsgpu_ssl_batch *b, uint32_t s, struct finish_ctx *f)
 {
+	const uint32_t *conns = f->conns;
+	int *conn_status = f->conn_status;
 	const tlsgpu_record *recs = b->w_recs + (size_t)s * b->w_rec_cap;
 	const int32_t *status = b->w_status + (size_t)s * b->w_rec_cap;
 	const uint32_t *pos = b->w_pos + (size_t)s * b->w_rec_cap;
@@ -585,16 +613,17 @@ tlsgpu_ssl_batch_write(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
 {
 	if (!b || (n && (!conns || !data || !len || !conn_status)))
 		return TLSGPU_EINVAL;
-	int total = 0, err = TLSGPU_OK;
 	for (uint32_t i = 0; i < n; i++) {
 		const uint32_t id = conns[i];
 		conn_status[i] = id < b->cap && b->c[id].wattached ? TLSGPU_SSL_OK :
 		    TLSGPU_SSL_NOT_ATTACHED;
 	}
-	uint32_t i = 0, s = 0;
-	size_t off = 0;     /* bytes of conns[i]'s data already framed */
-	int inflight = -1;  /* the write slot being sealed */
+	struct finish_ctx f = {conns, conn_status, NULL, NULL, 0, TLSGPU_OK};
+	struct pipe pp = {0, -1};
+	uint32_t i = 0;
+	size_t off = 0;  /* bytes of conns[i]'s data already framed */
 	while (i < n) {
+		const uint32_t s = pp.s;
 		/* frame records (do_ssl3_write: fragments of at most
 		 * SSL3_RT_MAX_PLAIN_LENGTH, s3_pkt.c:531-536) into slot s until it is
 		 * a group's worth or full; each record takes the connection's next
@@ -634,39 +663,9 @@ tlsgpu_ssl_batch_write(tlsgpu_ssl_batch *b, const uint32_t *conns, uint32_t n,
 		if (nrec == 0)
 			break;  /* nothing framed: every remaining connection is done */
 		b->wg[s] = (struct wgroup){nrec, in_used, out_used};
-		/* seal this group on the worker while the previous one is written out */
-		int prc = TLSGPU_OK;
-		if (inflight >= 0)
-			prc = wait_slot(b, 2u + (uint32_t)inflight);
-		pthread_mutex_lock(&b->mu);
-		b->done[2 + s] = 0;
-		b->posted = 2 + (int)s;
-		pthread_cond_broadcast(&b->cv);
-		pthread_mutex_unlock(&b->mu);
-		if (inflight >= 0) {
-			if (prc != TLSGPU_OK)
-				err = err != TLSGPU_OK ? err : prc;
-			else
-				total += emit_write_slot(b, (uint32_t)inflight, conns, conn_status);
-		}
-		inflight = (int)s;
-		if (b->nslot == 2)
-			s ^= 1u;
-		else {
-			const int rc1 = wait_slot(b, 2u + s);
-			inflight = -1;
-			if (rc1 != TLSGPU_OK)
-				err = err != TLSGPU_OK ? err : rc1;
-			else
-				total += emit_write_slot(b, s, conns, conn_status);
-		}
+		/* sealed on the worker while the previous group is written out */
+		pipe_close(b, &pp, 2, emit_write_slot, &f);
 	}
-	if (inflight >= 0) {
-		const int rc = wait_slot(b, 2u + (uint32_t)inflight);
-		if (rc != TLSGPU_OK)
-			err = err != TLSGPU_OK ? err : rc;
-		else
-			total += emit_write_slot(b, (uint32_t)inflight, conns, conn_status);
-	}
-	return err != TLSGPU_OK ? err : total;
+	pipe_drain(b, &pp, 2, emit_write_slot, &f);
+	return f.err != TLSGPU_OK ? f.err : f.total;
 }
